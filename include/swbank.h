@@ -1,0 +1,150 @@
+/*
+ * swbank.h — C ABI of the MI355X Smith-Waterman score bank (libswbank.so).
+ *
+ * This is the drop-in boundary for the reference's scoring path.  Each entry point
+ * replaces one port group of the ScoreBank hardware (paths relative to the reference repo,
+ * ilirlikalla/Smith-Waterman-FPGA-module) or one call of its C host over libcxl:
+ *
+ *   sw_bank_create / sw_bank_destroy
+ *       ≙ instantiating ScoreBank_v2 (ScoreBank/ScoreBank_v2.v:11-44) + reset; on the CAPI
+ *         host, cxl_afu_open_dev / cxl_afu_attach / cxl_afu_free
+ *         (capi_sample_aligner/software-C,C++/src/main_test.c:342,370,530)
+ *   sw_set_penalties
+ *       ≙ ld_penalties with penalties = {match, mismatch, gap_open, gap_extend}
+ *         (ScoreBank_v2.v:33-34,161; propagated to every PE, ScoringModule_v1.1.v:128-148)
+ *   sw_set_matrix
+ *       ≙ the PE's substitution LUT (SW_ProcessingElement_v1.0.v:119) widened to a full
+ *         alphabet x alphabet matrix (protein mode; not in the reference)
+ *   sw_load_query
+ *       ≙ ld_sequence with the query flag, data_in = {01, ID, LEN, SEQ}
+ *         (ScoreBank_v2.v:101-102,162; ScoreBank_v1_tb.sv:193-197)
+ *   sw_score_batch / sw_score_batch_device
+ *       ≙ streaming target records {10, ID, LEN, SEQ} (ScoreBank_v2.v:164-165,
+ *         ScoreBank_v1_tb.sv:236-266) and collecting results/IDs/vld (ScoreBank_v2.v:39-41).
+ *         Scores come back UNBIASED (the RTL's biased - 2048, ScoreBank_v1_tb.sv:280) and in
+ *         INPUT order (the RTL reports completion order; callers re-keyed by ID).
+ *   sw_best_hit
+ *       ≙ the bank's max / vld_max outputs (ScoreBank_v2.v:42-43, declared but never driven).
+ *   sw_encode_ascii
+ *       ≙ ConvertToBase (ScoreBank_v1_tb.sv:44-52): A=2 G=3 T=0 C=1 (lower case too);
+ *         any other byte -> SW_DNA_N (4), which mismatches every code.
+ *   sw_pack_2bit
+ *       ≙ charTo2bit (capi_sample_aligner/software-C,C++/include/aligner_Header.c:14-47):
+ *         2 bits per base, base i at bits 2*(i%4) of byte i/4 (LSB first), N -> 00.
+ *
+ * Conventions (mirroring the reference host, main_test.c):
+ *   - every call returns sw_status: 0 = SW_OK, negative = error; sw_last_error() gives text.
+ *     The library never prints and never exits.
+ *   - the caller owns every host buffer; the bank owns its device buffers and stream.
+ *   - a bank is not thread-safe; use one bank per host thread (like one AFU context).
+ *   - there is NO CPU fallback: without a usable gfx950 device sw_bank_create fails with
+ *     SW_ERR_NO_DEVICE.
+ */
+#ifndef SWBANK_H
+#define SWBANK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SWBANK_ABI_VERSION 1
+
+typedef int32_t sw_status;
+enum {
+  SW_OK = 0,
+  SW_ERR_ARG = -1,         /* bad argument (NULL pointer, code out of alphabet, ...)      */
+  SW_ERR_NO_DEVICE = -2,   /* no HIP device / not gfx950                                 */
+  SW_ERR_HIP = -3,         /* HIP runtime error (text in sw_last_error)                  */
+  SW_ERR_RANGE = -4,       /* score range of the 16-bit lanes could overflow             */
+  SW_ERR_STATE = -5,       /* penalties or query not loaded yet                          */
+  SW_ERR_NOMEM = -6,       /* host or device allocation failed                           */
+  SW_ERR_IO = -7,          /* file I/O or parse error (FASTA helpers)                    */
+  SW_ERR_UNSUPPORTED = -8  /* configuration not implemented (e.g. query too long)       */
+};
+
+enum { SW_ALPHABET_DNA = 0, SW_ALPHABET_PROTEIN = 1 };
+enum {
+  SW_GAP_MERGED = 0, /* ScoreBank PE: one gap matrix I shared by both directions (default) */
+  SW_GAP_GOTOH = 1   /* separate E/F matrices (ssearch36); equal to MERGED when
+                        2*gap_extend <= min substitution score                           */
+};
+/* DNA codes (ConvertToBase). */
+enum { SW_DNA_T = 0, SW_DNA_C = 1, SW_DNA_A = 2, SW_DNA_G = 3, SW_DNA_N = 4 };
+#define SW_DNA_ALPHA 5
+#define SW_PROTEIN_ALPHA 24 /* ARNDCQEGHILKMFPSTWYVBZX* */
+
+typedef struct sw_config {
+  int32_t device;        /* HIP device ordinal; -1 = current device                       */
+  int32_t alphabet;      /* SW_ALPHABET_*                                                 */
+  int32_t gap_model;     /* SW_GAP_*                                                      */
+  uint32_t max_query_len;/* 0 = library maximum (sw_max_query_len())                      */
+  uint32_t flags;        /* reserved, 0                                                   */
+} sw_config;
+
+typedef struct sw_bank sw_bank;
+
+/* ---- library / device ---------------------------------------------------------------- */
+int32_t sw_abi_version(void);
+const char *sw_status_string(sw_status s);
+int32_t sw_device_count(void);           /* HIP devices visible; 0 when none               */
+uint32_t sw_max_query_len(void);
+sw_status sw_config_default(sw_config *cfg);
+
+/* ---- bank lifecycle (≙ ScoreBank_v2 instance) ------------------------------------------ */
+sw_status sw_bank_create(sw_bank **out, const sw_config *cfg);
+void sw_bank_destroy(sw_bank *bank);
+const char *sw_last_error(const sw_bank *bank);
+
+/* ---- ld_penalties / LUT ---------------------------------------------------------------- */
+sw_status sw_set_penalties(sw_bank *bank, int32_t match, int32_t mismatch, int32_t gap_open,
+                           int32_t gap_extend);
+sw_status sw_set_matrix(sw_bank *bank, const int8_t *matrix, int32_t alpha, int32_t gap_open,
+                        int32_t gap_extend);
+
+/* ---- ld_sequence (query) --------------------------------------------------------------- */
+sw_status sw_load_query(sw_bank *bank, uint64_t id, const uint8_t *codes, uint32_t len);
+
+/* ---- target stream -> scores ----------------------------------------------------------- */
+/* Host buffers, blocking.  Target k = residues[offsets[k] .. offsets[k]+lens[k]) (codes).
+ * scores_out[k] = max local-alignment score of (query, target k). */
+sw_status sw_score_batch(sw_bank *bank, const uint8_t *residues, const uint64_t *offsets,
+                         const uint32_t *lens, size_t n, int32_t *scores_out);
+
+/* Device buffers, asynchronous on `stream` (a hipStream_t; NULL = the bank's stream).
+ * max_len must be >= every lens[k]. d_scores receives int32 scores in input order.
+ * Nothing is copied to or from the host. */
+sw_status sw_score_batch_device(sw_bank *bank, const uint8_t *d_residues,
+                                const uint64_t *d_offsets, const uint32_t *d_lens, size_t n,
+                                uint32_t max_len, int32_t *d_scores, void *stream);
+
+/* Best hit of the last sw_score_batch (≙ max / vld_max): the lowest index with the maximum
+ * score; *best_id = ids ? ids[index] : index. */
+sw_status sw_best_hit(sw_bank *bank, const int32_t *scores, const uint64_t *ids, size_t n,
+                      uint64_t *best_id, int32_t *best_score);
+
+/* ---- profiling (≙ the CAPI AFU's cycle counters, capi_sample_aligner/hdl-verliog/afu.v
+ *      _DEBUGGING_ "calculation #N completed, runtime: C cycles") ------------------------- */
+/* When enabled, every launch is bracketed by hipEvents on the stream it runs on. */
+sw_status sw_bank_set_timing(sw_bank *bank, int32_t enable);
+/* Synchronises on the recorded events and returns the launches and the summed device
+ * milliseconds of the feeder (pack) and score kernels since the previous call. */
+sw_status sw_bank_timing(sw_bank *bank, uint64_t *launches, double *pack_ms, double *score_ms);
+
+/* ---- host-side helpers (no device needed) ---------------------------------------------- */
+/* ASCII -> codes for the alphabet; returns n. */
+size_t sw_encode_ascii(int32_t alphabet, const char *ascii, size_t n, uint8_t *codes);
+/* ASCII DNA -> 2-bit LSB-first packing (charTo2bit); out must hold (n+3)/4 bytes, which are
+ * OR-ed into (caller zeroes them, as the reference host's posix_memalign'd buffer).  */
+size_t sw_pack_2bit(const char *ascii, size_t n, uint8_t *out);
+/* 2-bit packed -> DNA codes (inverse of sw_pack_2bit for A/C/G/T). */
+size_t sw_unpack_2bit(const uint8_t *packed, size_t n, uint8_t *codes);
+/* Fill a substitution matrix: DNA (alpha 5) from match/mismatch, or BLOSUM62 (alpha 24). */
+sw_status sw_fill_matrix(int32_t alphabet, int32_t match, int32_t mismatch, int8_t *matrix);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SWBANK_H */

@@ -1,0 +1,202 @@
+/*
+ * swbank — command-line host for libswbank.so.
+ *
+ * Mirrors the reference's two hosts:
+ *   - the CAPI sample host's flags  -q query -l library  (capi_sample_aligner/software-C,C++/
+ *     src/main_test.c:231-279), without the libcxl/AFU plumbing;
+ *   - the ScoreBank testbench's transcript lines ">name score: S" (ScoreBank/ScoreBank_v1_tb.sv:
+ *     271-285), one per library record, in library order (the RTL printed completion order).
+ *
+ * Usage: swbank -q query.fa -l library.fa [-p match,mismatch,open,extend] [-P] [-g]
+ *               [-d device] [-o out.txt] [-T]
+ *   -p  penalties (default 5,-4,-12,-4: ScoreBank_v1_tb.sv:16-19, data/smith-waterman.py:6-10)
+ *   -P  protein mode (BLOSUM62; -p gives only open,extend)      -g  Gotoh gap model
+ *   -T  testbench transcript format "@     0ns: %10s score: \t%d"
+ * Exit status: 0 ok, 1 usage, 2 I/O, 3 library/device error.
+ */
+#define _POSIX_C_SOURCE 200809L
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "swbank.h"
+
+typedef struct {
+  char **names;
+  char **seqs;
+  size_t n, cap;
+} fasta_t;
+
+static int fasta_push(fasta_t *f, char *name) {
+  if (f->n == f->cap) {
+    size_t nc = f->cap ? 2 * f->cap : 64;
+    char **nn = realloc(f->names, nc * sizeof(char *));
+    char **ns = realloc(f->seqs, nc * sizeof(char *));
+    if (!nn || !ns) return -1;
+    f->names = nn;
+    f->seqs = ns;
+    f->cap = nc;
+  }
+  f->names[f->n] = name;
+  f->seqs[f->n] = calloc(1, 1);
+  if (!f->seqs[f->n]) return -1;
+  f->n++;
+  return 0;
+}
+
+/* '>' starts a record (name = first token); sequence lines are concatenated (the testbench
+ * read exactly one token per record, ScoreBank_v1_tb.sv:185-212; multi-line is a superset). */
+static int read_fasta(const char *path, fasta_t *f) {
+  FILE *fp = fopen(path, "r");
+  if (!fp) return -1;
+  char *line = NULL;
+  size_t cap = 0;
+  ssize_t len;
+  while ((len = getline(&line, &cap, fp)) >= 0) {
+    while (len > 0 && (line[len - 1] == '\n' || line[len - 1] == '\r' || line[len - 1] == ' '))
+      line[--len] = 0;
+    if (len == 0) continue;
+    if (line[0] == '>') {
+      char *p = line + 1;
+      size_t k = strcspn(p, " \t");
+      char *name = strndup(p, k);
+      if (!name || fasta_push(f, name)) goto fail;
+    } else {
+      if (f->n == 0) { /* bare sequence file (the CAPI host's build/query) */
+        char *name = strdup("seq");
+        if (!name || fasta_push(f, name)) goto fail;
+      }
+      char **s = &f->seqs[f->n - 1];
+      size_t old = strlen(*s);
+      char *ns = realloc(*s, old + (size_t)len + 1);
+      if (!ns) goto fail;
+      memcpy(ns + old, line, (size_t)len + 1);
+      *s = ns;
+    }
+  }
+  free(line);
+  fclose(fp);
+  return 0;
+fail:
+  free(line);
+  fclose(fp);
+  return -1;
+}
+
+static void usage(const char *argv0) {
+  fprintf(stderr,
+          "usage: %s -q query.fa -l library.fa [-p match,mismatch,open,extend] [-P] [-g]\n"
+          "          [-d device] [-o out.txt] [-T]\n",
+          argv0);
+}
+
+int main(int argc, char **argv) {
+  const char *qpath = NULL, *lpath = NULL, *opath = NULL, *pen = NULL;
+  int protein = 0, gotoh = 0, device = -1, transcript = 0, opt;
+  while ((opt = getopt(argc, argv, "q:l:p:Pgd:o:Th")) != -1) {
+    switch (opt) {
+      case 'q': qpath = optarg; break;
+      case 'l': lpath = optarg; break;
+      case 'p': pen = optarg; break;
+      case 'P': protein = 1; break;
+      case 'g': gotoh = 1; break;
+      case 'd': device = atoi(optarg); break;
+      case 'o': opath = optarg; break;
+      case 'T': transcript = 1; break;
+      default: usage(argv[0]); return opt == 'h' ? 0 : 1;
+    }
+  }
+  if (!qpath || !lpath) {
+    fprintf(stderr, "Input files missing\n");
+    usage(argv[0]);
+    return 1;
+  }
+  int ma = 5, mm = -4, go = -12, ge = -4;
+  if (protein) {
+    go = -11;
+    ge = -1;
+    if (pen && sscanf(pen, "%d,%d", &go, &ge) != 2) return usage(argv[0]), 1;
+  } else if (pen && sscanf(pen, "%d,%d,%d,%d", &ma, &mm, &go, &ge) != 4) {
+    return usage(argv[0]), 1;
+  }
+
+  fasta_t q = {0}, lib = {0};
+  if (read_fasta(qpath, &q) || q.n == 0) {
+    fprintf(stderr, "Query file error!\n");
+    return 2;
+  }
+  if (read_fasta(lpath, &lib)) {
+    fprintf(stderr, "Database file error!\n");
+    return 2;
+  }
+  const int alphabet = protein ? SW_ALPHABET_PROTEIN : SW_ALPHABET_DNA;
+
+  sw_config cfg;
+  sw_config_default(&cfg);
+  cfg.device = device;
+  cfg.alphabet = alphabet;
+  cfg.gap_model = gotoh ? SW_GAP_GOTOH : SW_GAP_MERGED;
+  sw_bank *bank = NULL;
+  sw_status st = sw_bank_create(&bank, &cfg);
+  if (st != SW_OK) {
+    fprintf(stderr, "swbank: bank create failed: %s\n", sw_status_string(st));
+    return 3;
+  }
+  if (protein) {
+    int8_t m[SW_PROTEIN_ALPHA * SW_PROTEIN_ALPHA];
+    sw_fill_matrix(SW_ALPHABET_PROTEIN, 0, 0, m);
+    st = sw_set_matrix(bank, m, SW_PROTEIN_ALPHA, go, ge);
+  } else {
+    st = sw_set_penalties(bank, ma, mm, go, ge);
+  }
+  size_t qlen = strlen(q.seqs[0]);
+  uint8_t *qc = malloc(qlen + 1);
+  if (st == SW_OK && qc) {
+    sw_encode_ascii(alphabet, q.seqs[0], qlen, qc);
+    st = sw_load_query(bank, 0, qc, (uint32_t)qlen);
+  }
+  size_t total = 0;
+  for (size_t k = 0; k < lib.n; ++k) total += strlen(lib.seqs[k]);
+  uint8_t *res = malloc(total + 1);
+  uint64_t *offs = malloc((lib.n + 1) * sizeof(uint64_t));
+  uint32_t *lens = malloc((lib.n + 1) * sizeof(uint32_t));
+  int32_t *scores = malloc((lib.n + 1) * sizeof(int32_t));
+  if (!res || !offs || !lens || !scores) st = SW_ERR_NOMEM;
+  size_t pos = 0;
+  for (size_t k = 0; st == SW_OK && k < lib.n; ++k) {
+    size_t l = strlen(lib.seqs[k]);
+    sw_encode_ascii(alphabet, lib.seqs[k], l, res + pos);
+    offs[k] = pos;
+    lens[k] = (uint32_t)l;
+    pos += l;
+  }
+  if (st == SW_OK) st = sw_score_batch(bank, res, offs, lens, lib.n, scores);
+  if (st != SW_OK) {
+    fprintf(stderr, "swbank: %s: %s\n", sw_status_string(st), sw_last_error(bank));
+    sw_bank_destroy(bank);
+    return 3;
+  }
+  FILE *out = opath ? fopen(opath, "w") : stdout;
+  if (!out) {
+    sw_bank_destroy(bank);
+    return 2;
+  }
+  for (size_t k = 0; k < lib.n; ++k) {
+    char nm[256];
+    snprintf(nm, sizeof(nm), ">%s", lib.names[k]);
+    if (transcript)
+      fprintf(out, "@%6dns: %10s score: \t%10d\n", 0, nm, scores[k]);
+    else
+      fprintf(out, "%s score: %d\n", nm, scores[k]);
+  }
+  if (opath) fclose(out);
+  sw_bank_destroy(bank);
+  free(qc);
+  free(res);
+  free(offs);
+  free(lens);
+  free(scores);
+  return 0;
+}

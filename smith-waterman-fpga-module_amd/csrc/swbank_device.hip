@@ -1,0 +1,436 @@
+// swbank_device.hip — C-ABI of libswbank.so: the bank object and its device plumbing.
+//
+// Call surface mirrors ScoreBank_v2 (reference ScoreBank/ScoreBank_v2.v:30-44): penalties once,
+// a query once, then any number of target batches; one max score per target.  See
+// include/swbank.h for the per-function reference citations.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "swbank.h"
+#include "swbank_internal.h"
+
+extern "C" int swk_has_variant(int R, int RB);
+extern "C" hipError_t swk_launch_score_dna(int R, int RB, int col0, const uint8_t* res,
+                                           const uint64_t* offs, const uint32_t* lens, size_t n,
+                                           unsigned* queue, const uint32_t* qtab, int W,
+                                           uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
+                                           int32_t* scores, uint32_t max_len, int grid_cap,
+                                           hipStream_t st);
+
+namespace {
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 64);
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), want * sizeof(T));
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+}  // namespace
+
+struct sw_bank {
+  sw_config cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  char err[512] = {0};
+
+  // ld_penalties
+  bool have_pen = false;
+  int alpha = SW_DNA_ALPHA;
+  std::vector<int8_t> matrix;  // alpha x alpha
+  int32_t gap_open = 0, gap_extend = 0;
+
+  // ld_sequence (query)
+  bool have_query = false;
+  uint64_t qid = 0;
+  std::vector<uint8_t> query;
+
+  // derived per (penalties, query)
+  bool dirty = true;
+  int R = 32, RB = 4, W = 1, col0 = 0, grid_cap = 0;
+  uint32_t S = 0, O = 0, E = 0, nv = 0;
+  int32_t smax = 0;
+  DevBuf<uint32_t> qtab;
+  DevBuf<unsigned> queue;  // tile queue head of the persistent score kernel
+
+  // workspaces
+  DevBuf<uint8_t> res;
+  DevBuf<uint64_t> offs;
+  DevBuf<uint32_t> lens;
+  DevBuf<int32_t> scores;
+
+  // profiling
+  bool timing = false;
+  struct Ev { hipEvent_t a, b, c; };
+  std::vector<Ev> events;
+};
+
+static sw_status fail(sw_bank* b, sw_status st, const char* fmt, ...) {
+  if (b) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(b->err, sizeof(b->err), fmt, ap);
+    va_end(ap);
+  }
+  return st;
+}
+
+#define HIPOK(bank, expr)                                                                 \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail((bank), SW_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),    \
+                  __FILE__, __LINE__);                                                    \
+  } while (0)
+
+extern "C" int32_t sw_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+extern "C" sw_status sw_bank_create(sw_bank** out, const sw_config* cfg_in) {
+  if (!out) return SW_ERR_ARG;
+  *out = nullptr;
+  sw_config cfg;
+  if (cfg_in)
+    cfg = *cfg_in;
+  else
+    sw_config_default(&cfg);
+  if (cfg.alphabet != SW_ALPHABET_DNA && cfg.alphabet != SW_ALPHABET_PROTEIN) return SW_ERR_ARG;
+  if (cfg.gap_model != SW_GAP_MERGED && cfg.gap_model != SW_GAP_GOTOH) return SW_ERR_ARG;
+  if (cfg.alphabet != SW_ALPHABET_DNA || cfg.gap_model != SW_GAP_MERGED)
+    return SW_ERR_UNSUPPORTED;  // protein / Gotoh kernels: not in this build
+  if (cfg.max_query_len > SWB_MAX_QUERY) return SW_ERR_UNSUPPORTED;
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SW_ERR_NO_DEVICE;
+  int dev = cfg.device;
+  if (dev < 0) {
+    if (hipGetDevice(&dev) != hipSuccess) return SW_ERR_NO_DEVICE;
+  }
+  if (dev >= ndev) return SW_ERR_NO_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return SW_ERR_NO_DEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SW_ERR_NO_DEVICE;
+
+  sw_bank* b = new (std::nothrow) sw_bank();
+  if (!b) return SW_ERR_NOMEM;
+  b->cfg = cfg;
+  b->device = dev;
+  if (hipSetDevice(dev) != hipSuccess ||
+      hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete b;
+    return SW_ERR_HIP;
+  }
+  b->alpha = SW_DNA_ALPHA;
+  *out = b;
+  return SW_OK;
+}
+
+extern "C" void sw_bank_destroy(sw_bank* b) {
+  if (!b) return;
+  (void)hipSetDevice(b->device);
+  if (b->stream) (void)hipStreamSynchronize(b->stream);
+  uint64_t nl;
+  double pm, sm;
+  (void)sw_bank_timing(b, &nl, &pm, &sm);
+  b->qtab.release();
+  b->queue.release();
+  b->res.release();
+  b->offs.release();
+  b->lens.release();
+  b->scores.release();
+  if (b->stream) (void)hipStreamDestroy(b->stream);
+  delete b;
+}
+
+extern "C" const char* sw_last_error(const sw_bank* b) { return b ? b->err : "null bank"; }
+
+static sw_status set_matrix_impl(sw_bank* b, const int8_t* m, int alpha, int32_t go,
+                                 int32_t ge) {
+  if (go > 0 || ge > 0 || go < -32767 || ge < -32767)
+    return fail(b, SW_ERR_ARG, "gap penalties must be <= 0 (got open %d, extend %d)", go, ge);
+  b->matrix.assign(m, m + (size_t)alpha * alpha);
+  b->alpha = alpha;
+  b->gap_open = go;
+  b->gap_extend = ge;
+  b->have_pen = true;
+  b->dirty = true;
+  return SW_OK;
+}
+
+extern "C" sw_status sw_set_penalties(sw_bank* b, int32_t match, int32_t mismatch,
+                                      int32_t gap_open, int32_t gap_extend) {
+  if (!b) return SW_ERR_ARG;
+  if (b->cfg.alphabet != SW_ALPHABET_DNA)
+    return fail(b, SW_ERR_ARG, "sw_set_penalties needs a DNA bank; use sw_set_matrix");
+  int8_t m[SW_DNA_ALPHA * SW_DNA_ALPHA];
+  if (sw_fill_matrix(SW_ALPHABET_DNA, match, mismatch, m) != SW_OK)
+    return fail(b, SW_ERR_ARG, "match/mismatch outside int8 (%d, %d)", match, mismatch);
+  return set_matrix_impl(b, m, SW_DNA_ALPHA, gap_open, gap_extend);
+}
+
+extern "C" sw_status sw_set_matrix(sw_bank* b, const int8_t* m, int32_t alpha, int32_t gap_open,
+                                   int32_t gap_extend) {
+  if (!b || !m) return SW_ERR_ARG;
+  const int want = b->cfg.alphabet == SW_ALPHABET_DNA ? SW_DNA_ALPHA : SW_PROTEIN_ALPHA;
+  if (alpha != want) return fail(b, SW_ERR_ARG, "matrix alphabet %d, bank expects %d", alpha, want);
+  return set_matrix_impl(b, m, alpha, gap_open, gap_extend);
+}
+
+extern "C" sw_status sw_load_query(sw_bank* b, uint64_t id, const uint8_t* codes, uint32_t len) {
+  if (!b || (!codes && len)) return SW_ERR_ARG;
+  const uint32_t cap = b->cfg.max_query_len ? b->cfg.max_query_len : SWB_MAX_QUERY;
+  if (len > cap)
+    return fail(b, SW_ERR_UNSUPPORTED, "query length %u exceeds the bank maximum %u", len, cap);
+  for (uint32_t i = 0; i < len; ++i)
+    if (codes[i] >= (uint32_t)b->alpha)
+      return fail(b, SW_ERR_ARG, "query code %u at %u outside alphabet %d", codes[i], i, b->alpha);
+  b->query.assign(codes, codes + len);
+  b->qid = id;
+  b->have_query = true;
+  b->dirty = true;
+  return SW_OK;
+}
+
+// Build the per-row LUTs (the PE query registers + penalty registers,
+// ScoringModule_v1.1.v:110-150) for the resident query.
+static sw_status prepare(sw_bank* b) {
+  if (!b->have_pen || !b->have_query)
+    return fail(b, SW_ERR_STATE, "load penalties (ld_penalties) and a query (ld_sequence) first");
+  if (!b->dirty) return SW_OK;
+  const int A = b->alpha;
+  const int8_t* m = b->matrix.data();
+  int smax = -128, smin = 127;
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < A; ++j) {
+      smax = std::max<int>(smax, m[i * A + j]);
+      smin = std::min<int>(smin, m[i * A + j]);
+    }
+  for (int j = 0; j < A; ++j) {  // row N too
+    smax = std::max<int>(smax, m[4 * A + j]);
+    smin = std::min<int>(smin, m[4 * A + j]);
+  }
+  // column N must be uniform per kernel (one shared VGPR for codes 4..7)
+  const int sN = m[0 * A + 4];
+  for (int i = 0; i < A; ++i)
+    if (m[i * A + 4] != sN)
+      return fail(b, SW_ERR_UNSUPPORTED, "DNA kernel needs a uniform N column in the matrix");
+  if (sN > 0) return fail(b, SW_ERR_ARG, "mismatch/N scores must be <= 0");
+  const int S = std::max(0, smax);
+  if (S - smin > 254)
+    return fail(b, SW_ERR_RANGE, "substitution range [%d, %d] exceeds 254", smin, smax);
+  const int o = -b->gap_open, e = -b->gap_extend;
+
+  const int qlen = (int)b->query.size();
+  // Rows per wave: 32 (16 for tiny queries, 64 past 16 waves).  SWBANK_R/C/RB override
+  // (tuning only; must name a compiled variant).
+  int R = qlen <= 16 ? 16 : 32, RB = 4;
+  if ((qlen + R - 1) / R > 16) R = 64;
+  R = env_int("SWBANK_R", R);
+  RB = env_int("SWBANK_RB", RB);
+  if (!swk_has_variant(R, RB))
+    return fail(b, SW_ERR_UNSUPPORTED, "no kernel variant R=%d RB=%d", R, RB);
+  const int W = std::max(1, (qlen + R - 1) / R);
+  if (W * 64 > (R >= 64 ? 512 : 1024))
+    return fail(b, SW_ERR_UNSUPPORTED, "query length %d too long for one bank", qlen);
+
+  std::vector<uint32_t> tab((size_t)W * R, 0xFFFFFFFFu);
+  for (int i = 0; i < qlen; ++i) {
+    uint32_t w = 0;
+    for (int c = 0; c < 4; ++c) w |= (uint32_t)(uint8_t)(S - m[b->query[i] * A + c]) << (8 * c);
+    tab[i] = w;
+  }
+  const uint32_t pN = (uint32_t)(uint8_t)(S - sN);
+  HIPOK(b, hipSetDevice(b->device));
+  HIPOK(b, b->qtab.reserve(tab.size()));
+  HIPOK(b, hipMemcpyAsync(b->qtab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice,
+                          b->stream));
+  HIPOK(b, hipStreamSynchronize(b->stream));
+  b->R = R;
+  b->RB = RB;
+  b->grid_cap = env_int("SWBANK_GRID", 0);
+  b->W = W;
+  b->S = (uint32_t)S;
+  b->O = (uint32_t)o;
+  b->E = (uint32_t)e;
+  b->nv = pN * 0x01010101u;
+  b->smax = smax;
+  // HDL column-0 rule differs from the plain recurrence only if a match can pay for a gap open
+  b->col0 = (smax > o + e) ? 1 : 0;
+  b->dirty = false;
+  return SW_OK;
+}
+
+static sw_status range_check(sw_bank* b, uint32_t max_len) {
+  const uint64_t qlen = b->query.size();
+  const uint64_t cells = std::min<uint64_t>(qlen, max_len);
+  const uint64_t top = cells * (uint64_t)std::max(0, b->smax) + b->S;
+  if (top > 65535u)
+    return fail(b, SW_ERR_RANGE, "max score bound %llu exceeds the 16-bit lanes",
+                (unsigned long long)top);
+  return SW_OK;
+}
+
+static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
+                        const uint32_t* d_lens, size_t n, uint32_t max_len, int32_t* d_scores,
+                        hipStream_t st) {
+  HIPOK(b, b->queue.reserve(16));
+  sw_bank::Ev ev{};
+  if (b->timing) {
+    HIPOK(b, hipEventCreate(&ev.a));
+    HIPOK(b, hipEventCreate(&ev.b));
+    HIPOK(b, hipEventCreate(&ev.c));
+    HIPOK(b, hipEventRecord(ev.a, st));
+  }
+  // no separate feeder kernel any more: the score kernel streams the codes itself, so the
+  // "pack" interval (a..b) is empty and kept only for ABI stability
+  if (b->timing) HIPOK(b, hipEventRecord(ev.b, st));
+  HIPOK(b, swk_launch_score_dna(b->R, b->RB, b->col0, d_res, d_offs, d_lens, n, b->queue.p,
+                                b->qtab.p, b->W, b->nv, b->S, b->O, b->E, d_scores, max_len,
+                                b->grid_cap, st));
+  if (b->timing) {
+    HIPOK(b, hipEventRecord(ev.c, st));
+    b->events.push_back(ev);
+  }
+  return SW_OK;
+}
+
+extern "C" sw_status sw_score_batch_device(sw_bank* b, const uint8_t* d_res,
+                                           const uint64_t* d_offs, const uint32_t* d_lens,
+                                           size_t n, uint32_t max_len, int32_t* d_scores,
+                                           void* stream) {
+  if (!b) return SW_ERR_ARG;
+  if (n == 0) return SW_OK;
+  if (!d_res || !d_offs || !d_lens || !d_scores) return fail(b, SW_ERR_ARG, "null device buffer");
+  sw_status st = prepare(b);
+  if (st != SW_OK) return st;
+  if ((st = range_check(b, max_len)) != SW_OK) return st;
+  HIPOK(b, hipSetDevice(b->device));
+  return launch(b, d_res, d_offs, d_lens, n, max_len, d_scores,
+                stream ? reinterpret_cast<hipStream_t>(stream) : b->stream);
+}
+
+extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const uint64_t* offsets,
+                                    const uint32_t* lens, size_t n, int32_t* scores_out) {
+  if (!b) return SW_ERR_ARG;
+  if (n == 0) return SW_OK;
+  if (!offsets || !lens || !scores_out) return fail(b, SW_ERR_ARG, "null host buffer");
+  sw_status st = prepare(b);
+  if (st != SW_OK) return st;
+
+  // Feeder order: longest targets first so each 128-target tile has similar lengths
+  // (the RTL's PrioEncoder routes to the first free module, ScoreBank_v2.v:142-148).
+  std::vector<uint32_t> order(n);
+  std::iota(order.begin(), order.end(), 0u);
+  std::stable_sort(order.begin(), order.end(),
+                   [&](uint32_t a, uint32_t c) { return lens[a] > lens[c]; });
+  uint32_t max_len = n ? lens[order[0]] : 0;
+  if (max_len && !residues) return fail(b, SW_ERR_ARG, "null residues");
+  if ((st = range_check(b, max_len)) != SW_OK) return st;
+
+  size_t total = 0;
+  for (size_t k = 0; k < n; ++k) total += lens[k];
+  std::vector<uint8_t> hres(std::max<size_t>(total, 1));
+  std::vector<uint64_t> hoffs(n);
+  std::vector<uint32_t> hlens(n);
+  size_t pos = 0;
+  for (size_t k = 0; k < n; ++k) {
+    const uint32_t src = order[k];
+    const uint8_t* p = residues + offsets[src];
+    for (uint32_t j = 0; j < lens[src]; ++j)
+      if (p[j] >= (uint32_t)b->alpha)
+        return fail(b, SW_ERR_ARG, "target %u code %u outside alphabet", src, p[j]);
+    std::memcpy(hres.data() + pos, p, lens[src]);
+    hoffs[k] = pos;
+    hlens[k] = lens[src];
+    pos += lens[src];
+  }
+
+  HIPOK(b, hipSetDevice(b->device));
+  HIPOK(b, b->res.reserve(hres.size()));
+  HIPOK(b, b->offs.reserve(n));
+  HIPOK(b, b->lens.reserve(n));
+  HIPOK(b, b->scores.reserve(n));
+  HIPOK(b, hipMemcpyAsync(b->res.p, hres.data(), hres.size(), hipMemcpyHostToDevice, b->stream));
+  HIPOK(b, hipMemcpyAsync(b->offs.p, hoffs.data(), n * 8, hipMemcpyHostToDevice, b->stream));
+  HIPOK(b, hipMemcpyAsync(b->lens.p, hlens.data(), n * 4, hipMemcpyHostToDevice, b->stream));
+  st = launch(b, b->res.p, b->offs.p, b->lens.p, n, max_len, b->scores.p, b->stream);
+  if (st != SW_OK) return st;
+  std::vector<int32_t> sorted(n);
+  HIPOK(b, hipMemcpyAsync(sorted.data(), b->scores.p, n * 4, hipMemcpyDeviceToHost, b->stream));
+  HIPOK(b, hipStreamSynchronize(b->stream));
+  for (size_t k = 0; k < n; ++k) scores_out[order[k]] = sorted[k];
+  return SW_OK;
+}
+
+extern "C" sw_status sw_bank_set_timing(sw_bank* b, int32_t enable) {
+  if (!b) return SW_ERR_ARG;
+  b->timing = enable != 0;
+  return SW_OK;
+}
+
+extern "C" sw_status sw_bank_timing(sw_bank* b, uint64_t* launches, double* pack_ms,
+                                    double* score_ms) {
+  if (!b) return SW_ERR_ARG;
+  double p = 0, s = 0;
+  uint64_t n = 0;
+  sw_status st = SW_OK;
+  for (auto& ev : b->events) {
+    float t1 = 0, t2 = 0;
+    if (st == SW_OK && hipEventSynchronize(ev.c) == hipSuccess &&
+        hipEventElapsedTime(&t1, ev.a, ev.b) == hipSuccess &&
+        hipEventElapsedTime(&t2, ev.b, ev.c) == hipSuccess) {
+      p += t1;
+      s += t2;
+      ++n;
+    } else {
+      st = fail(b, SW_ERR_HIP, "event timing failed");
+    }
+    (void)hipEventDestroy(ev.a);
+    (void)hipEventDestroy(ev.b);
+    (void)hipEventDestroy(ev.c);
+  }
+  b->events.clear();
+  if (launches) *launches = n;
+  if (pack_ms) *pack_ms = p;
+  if (score_ms) *score_ms = s;
+  return st;
+}
+
+extern "C" sw_status sw_best_hit(sw_bank* b, const int32_t* scores, const uint64_t* ids, size_t n,
+                                 uint64_t* best_id, int32_t* best_score) {
+  if (!scores || !best_id || !best_score || n == 0)
+    return b ? fail(b, SW_ERR_ARG, "sw_best_hit: empty or null input") : SW_ERR_ARG;
+  size_t bi = 0;
+  for (size_t k = 1; k < n; ++k)
+    if (scores[k] > scores[bi]) bi = k;
+  *best_id = ids ? ids[bi] : (uint64_t)bi;
+  *best_score = scores[bi];
+  return SW_OK;
+}

@@ -1,0 +1,14 @@
+/* swbank_internal.h — constants shared by the host helpers and the device code. */
+#ifndef SWBANK_INTERNAL_H
+#define SWBANK_INTERNAL_H
+
+/* Longest query one bank holds resident: 16 waves x 32 rows (or 8 x 64). */
+#define SWB_MAX_QUERY 512u
+/* Targets per workgroup tile: 64 lanes x 2 packed u16 halves (the PE "toggle" pair). */
+#define SWB_TILE 128
+/* Selector byte that reads 0xFF from v_perm_b32 (padding: substitution = S - 255 < 0). */
+#define SWB_SEL_PAD 0x0Du
+/* Selector byte that reads 0x00 from v_perm_b32. */
+#define SWB_SEL_ZERO 0x0Cu
+
+#endif

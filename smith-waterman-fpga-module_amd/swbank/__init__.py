@@ -1,0 +1,259 @@
+"""swbank — Python host over libswbank.so (ctypes), mirroring the reference ScoreBank surface.
+
+The reference's "host" for this path is the ScoreBank testbench (ScoreBank/ScoreBank_v1_tb.sv)
+and the CAPI C host (capi_sample_aligner/software-C,C++/src/main_test.c).  This module keeps
+their order of operations:
+
+    bank = ScoreBank()                                  # ScoreBank_v2 instance + reset
+    bank.set_penalties(5, -4, -12, -4)                  # ld_penalties   (ScoreBank_v2.v:161)
+    bank.load_query(encode("AGGGCG..."))                # ld_sequence q  (ScoreBank_v2.v:162)
+    scores = bank.score_batch(targets)                  # target records -> results/IDs/vld
+
+Everything goes through the C ABI declared in include/swbank.h; there is no Python compute
+path and no CPU fallback: if libswbank.so is missing, or no gfx950 device is present,
+construction raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, Optional, Sequence, Tuple
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("SWBANK_LIB", os.path.join(_PKG, "lib", "libswbank.so"))
+CLI_PATH = os.path.join(_PKG, "bin", "swbank")
+
+OK = 0
+ERR_ARG, ERR_NO_DEVICE, ERR_HIP, ERR_RANGE, ERR_STATE, ERR_NOMEM, ERR_IO, ERR_UNSUPPORTED = \
+    -1, -2, -3, -4, -5, -6, -7, -8
+ALPHABET_DNA, ALPHABET_PROTEIN = 0, 1
+GAP_MERGED, GAP_GOTOH = 0, 1
+DNA_ALPHA, PROTEIN_ALPHA = 5, 24
+
+# Every symbol include/swbank.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "sw_abi_version", "sw_status_string", "sw_device_count", "sw_max_query_len",
+    "sw_config_default", "sw_bank_create", "sw_bank_destroy", "sw_last_error",
+    "sw_set_penalties", "sw_set_matrix", "sw_load_query", "sw_score_batch",
+    "sw_score_batch_device", "sw_best_hit", "sw_encode_ascii", "sw_pack_2bit",
+    "sw_unpack_2bit", "sw_fill_matrix", "sw_bank_set_timing", "sw_bank_timing",
+)
+
+
+class SwbankError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"swbank status {status}: {msg}")
+        self.status = status
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("alphabet", ctypes.c_int32),
+                ("gap_model", ctypes.c_int32), ("max_query_len", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
+
+
+_LIB: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libswbank.so (raises if it has not been built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise SwbankError(ERR_UNSUPPORTED, f"{LIB_PATH} not built (run make in {_PKG})")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (same SONAME). If
+    # torch is imported first, libswbank binds to that copy, so torch tensors and streams can
+    # be handed across the ABI; loading /opt/rocm's copy first would leave torch unable to
+    # initialise its own.  So import torch (when present) before dlopen-ing the library.
+    if os.environ.get("SWBANK_STANDALONE_HIP") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+    L = ctypes.CDLL(LIB_PATH)
+    P, i32, u32, u64, sz = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64,
+                            ctypes.c_size_t)
+    sig = {
+        "sw_abi_version": (i32, []),
+        "sw_status_string": (ctypes.c_char_p, [i32]),
+        "sw_device_count": (i32, []),
+        "sw_max_query_len": (u32, []),
+        "sw_config_default": (i32, [P]),
+        "sw_bank_create": (i32, [ctypes.POINTER(P), P]),
+        "sw_bank_destroy": (None, [P]),
+        "sw_last_error": (ctypes.c_char_p, [P]),
+        "sw_set_penalties": (i32, [P, i32, i32, i32, i32]),
+        "sw_set_matrix": (i32, [P, P, i32, i32, i32]),
+        "sw_load_query": (i32, [P, u64, P, u32]),
+        "sw_score_batch": (i32, [P, P, P, P, sz, P]),
+        "sw_score_batch_device": (i32, [P, P, P, P, sz, u32, P, P]),
+        "sw_best_hit": (i32, [P, P, P, sz, P, P]),
+        "sw_encode_ascii": (sz, [i32, ctypes.c_char_p, sz, P]),
+        "sw_pack_2bit": (sz, [ctypes.c_char_p, sz, P]),
+        "sw_unpack_2bit": (sz, [P, sz, P]),
+        "sw_fill_matrix": (i32, [i32, i32, i32, P]),
+        "sw_bank_set_timing": (i32, [P, i32]),
+        "sw_bank_timing": (i32, [P, P, P, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = L
+    return L
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def status_string(st: int) -> str:
+    return lib().sw_status_string(st).decode()
+
+
+def device_count() -> int:
+    return int(lib().sw_device_count())
+
+
+# ---- host helpers (no device) --------------------------------------------------------------
+def encode(seq: str | bytes, alphabet: int = ALPHABET_DNA) -> np.ndarray:
+    """ASCII -> codes (sw_encode_ascii; ConvertToBase for DNA)."""
+    b = seq.encode() if isinstance(seq, str) else bytes(seq)
+    out = np.zeros(max(len(b), 1), dtype=np.uint8)
+    lib().sw_encode_ascii(alphabet, b, len(b), _p(out))
+    return out[:len(b)]
+
+
+def pack_2bit(seq: str | bytes) -> np.ndarray:
+    """charTo2bit packing (sw_pack_2bit)."""
+    b = seq.encode() if isinstance(seq, str) else bytes(seq)
+    out = np.zeros(max((len(b) + 3) // 4, 1), dtype=np.uint8)
+    lib().sw_pack_2bit(b, len(b), _p(out))
+    return out[:(len(b) + 3) // 4]
+
+
+def unpack_2bit(packed: np.ndarray, n: int) -> np.ndarray:
+    packed = np.ascontiguousarray(packed, dtype=np.uint8)
+    out = np.zeros(max(n, 1), dtype=np.uint8)
+    lib().sw_unpack_2bit(_p(packed), n, _p(out))
+    return out[:n]
+
+
+def fill_matrix(alphabet: int, match: int = 5, mismatch: int = -4) -> np.ndarray:
+    a = DNA_ALPHA if alphabet == ALPHABET_DNA else PROTEIN_ALPHA
+    m = np.zeros((a, a), dtype=np.int8)
+    st = lib().sw_fill_matrix(alphabet, match, mismatch, _p(m))
+    if st != OK:
+        raise SwbankError(st, status_string(st))
+    return m
+
+
+def pack_targets(seqs: Sequence[np.ndarray]) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Concatenate code arrays -> (residues, offsets u64, lens u32)."""
+    lens = np.array([len(s) for s in seqs], dtype=np.uint32)
+    offs = np.zeros(len(seqs), dtype=np.uint64)
+    if len(seqs) > 1:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    res = np.concatenate([np.asarray(s, dtype=np.uint8) for s in seqs]) if len(seqs) else None
+    if res is None or res.size == 0:
+        res = np.zeros(1, dtype=np.uint8)
+    return res, offs, lens
+
+
+# ---- the bank ----------------------------------------------------------------------------
+class ScoreBank:
+    """One ScoreBank_v2 instance on one GPU (sw_bank_create)."""
+
+    def __init__(self, device: int = -1, alphabet: int = ALPHABET_DNA,
+                 gap_model: int = GAP_MERGED, max_query_len: int = 0):
+        L = lib()
+        cfg = _Config()
+        L.sw_config_default(ctypes.byref(cfg))
+        cfg.device, cfg.alphabet, cfg.gap_model, cfg.max_query_len = (
+            device, alphabet, gap_model, max_query_len)
+        h = ctypes.c_void_p()
+        st = L.sw_bank_create(ctypes.byref(h), ctypes.byref(cfg))
+        if st != OK:
+            raise SwbankError(st, status_string(st))
+        self._h = h
+        self.alphabet = alphabet
+        self.gap_model = gap_model
+
+    # errors
+    def _check(self, st: int):
+        if st != OK:
+            raise SwbankError(st, f"{status_string(st)}: {lib().sw_last_error(self._h).decode()}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().sw_bank_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ld_penalties
+    def set_penalties(self, match: int, mismatch: int, gap_open: int, gap_extend: int):
+        self._check(lib().sw_set_penalties(self._h, match, mismatch, gap_open, gap_extend))
+
+    def set_matrix(self, matrix: np.ndarray, gap_open: int, gap_extend: int):
+        m = np.ascontiguousarray(matrix, dtype=np.int8)
+        self._check(lib().sw_set_matrix(self._h, _p(m), m.shape[0], gap_open, gap_extend))
+
+    # ld_sequence (query)
+    def load_query(self, codes: np.ndarray, qid: int = 0):
+        c = np.ascontiguousarray(codes, dtype=np.uint8)
+        buf = c if c.size else np.zeros(1, np.uint8)
+        self._check(lib().sw_load_query(self._h, qid, _p(buf), len(c)))
+
+    # target stream
+    def score_batch(self, residues: np.ndarray, offsets: np.ndarray, lens: np.ndarray) -> np.ndarray:
+        res = np.ascontiguousarray(residues, dtype=np.uint8)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = np.zeros(len(ln), dtype=np.int32)
+        if len(ln) == 0:
+            return out
+        self._check(lib().sw_score_batch(self._h, _p(res), _p(offs), _p(ln), len(ln), _p(out)))
+        return out
+
+    def score_targets(self, seqs: Iterable[np.ndarray]) -> np.ndarray:
+        return self.score_batch(*pack_targets(list(seqs)))
+
+    def score_batch_device(self, d_res: int, d_offs: int, d_lens: int, n: int, max_len: int,
+                           d_scores: int, stream: int = 0):
+        """Device pointers (ints, e.g. torch.Tensor.data_ptr()); async on `stream`."""
+        self._check(lib().sw_score_batch_device(self._h, d_res, d_offs, d_lens, n, max_len,
+                                                d_scores, stream or None))
+
+    def best_hit(self, scores: np.ndarray, ids: Optional[np.ndarray] = None) -> Tuple[int, int]:
+        """ScoreBank max / vld_max: (id of the best target, its score)."""
+        s = np.ascontiguousarray(scores, dtype=np.int32)
+        bid, bsc = ctypes.c_uint64(), ctypes.c_int32()
+        ida = np.ascontiguousarray(ids, dtype=np.uint64) if ids is not None else None
+        self._check(lib().sw_best_hit(self._h, _p(s), _p(ida) if ida is not None else None,
+                                      len(s), ctypes.byref(bid), ctypes.byref(bsc)))
+        return int(bid.value), int(bsc.value)
+
+    # profiling
+    def set_timing(self, enable: bool = True):
+        self._check(lib().sw_bank_set_timing(self._h, 1 if enable else 0))
+
+    def timing(self) -> Tuple[int, float, float]:
+        """(launches, pack_ms, score_ms) accumulated since the previous call."""
+        n, pm, sm = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
+        self._check(lib().sw_bank_timing(self._h, ctypes.byref(n), ctypes.byref(pm),
+                                         ctypes.byref(sm)))
+        return int(n.value), float(pm.value), float(sm.value)

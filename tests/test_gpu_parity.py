@@ -1,0 +1,196 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden vectors and the oracle.
+
+Bar: bit-exact int32 scores.  Every test here runs the product path (libswbank.so on a
+gfx950 device); the oracle is only the checker.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import swbank as S
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+REF = (5, -4, -12, -4)
+
+
+@pytest.fixture(scope="module")
+def bank():
+    b = S.ScoreBank()
+    yield b
+    b.close()
+
+
+def _lib_records(name):
+    return O.read_fasta(O.golden_fasta(name))
+
+
+def test_every_golden_score(bank):
+    """730 HDL transcript + 598 ssearch36 + 1 CAPI scores, keyed by target name."""
+    rows = O.load_ref_scores()
+    bank.set_penalties(*REF)
+    checked = 0
+    for q in sorted({r[2] for r in rows}):
+        bank.load_query(O.encode_dna(_lib_records(q)[0][1]))
+        for lib in sorted({r[1] for r in rows if r[2] == q}):
+            recs = _lib_records(lib)
+            got = dict(zip([n for n, _ in recs],
+                           bank.score_targets([O.encode_dna(s) for _, s in recs])))
+            for src, l, qq, t, s in rows:
+                if l == lib and qq == q:
+                    assert got[t] == s, (src, lib, q, t, s, got[t])
+                    checked += 1
+    assert checked == len(rows) == 1329
+
+
+def test_swalign_control_differs(bank):
+    bank.set_penalties(*REF)
+    bank.load_query(O.encode_dna(_lib_records("query1.fa")[0][1]))
+    recs = dict(_lib_records("data1.fa"))
+    ctrl = O.load_swalign_control()
+    names = sorted(ctrl)
+    got = bank.score_targets([O.encode_dna(recs[n]) for n in names])
+    diff = sorted(n for n, g in zip(names, got) if g != ctrl[n])
+    assert diff == ["db10", "db12", "db13", "db8"]
+
+
+def _random_case(rng, qlen, ntargets, maxlen, alpha=5, p_n=0.02):
+    q = rng.integers(0, 4, qlen, dtype=np.uint8)
+    q[rng.random(qlen) < p_n] = 4
+    seqs = []
+    for _ in range(ntargets):
+        t = rng.integers(0, 4, int(rng.integers(0, maxlen + 1)), dtype=np.uint8)
+        t[rng.random(len(t)) < p_n] = 4
+        seqs.append(t)
+    return q, seqs
+
+
+@pytest.mark.parametrize("params", [REF, (5, -4, -10, -1), (2, -3, -5, -2), (1, -1, -1, -1),
+                                    (20, -4, -2, -1), (3, 0, -6, -1)])
+@pytest.mark.parametrize("qlen", [1, 7, 16, 17, 31, 32, 33, 63, 64, 65, 100, 128, 150, 255, 256,
+                                  300, 512])
+def test_random_vs_oracle(bank, params, qlen):
+    rng = np.random.default_rng(qlen * 1009 + params[0] * 31 + params[3])
+    q, seqs = _random_case(rng, qlen, 300, 260)
+    # homologous targets exercise long gapped alignments
+    for k in range(0, 300, 10):
+        m = q.copy()
+        if len(m):
+            cut = rng.integers(0, len(m) + 1)
+            m = np.concatenate([m[:cut], rng.integers(0, 4, rng.integers(0, 8), dtype=np.uint8),
+                                m[cut + rng.integers(0, 4):]])
+        seqs[k] = m[:300]
+    bank.set_penalties(*params)
+    bank.load_query(q)
+    got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(params[0], params[1]), params[2],
+                         params[3])
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), int(lens[i]), int(got[i]), int(want[i])) for i in bad[:8]]
+
+
+def test_edge_shapes(bank):
+    bank.set_penalties(*REF)
+    bank.load_query(O.encode_dna("ACGT"))
+    # empty batch, empty targets, single-base targets, all-N target
+    assert bank.score_targets([]).size == 0
+    got = bank.score_targets([np.zeros(0, np.uint8), O.encode_dna("A"), O.encode_dna("NNNN"),
+                              O.encode_dna("ACGT")])
+    assert got.tolist() == [0, 5, 0, 20]
+    # empty query scores 0 everywhere
+    bank.load_query(np.zeros(0, np.uint8))
+    assert bank.score_targets([O.encode_dna("ACGT")]).tolist() == [0]
+    # ragged tile tails: n not a multiple of the 128-target tile
+    rng = np.random.default_rng(2)
+    q, seqs = _random_case(rng, 128, 129, 140)
+    bank.load_query(q)
+    got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    assert (got == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
+
+
+def test_errors(bank):
+    bank.set_penalties(*REF)
+    with pytest.raises(S.SwbankError) as e:
+        bank.load_query(np.zeros(S.lib().sw_max_query_len() + 1, np.uint8))
+    assert e.value.status == S.ERR_UNSUPPORTED
+    with pytest.raises(S.SwbankError) as e:
+        bank.load_query(np.array([0, 1, 9], np.uint8))
+    assert e.value.status == S.ERR_ARG
+    with pytest.raises(S.SwbankError) as e:
+        bank.set_penalties(5, -4, 3, -1)
+    assert e.value.status == S.ERR_ARG
+    fresh = S.ScoreBank()
+    with pytest.raises(S.SwbankError) as e:
+        fresh.score_targets([O.encode_dna("ACGT")])
+    assert e.value.status == S.ERR_STATE
+    # a substitution range past the 8-bit LUT is refused, not wrapped
+    fresh.set_penalties(127, -128, -12, -4)
+    fresh.load_query(np.zeros(16, np.uint8))
+    with pytest.raises(S.SwbankError) as e:
+        fresh.score_targets([np.zeros(20, np.uint8)])
+    assert e.value.status == S.ERR_RANGE
+    # the largest DNA scores fit the u16 lanes: 127 * 512 + S
+    fresh.set_penalties(127, -4, -12, -4)
+    fresh.load_query(np.zeros(512, np.uint8))
+    assert fresh.score_targets([np.zeros(600, np.uint8)]).tolist() == [127 * 512]
+    fresh.close()
+
+
+def test_device_api_with_torch_buffers(bank):
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(9)
+    q, seqs = _random_case(rng, 128, 1000, 128, p_n=0.0)
+    res, offs, lens = O.pack_residues(seqs)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    d_sc = torch.full((len(seqs),), -1, dtype=torch.int32, device=dev)
+    bank.set_penalties(*REF)
+    bank.load_query(q)
+    stream = torch.cuda.current_stream()
+    bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), len(seqs),
+                            int(lens.max()), d_sc.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)
+    assert (d_sc.cpu().numpy() == want).all()
+
+
+def test_bench_scale_properties(bank):
+    """query100 x 499*64 synthetic 128-bp targets (the bench's shape at reduced replication):
+    a seeded subset is checked against the oracle, and size-independent properties hold for
+    the whole batch: duplicated targets score identically, scores are permutation-equivariant,
+    and every score is bounded by 5 * min(|q|, |t|)."""
+    q = O.encode_dna(_lib_records("query100.fa")[0][1])
+    n, L = 499 * 64, 128
+    codes = O.random_codes(2024, n * L, 4).reshape(n, L)
+    codes[1::7] = codes[0::7][: len(codes[1::7])]
+    seqs = list(codes)
+    bank.set_penalties(*REF)
+    bank.load_query(q)
+    got = bank.score_targets(seqs)
+    assert (got[1::7] == got[0::7][: len(got[1::7])]).all()
+    perm = np.random.default_rng(4).permutation(n)
+    got_p = bank.score_targets([seqs[i] for i in perm])
+    assert (got_p == got[perm]).all()
+    assert got.min() >= 0 and got.max() <= 5 * L
+    idx = np.random.default_rng(5).choice(n, 2000, replace=False)
+    res, offs, lens = O.pack_residues([seqs[i] for i in idx])
+    assert (got[idx] == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
+
+
+def test_cli_reproduces_transcript():
+    out = subprocess.run([S.CLI_PATH, "-q", O.golden_fasta("query100.fa"), "-l",
+                          O.golden_fasta("data100.fa")], capture_output=True, text=True,
+                         check=True).stdout
+    got = {}
+    for line in out.splitlines():
+        name, _, score = line.partition(" score: ")
+        got[name.lstrip(">")] = int(score)
+    want = {t: s for src, lib, q, t, s in O.load_ref_scores() if lib == "data100.fa"}
+    assert all(got[t] == s for t, s in want.items()) and len(want) == 99
