@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--variants", nargs="*",
-                    default=["32,8,4", "16,8,4", "32,8,2", "32,8,8", "32,16,4", "64,8,4"])
+                    default=["32,4", "16,4", "32,8", "64,4"])
     args = ap.parse_args()
     import torch
 
@@ -52,8 +52,8 @@ def main():
     results = {v: [] for v in args.variants}
     for rnd in range(args.rounds):
         for v in args.variants:
-            R, C, RB = v.split(",")
-            os.environ["SWBANK_R"], os.environ["SWBANK_C"], os.environ["SWBANK_RB"] = R, C, RB
+            R, RB = v.split(",")
+            os.environ["SWBANK_R"], os.environ["SWBANK_RB"] = R, RB
             bank.load_query(q)  # re-prepare with the new variant
             bank.set_timing(False)
             bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,

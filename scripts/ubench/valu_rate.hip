@@ -1,0 +1,80 @@
+// VALU issue-rate microbenchmark for the instructions of the score kernel's inner loop.
+// Each thread runs 8 independent dependency chains (ILP 8) of one instruction kind, so the
+// rate measured is the SIMD issue rate, not latency.  Prints wave-instructions per SIMD per
+// cycle at the measured clock (GRBM-free: uses wall time x 2.4 GHz nominal, and s_memtime
+// ticks per wave for the in-kernel clock).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+#define ITERS 4096
+
+template <int KIND>
+__global__ void __launch_bounds__(256) k(uint32_t* out, uint32_t seed, unsigned long long* ticks) {
+  uint32_t a[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = seed * (threadIdx.x + 1) + i * 77;
+  const uint32_t b = seed ^ 0x00050005u;
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (KIND == 0) {  // v_pk_max_u16
+        u16x2 x = __builtin_bit_cast(u16x2, a[i]), y = __builtin_bit_cast(u16x2, b);
+        a[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y) + (u16x2){1, 1});
+      } else if (KIND == 1) {  // v_max_u32 + v_add_u32
+        a[i] = max(a[i], b) + 1u;
+      } else if (KIND == 2) {  // v_perm_b32 + v_add
+        a[i] = __builtin_amdgcn_perm(b, a[i], 0x0c010c00u) + 1u;
+      } else {  // v_pk_sub_u16 clamp + v_pk_add_u16
+        u16x2 x = __builtin_bit_cast(u16x2, a[i]), y = __builtin_bit_cast(u16x2, b);
+        a[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x, y) + (u16x2){7, 7});
+      }
+    }
+  }
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if (threadIdx.x == 0) atomicAdd(ticks, t1 - t0);
+}
+
+template <int KIND>
+void run(const char* name, int blocks) {
+  uint32_t* out;
+  unsigned long long* ticks;
+  hipMalloc(&out, (size_t)blocks * 256 * 4);
+  hipMalloc(&ticks, 8);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(256), 0, 0, out, 3u, ticks);
+  hipMemset(ticks, 0, 8);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(256), 0, 0, out, 3u, ticks);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  unsigned long long t;
+  hipMemcpy(&t, ticks, 8, hipMemcpyDeviceToHost);
+  const double waves = blocks * 4.0;
+  const double instr = waves * ITERS * 8 * 2;  // 2 VALU per chain step
+  const double simd_cycles = 1024.0 * ms * 1e-3 * 2.4e9;
+  printf("{\"kind\": \"%s\", \"blocks\": %d, \"ms\": %.3f, \"wave_instr_per_simd_cycle_at_2.4GHz\": %.3f, "
+         "\"avg_wave_ticks\": %.0f}\n",
+         name, blocks, ms, instr / simd_cycles, (double)t / blocks);
+  hipFree(out);
+  hipFree(ticks);
+}
+
+int main() {
+  for (int blocks : {1024, 2048, 8192}) {
+    run<0>("v_pk_max_u16+v_pk_add_u16", blocks);
+    run<1>("v_max_u32+v_add_u32", blocks);
+    run<2>("v_perm_b32+v_add_u32", blocks);
+    run<3>("v_pk_sub_u16_clamp+v_pk_add_u16", blocks);
+  }
+  return 0;
+}

@@ -8,13 +8,9 @@
 //                                              wave through an LDS ring (one barrier per C cols)
 //   toggle (2 targets time-shared per PE)   -> 2 targets per lane, one per u16 half of every
 //                                              register, updated together by v_pk_* ops
-//   MODULES + PrioEncoder (ScoreBank_v2.v)  -> persistent workgroups pulling 128-target tiles
-//                                              from a device queue; the chain never drains
-//                                              between tiles (a wave starts tile k+1 the phase
-//                                              after it finishes tile k, like the RTL feeding
-//                                              the next target into a freed module)
+//   MODULES (independent modules per bank)  -> 64 lanes x workgroups: 128 targets per tile
 //   Feeder (SM_Feeder3.v target register)   -> each lane streams its two targets' codes from
-//                                              HBM, one chunk ahead of use
+//                                              HBM (unaligned 8-byte loads), one chunk ahead
 //
 // Cell update (merged gap matrix, SW_ProcessingElement_v1.0.v:119-141,287-291,411-420) in
 // the shifted/clamped form used here (all u16, per half):
@@ -44,7 +40,7 @@ __device__ __forceinline__ u16x2 vsubs(u16x2 a, u16x2 b) {
   return __builtin_elementwise_sub_sat(a, b);
 }
 
-constexpr int kIdRing = 32;  // LDS slots for queued tile ids (> max wave lag in tiles)
+
 
 // One column of R rows for one wave.  ZDOWN: HDL column-0 rule (G passed down = 0).
 // RB: rows per scheduling group (a sched_barrier every RB rows bounds how far the scheduler
@@ -128,38 +124,38 @@ __device__ __forceinline__ void tile_chunks(const Lane2& t, size_t tlo, size_t t
   nfull = (int)(__builtin_amdgcn_readfirstlane(Lmin) / 8);
 }
 
-// Persistent score kernel.  Each workgroup (W waves x R rows = the query) pulls 128-target
-// tiles from *queue until it runs dry.  Wave w processes global chunk g at phase g + w; one
-// __syncthreads per phase orders the LDS ring hand-off wave w -> w+1.
+// Score kernel: one workgroup = one tile of 128 targets x the whole query (W waves x R rows).
+// Wave w processes chunk c (8 columns) at phase c + w; one __syncthreads per phase orders the
+// LDS ring hand-off wave w -> w+1 (the RTL's PE-to-PE registers).
 //   qtab   W*R row LUTs: byte b = S - s(q_i, b) for codes b = 0..3; pad rows 0xFFFFFFFF
 //   nv     4 x (S - s(*, N)) for target codes 4..7
 //   S,O,E  shift (>= max s), -gap_open, -gap_extend
-// LDS: best[(W+1)][128] | ids[32] | done | edge[2][64] | ring[(W-1)][2][8][64] {H~, G}
+// LDS: best[128] | edge[2][64] | ring[(W-1)][2][8][64] {H~, G}
 template <int R, int RB, bool COL0>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024)
     score_dna(const uint8_t* __restrict__ res, const uint64_t* __restrict__ offs,
-              const uint32_t* __restrict__ lens, size_t n, int ntiles,
-              unsigned* __restrict__ queue, const uint32_t* __restrict__ qtab, uint32_t nv,
-              uint32_t S, uint32_t O, uint32_t E, int32_t* __restrict__ scores, int max_phases) {
+              const uint32_t* __restrict__ lens, size_t n, const uint32_t* __restrict__ qtab,
+              uint32_t nv, uint32_t S, uint32_t O, uint32_t E, int32_t* __restrict__ scores) {
   constexpr int C = 8;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int W = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
-  uint32_t* bestsh = smem;                            // (W+1) x 128
-  int* ids = reinterpret_cast<int*>(smem + (W + 1) * SWB_TILE);
-  int* done = ids + kIdRing;
-  uint2* edge = reinterpret_cast<uint2*>(smem + (W + 1) * SWB_TILE + kIdRing + 4);  // 2 x 64
+  uint32_t* bestsh = smem;                                   // 128 words
+  uint2* edge = reinterpret_cast<uint2*>(smem + SWB_TILE);   // 2 x 64: top boundary | sink
   uint2* ring = edge + 128;
 
-  for (int i = threadIdx.x; i < (W + 1) * SWB_TILE; i += blockDim.x) bestsh[i] = 0;
-  if (threadIdx.x < 64) edge[threadIdx.x] = make_uint2(S | (S << 16), 0u);  // row -1: H~=S, G=0
-  if (threadIdx.x == 0) {
-    ids[0] = (int)atomicAdd(queue, 1u);
-    ids[1] = (int)atomicAdd(queue, 1u);
-    *done = 0;
-  }
+  const int tile = blockIdx.x;
+  const size_t tlo = (size_t)tile * SWB_TILE + lane, thi = tlo + 64;
+  const Lane2 cur = lane_targets(res, offs, lens, n, tile, lane);
+  int nch, nfull;
+  tile_chunks(cur, tlo, thi, n, nch, nfull);
 
+  if (wave == 0) {
+    bestsh[lane] = 0;
+    bestsh[lane + 64] = 0;
+    edge[lane] = make_uint2(S | (S << 16), 0u);  // row -1: H~ = S, G = 0
+  }
   // nv in a VGPR so each v_perm_b32 takes its row LUT straight from an SGPR (one scalar
   // operand per VOP3 on gfx950).
   asm volatile("" : "+v"(nv));
@@ -169,24 +165,6 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024)
   const u16x2 S2 = {(unsigned short)S, (unsigned short)S};
   const u16x2 O2 = {(unsigned short)O, (unsigned short)O};
   const u16x2 E2 = {(unsigned short)E, (unsigned short)E};
-  const uint32_t SELC = 0x0C000C00u;
-  __syncthreads();
-
-  // current tile
-  int k = 0;                  // tile sequence index within this workgroup
-  int tile = ids[0];
-  bool finished = tile >= ntiles;
-  Lane2 cur{}, nxt_t{};
-  int nch = 1, nfull = 0, c = 0, nxt_tile = ntiles;
-  size_t tlo = 0, thi = 0;
-  if (!finished) {
-    cur = lane_targets(res, offs, lens, n, tile, lane);
-    tlo = (size_t)tile * SWB_TILE + lane;
-    thi = tlo + 64;
-    tile_chunks(cur, tlo, thi, n, nch, nfull);
-  }
-  uint2 rlo = {0, 0}, rhi = {0, 0};  // raw codes of the chunk to process next
-  if (!finished) load_raw(cur, 0, nfull > 0, rlo, rhi);
 
   u16x2 Hl[R], Gl[R];
 #pragma unroll
@@ -196,30 +174,21 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024)
   }
   u16x2 best = {0, 0};
   u16x2 prevUpH = S2;  // H~(row above, column -1) = S
+  uint2 rlo, rhi;      // raw codes of the next chunk (prefetched one phase ahead)
+  load_raw(cur, 0, nfull > 0, rlo, rhi);
+  __syncthreads();
 
-  for (int ph = 0;; ++ph) {
-    if (!finished && ph >= wave) {
-      // ---- tile start: queue two tiles ahead, learn the next tile ----
-      if (c == 0) {
-        if (wave == 0 && lane == 0) ids[(k + 2) % kIdRing] = (int)atomicAdd(queue, 1u);
-        nxt_tile = ids[(k + 1) % kIdRing];
-        if (nxt_tile < ntiles) nxt_t = lane_targets(res, offs, lens, n, nxt_tile, lane);
-      }
-      // ---- this chunk's raw codes; prefetch the following chunk ----
+  // branch-free hand-off: wave 0 reads the constant top boundary, the last wave writes into a
+  // sink, both with column stride 0 (branches here split the column loop into blocks and LLVM
+  // then sinks the H updates across columns, blowing up register pressure)
+  const int istride = wave > 0 ? 64 : 0, ostride = wave < W - 1 ? 64 : 0;
+  const int nph = nch + W - 1;
+  for (int ph = 0; ph < nph; ++ph) {
+    const int c = ph - wave;
+    if (c >= 0 && c < nch) {
       const uint2 clo = rlo, chi = rhi;
-      int nnch = nch, nnfull = nfull;
-      if (c + 1 < nch) {
-        load_raw(cur, c + 1, c + 1 < nfull, rlo, rhi);
-      } else if (nxt_tile < ntiles) {
-        tile_chunks(nxt_t, (size_t)nxt_tile * SWB_TILE + lane,
-                    (size_t)nxt_tile * SWB_TILE + lane + 64, n, nnch, nnfull);
-        load_raw(nxt_t, 0, nnfull > 0, rlo, rhi);
-      }
-      const int slot = (ph - wave) & 1;  // global chunk parity: writer w and reader w+1 agree
-      // branch-free hand-off: wave 0 reads the constant top boundary {S, 0}, the last wave
-      // writes into a sink; both with column stride 0 (branches here split the column loop
-      // into blocks and LLVM then sinks the H updates, blowing up register pressure)
-      const int istride = wave > 0 ? 64 : 0, ostride = wave < W - 1 ? 64 : 0;
+      if (c + 1 < nch) load_raw(cur, c + 1, c + 1 < nfull, rlo, rhi);
+      const int slot = c & 1;
       const uint2* rin = wave > 0 ? ring + ((size_t)((wave - 1) * 2 + slot) * C) * 64 + lane
                                   : edge + lane;
       uint2* rout = wave < W - 1 ? ring + ((size_t)(wave * 2 + slot) * C) * 64 + lane
@@ -232,9 +201,11 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024)
         if (jj + 1 < C) rv = rin[(jj + 1) * istride];  // one column ahead
         u16x2 diag = prevUpH;
         prevUpH = upH;
+        // selector: byte 0 = code of the low target, byte 2 = code of the high target
         const uint32_t sel = (uint32_t)(jj & 3) | ((uint32_t)(4 + (jj & 3)) << 16) | 0x0C000C00u;
         const uint32_t selw =
-            __builtin_amdgcn_perm(jj < 4 ? chi.x : chi.y, jj < 4 ? clo.x : clo.y, sel) | SELC;
+            __builtin_amdgcn_perm(jj < 4 ? chi.x : chi.y, jj < 4 ? clo.x : clo.y, sel) |
+            0x0C000C00u;
         __builtin_amdgcn_sched_barrier(0);
         if (COL0 && jj == 0 && c == 0)
           column<R, RB, true>(tab, nv, selw, diag, upG, Hl, Gl, best, S2, O2, E2);
@@ -245,79 +216,35 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024)
         asm volatile("" : "+v"(best));
         rout[jj * ostride] = make_uint2(as_u32(Hl[R - 1]), as_u32(upG));
       }
-
-      // ---- tile end: hand in this wave's best; the last wave publishes the scores ----
-      if (++c == nch) {
-        uint32_t* bs = bestsh + (k % (W + 1)) * SWB_TILE;
-        atomicMax(&bs[lane], (uint32_t)best.x);
-        atomicMax(&bs[lane + 64], (uint32_t)best.y);
-        if (wave == W - 1) {
-          const uint32_t blo = bs[lane], bhi = bs[lane + 64];
-          if (tlo < n) scores[tlo] = (int32_t)blo;
-          if (thi < n) scores[thi] = (int32_t)bhi;
-          bs[lane] = 0;
-          bs[lane + 64] = 0;
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          Hl[r] = S2;
-          Gl[r] = (u16x2){0, 0};
-        }
-        best = (u16x2){0, 0};
-        prevUpH = S2;
-        ++k;
-        c = 0;
-        tile = nxt_tile;
-        if (tile < ntiles) {
-          cur = nxt_t;
-          tlo = (size_t)tile * SWB_TILE + lane;
-          thi = tlo + 64;
-          nch = nnch;
-          nfull = nnfull;
-        } else {
-          finished = true;
-          if (wave == W - 1 && lane == 0) *done = 1;
-        }
-      }
-    } else if (finished && wave == W - 1 && ph == 0 && lane == 0) {
-      *done = 1;  // this workgroup got no tile at all
     }
     __syncthreads();
-    if (*done || ph >= max_phases) break;  // max_phases: host bound, never reached when correct
+  }
+
+  atomicMax(&bestsh[lane], (uint32_t)best.x);
+  atomicMax(&bestsh[lane + 64], (uint32_t)best.y);
+  __syncthreads();
+  if (wave == 0) {
+    if (tlo < n) scores[tlo] = (int32_t)bestsh[lane];
+    if (thi < n) scores[thi] = (int32_t)bestsh[lane + 64];
   }
 }
 
 template <int R, int RB, bool COL0>
 static hipError_t launch_score(const uint8_t* res, const uint64_t* offs, const uint32_t* lens,
-                               size_t n, unsigned* queue, const uint32_t* qtab, int W,
-                               uint32_t nv, uint32_t S, uint32_t O, uint32_t E, int32_t* scores,
-                               uint32_t max_len, int grid_cap, hipStream_t st) {
-  const int ntiles = (int)((n + SWB_TILE - 1) / SWB_TILE);
-  const long long mp = (long long)ntiles * (max_len / 8 + 1) + W + 2;
-  const int max_phases = mp > 0x7fffffff ? 0x7fffffff : (int)mp;
-  const size_t lds = ((size_t)(W + 1) * SWB_TILE + kIdRing + 4) * 4 +
-                     (size_t)(128 + (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8;
+                               size_t n, const uint32_t* qtab, int W, uint32_t nv, uint32_t S,
+                               uint32_t O, uint32_t E, int32_t* scores, hipStream_t st) {
+  const size_t ntiles = (n + SWB_TILE - 1) / SWB_TILE;
+  const size_t lds = SWB_TILE * 4 + (size_t)(128 + (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8;
   auto fn = &score_dna<R, RB, COL0>;
-  static int resident_per_cu[17] = {0};  // by W
-  if (resident_per_cu[W] == 0) {
+  static bool attr_set = false;
+  if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
-    int per_cu = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * W, lds);
-    if (e != hipSuccess) return e;
-    resident_per_cu[W] = per_cu > 0 ? per_cu : 1;
+    attr_set = true;
   }
-  int dev = 0, cus = 256;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  int grid = cus * resident_per_cu[W];
-  if (grid_cap > 0 && grid > grid_cap) grid = grid_cap;
-  if (grid > ntiles) grid = ntiles;
-  hipError_t e = hipMemsetAsync(queue, 0, 16, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(64 * W), (unsigned)lds, st, res, offs, lens,
-                     n, ntiles, queue, qtab, nv, S, O, E, scores, max_phases);
+  hipLaunchKernelGGL(fn, dim3((unsigned)ntiles), dim3(64 * W), (unsigned)lds, st, res, offs,
+                     lens, n, qtab, nv, S, O, E, scores);
   return hipGetLastError();
 }
 
@@ -346,12 +273,15 @@ extern "C" hipError_t swk_launch_score_dna(int R, int RB, int col0, const uint8_
                                            int32_t* scores, uint32_t max_len, int grid_cap,
                                            hipStream_t st) {
   if (n == 0) return hipSuccess;
+  (void)queue;  // reserved for a persistent (tile-queue) variant
+  (void)max_len;
+  (void)grid_cap;
 #define SWK_CASE(RR, BB)                                                                     \
   if (R == RR && RB == BB)                                                                   \
-    return col0 ? swk::launch_score<RR, BB, true>(res, offs, lens, n, queue, qtab, W, nv, S,  \
-                                                  O, E, scores, max_len, grid_cap, st)       \
-                : swk::launch_score<RR, BB, false>(res, offs, lens, n, queue, qtab, W, nv, S, \
-                                                   O, E, scores, max_len, grid_cap, st);
+    return col0 ? swk::launch_score<RR, BB, true>(res, offs, lens, n, qtab, W, nv, S, O, E,   \
+                                                  scores, st)                                \
+                : swk::launch_score<RR, BB, false>(res, offs, lens, n, qtab, W, nv, S, O, E,  \
+                                                   scores, st);
   SWK_VARIANTS(SWK_CASE)
 #undef SWK_CASE
   return hipErrorInvalidValue;
