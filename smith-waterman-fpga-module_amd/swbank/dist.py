@@ -1,0 +1,77 @@
+"""Multi-GPU sharding of a target batch (one process per GPU, torch.distributed / RCCL).
+
+The reference spreads independent targets over MODULES scoring modules through a priority
+encoder (ScoreBank/ScoreBank_v2.v:76-148) and reports (ID, score) pairs; across GPUs the
+same independence holds, so the batch is dealt out with no data-path collective and the
+only exchange is one gather of the int32 score vector to rank 0 (SURVEY §8 e).
+
+* ``shard(lens, world)``      length-balanced deal: targets sorted by length (descending)
+                              and dealt round-robin, so every rank gets ~cells/world.
+* ``gather_scores(...)``      rank 0 receives every rank's scores (padded to equal counts for
+                              the collective) and scatters them back to input order.
+* ``score_sharded(...)``      the whole path for one batch held on every rank's host.
+
+The backend is whatever process group is initialised: "nccl" (= RCCL over xGMI) on GPUs,
+"gloo" in the CPU tests.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+
+
+def shard(lens: np.ndarray, world: int) -> List[np.ndarray]:
+    """Indices of the targets each rank scores (length-balanced round-robin deal)."""
+    order = np.argsort(-np.asarray(lens, dtype=np.int64), kind="stable")
+    return [np.sort(order[r::world]) for r in range(world)]
+
+
+def gather_scores(local_scores, idx: np.ndarray, n: int, group=None) -> Optional[np.ndarray]:
+    """Gather per-rank scores (torch int32 tensor of len(idx)) to rank 0 -> int32[n] in input
+    order on rank 0, None elsewhere.  One dist.gather of equal-size (padded) buffers."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = local_scores.device
+    counts = torch.tensor([len(idx)], dtype=torch.int64, device=dev)
+    all_counts = [torch.zeros_like(counts) for _ in range(world)]
+    dist.all_gather(all_counts, counts, group=group)
+    cmax = int(max(int(c.item()) for c in all_counts))
+    buf = torch.full((cmax,), -1, dtype=torch.int32, device=dev)
+    buf[: len(idx)] = local_scores
+    ibuf = torch.full((cmax,), -1, dtype=torch.int64, device=dev)
+    ibuf[: len(idx)] = torch.as_tensor(idx, dtype=torch.int64, device=dev)
+    if rank == 0:
+        sc_list = [torch.empty_like(buf) for _ in range(world)]
+        ix_list = [torch.empty_like(ibuf) for _ in range(world)]
+    else:
+        sc_list = ix_list = None
+    dist.gather(buf, gather_list=sc_list, dst=0, group=group)
+    dist.gather(ibuf, gather_list=ix_list, dst=0, group=group)
+    if rank != 0:
+        return None
+    out = np.full(n, np.iinfo(np.int32).min, dtype=np.int32)
+    for sc, ix, c in zip(sc_list, ix_list, all_counts):
+        c = int(c.item())
+        out[ix[:c].cpu().numpy()] = sc[:c].cpu().numpy()
+    return out
+
+
+def score_sharded(bank, residues: np.ndarray, offsets: np.ndarray, lens: np.ndarray,
+                  group=None, device=None) -> Optional[np.ndarray]:
+    """Score a batch every rank holds on the host: rank r scores its shard on its own GPU
+    (``bank`` is that rank's ScoreBank), then scores are gathered to rank 0."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    idx = shard(lens, world)[rank]
+    mine = bank.score_batch(residues, np.asarray(offsets)[idx], np.asarray(lens)[idx])
+    t = torch.as_tensor(mine, dtype=torch.int32)
+    if device is not None:
+        t = t.to(device)
+    return gather_scores(t, idx, len(lens), group=group)

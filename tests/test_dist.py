@@ -1,0 +1,79 @@
+"""World-size-2 gloo tests of the multi-GPU path's host logic (sharding + score gather).
+
+On the GPU box each rank's ``bank`` is a ScoreBank on its own device and the process group is
+RCCL; here the per-rank scorer is the oracle (a test double exposing ``score_batch``), so the
+test exercises exactly the sharding and the gather collective that bench.py and
+swbank.dist.score_sharded use."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+import swbank.dist as D
+from oracle import oracle as O
+
+
+def test_shard_is_a_balanced_partition():
+    rng = np.random.default_rng(0)
+    lens = rng.integers(0, 1000, 1001)
+    for world in (1, 2, 3, 8):
+        parts = D.shard(lens, world)
+        allidx = np.sort(np.concatenate(parts))
+        assert (allidx == np.arange(len(lens))).all()
+        cells = [int(lens[p].sum()) for p in parts]
+        assert max(cells) - min(cells) <= int(lens.max())
+
+
+class _OracleBank:
+    """Test double with the ScoreBank.score_batch signature (CPU oracle)."""
+
+    def __init__(self, q):
+        self.q = q
+
+    def score_batch(self, res, offs, lens):
+        return O.score_batch(self.q, res, offs, lens, O.dna_matrix(), -12, -4)
+
+
+def _worker(rank, world, port, ret):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(42)  # same batch on every rank
+        q = rng.integers(0, 4, 100, dtype=np.uint8)
+        seqs = [rng.integers(0, 4, int(rng.integers(0, 200)), dtype=np.uint8) for _ in range(257)]
+        res, offs, lens = O.pack_residues(seqs)
+        out = D.score_sharded(_OracleBank(q), res, offs, lens)
+        if rank == 0:
+            want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)
+            ret.put(bool((out == want).all()))
+        else:
+            ret.put(out is None)
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_sharded_scores_equal_single_process(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(results)
