@@ -16,13 +16,13 @@
 #include "swbank.h"
 #include "swbank_internal.h"
 
-extern "C" int swk_has_variant(int R, int RB);
-extern "C" hipError_t swk_launch_score_dna(int R, int RB, int col0, const uint8_t* res,
-                                           const uint64_t* offs, const uint32_t* lens, size_t n,
-                                           unsigned* queue, const uint32_t* qtab, int W,
-                                           uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
-                                           int32_t* scores, uint32_t max_len, int grid_cap,
-                                           hipStream_t st);
+extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh);
+extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh,
+                                       const uint8_t* res, const uint64_t* offs,
+                                       const uint32_t* lens, size_t n, const uint32_t* qtab,
+                                       uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
+                                       uint32_t PS, uint32_t pad, int W, int32_t* scores,
+                                       hipStream_t st);
 
 namespace {
 int env_int(const char* name, int dflt) {
@@ -71,11 +71,10 @@ struct sw_bank {
 
   // derived per (penalties, query)
   bool dirty = true;
-  int R = 32, RB = 4, W = 1, col0 = 0, grid_cap = 0;
-  uint32_t S = 0, O = 0, E = 0, nv = 0;
+  int R = 32, RB = 4, W = 1, col0 = 0, prof = 0;
+  uint32_t S = 0, O = 0, E = 0, nv = 0, PS = 0, pad = 4;
   int32_t smax = 0;
-  DevBuf<uint32_t> qtab;
-  DevBuf<unsigned> queue;  // tile queue head of the persistent score kernel
+  DevBuf<uint32_t> qtab;  // LUT words or query-profile bytes
 
   // workspaces
   DevBuf<uint8_t> res;
@@ -123,8 +122,6 @@ extern "C" sw_status sw_bank_create(sw_bank** out, const sw_config* cfg_in) {
     sw_config_default(&cfg);
   if (cfg.alphabet != SW_ALPHABET_DNA && cfg.alphabet != SW_ALPHABET_PROTEIN) return SW_ERR_ARG;
   if (cfg.gap_model != SW_GAP_MERGED && cfg.gap_model != SW_GAP_GOTOH) return SW_ERR_ARG;
-  if (cfg.alphabet != SW_ALPHABET_DNA || cfg.gap_model != SW_GAP_MERGED)
-    return SW_ERR_UNSUPPORTED;  // protein / Gotoh kernels: not in this build
   if (cfg.max_query_len > SWB_MAX_QUERY) return SW_ERR_UNSUPPORTED;
 
   int ndev = 0;
@@ -147,7 +144,15 @@ extern "C" sw_status sw_bank_create(sw_bank** out, const sw_config* cfg_in) {
     delete b;
     return SW_ERR_HIP;
   }
-  b->alpha = SW_DNA_ALPHA;
+  b->alpha = cfg.alphabet == SW_ALPHABET_DNA ? SW_DNA_ALPHA : SW_PROTEIN_ALPHA;
+  if (cfg.alphabet == SW_ALPHABET_PROTEIN) {  // BLOSUM62 -11/-1 until sw_set_matrix is called
+    int8_t m[SW_PROTEIN_ALPHA * SW_PROTEIN_ALPHA];
+    sw_fill_matrix(SW_ALPHABET_PROTEIN, 0, 0, m);
+    b->matrix.assign(m, m + sizeof(m));
+    b->gap_open = -11;
+    b->gap_extend = -1;
+    b->have_pen = true;
+  }
   *out = b;
   return SW_OK;
 }
@@ -160,7 +165,6 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   double pm, sm;
   (void)sw_bank_timing(b, &nl, &pm, &sm);
   b->qtab.release();
-  b->queue.release();
   b->res.release();
   b->offs.release();
   b->lens.release();
@@ -218,8 +222,9 @@ extern "C" sw_status sw_load_query(sw_bank* b, uint64_t id, const uint8_t* codes
   return SW_OK;
 }
 
-// Build the per-row LUTs (the PE query registers + penalty registers,
-// ScoringModule_v1.1.v:110-150) for the resident query.
+// Build the resident query state (the ScoringModule's query + penalty registers,
+// ScoringModule_v1.1.v:110-150): either per-row 4-byte LUTs (DNA fast path) or a query
+// profile QP[letter][row] = S - s(q_row, letter) (any alphabet).
 static sw_status prepare(sw_bank* b) {
   if (!b->have_pen || !b->have_query)
     return fail(b, SW_ERR_STATE, "load penalties (ld_penalties) and a query (ld_sequence) first");
@@ -227,46 +232,60 @@ static sw_status prepare(sw_bank* b) {
   const int A = b->alpha;
   const int8_t* m = b->matrix.data();
   int smax = -128, smin = 127;
-  for (int i = 0; i < 4; ++i)
-    for (int j = 0; j < A; ++j) {
-      smax = std::max<int>(smax, m[i * A + j]);
-      smin = std::min<int>(smin, m[i * A + j]);
-    }
-  for (int j = 0; j < A; ++j) {  // row N too
-    smax = std::max<int>(smax, m[4 * A + j]);
-    smin = std::min<int>(smin, m[4 * A + j]);
+  for (int i = 0; i < A * A; ++i) {
+    smax = std::max<int>(smax, m[i]);
+    smin = std::min<int>(smin, m[i]);
   }
-  // column N must be uniform per kernel (one shared VGPR for codes 4..7)
-  const int sN = m[0 * A + 4];
-  for (int i = 0; i < A; ++i)
-    if (m[i * A + 4] != sN)
-      return fail(b, SW_ERR_UNSUPPORTED, "DNA kernel needs a uniform N column in the matrix");
-  if (sN > 0) return fail(b, SW_ERR_ARG, "mismatch/N scores must be <= 0");
   const int S = std::max(0, smax);
   if (S - smin > 254)
     return fail(b, SW_ERR_RANGE, "substitution range [%d, %d] exceeds 254", smin, smax);
   const int o = -b->gap_open, e = -b->gap_extend;
+  const bool gotoh = b->cfg.gap_model == SW_GAP_GOTOH;
+  if (gotoh && o + e + S > 65535) return fail(b, SW_ERR_RANGE, "gap penalties too large");
+
+  // LUT mode needs a DNA matrix whose N column (codes 4..7 share one word) is uniform and <= 0
+  bool lut = A == SW_DNA_ALPHA;
+  const int sN = m[4];
+  for (int i = 0; lut && i < A; ++i) lut = m[i * A + 4] == sN;
+  lut = lut && sN <= 0;
+  const int prof = (env_int("SWBANK_PROFILE", 0) || !lut) ? 1 : 0;
 
   const int qlen = (int)b->query.size();
-  // Rows per wave: 32 (16 for tiny queries, 64 past 16 waves).  SWBANK_R/C/RB override
+  // Rows per wave: 32 (16 for tiny queries, 64 past 16 waves).  SWBANK_R / SWBANK_RB override
   // (tuning only; must name a compiled variant).
   int R = qlen <= 16 ? 16 : 32, RB = 4;
   if ((qlen + R - 1) / R > 16) R = 64;
   R = env_int("SWBANK_R", R);
   RB = env_int("SWBANK_RB", RB);
-  if (!swk_has_variant(R, RB))
-    return fail(b, SW_ERR_UNSUPPORTED, "no kernel variant R=%d RB=%d", R, RB);
+  // the HDL column-0 rule differs from the plain recurrence only if a match pays for a gap
+  const int col0 = (!gotoh && smax > o + e) ? 1 : 0;
+  if (!swk_has_variant(R, RB, col0, prof, gotoh ? 1 : 0))
+    return fail(b, SW_ERR_UNSUPPORTED, "no kernel variant R=%d RB=%d col0=%d prof=%d gotoh=%d", R,
+                RB, col0, prof, (int)gotoh);
   const int W = std::max(1, (qlen + R - 1) / R);
   if (W * 64 > (R >= 64 ? 512 : 1024))
     return fail(b, SW_ERR_UNSUPPORTED, "query length %d too long for one bank", qlen);
 
-  std::vector<uint32_t> tab((size_t)W * R, 0xFFFFFFFFu);
-  for (int i = 0; i < qlen; ++i) {
-    uint32_t w = 0;
-    for (int c = 0; c < 4; ++c) w |= (uint32_t)(uint8_t)(S - m[b->query[i] * A + c]) << (8 * c);
-    tab[i] = w;
+  std::vector<uint32_t> tab;
+  uint32_t PS = 0, pad = 4, nv = 0;
+  if (!prof) {
+    tab.assign((size_t)W * R, 0xFFFFFFFFu);
+    for (int i = 0; i < qlen; ++i) {
+      uint32_t w = 0;
+      for (int c = 0; c < 4; ++c) w |= (uint32_t)(uint8_t)(S - m[b->query[i] * A + c]) << (8 * c);
+      tab[i] = w;
+    }
+    nv = (uint32_t)(uint8_t)(S - sN) * 0x01010101u;
+  } else {
+    PS = (uint32_t)((W * R + 15) / 16 * 16);
+    pad = (uint32_t)A;  // letter A = padding row (all 0xFF)
+    std::vector<uint8_t> qp((size_t)(A + 1) * PS, 0xFF);
+    for (int c = 0; c < A; ++c)
+      for (int i = 0; i < qlen; ++i)
+        qp[(size_t)c * PS + i] = (uint8_t)(S - m[b->query[i] * A + c]);
+    tab.resize(qp.size() / 4);
+    std::memcpy(tab.data(), qp.data(), qp.size());
   }
-  const uint32_t pN = (uint32_t)(uint8_t)(S - sN);
   HIPOK(b, hipSetDevice(b->device));
   HIPOK(b, b->qtab.reserve(tab.size()));
   HIPOK(b, hipMemcpyAsync(b->qtab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice,
@@ -274,15 +293,16 @@ static sw_status prepare(sw_bank* b) {
   HIPOK(b, hipStreamSynchronize(b->stream));
   b->R = R;
   b->RB = RB;
-  b->grid_cap = env_int("SWBANK_GRID", 0);
   b->W = W;
   b->S = (uint32_t)S;
   b->O = (uint32_t)o;
   b->E = (uint32_t)e;
-  b->nv = pN * 0x01010101u;
+  b->nv = nv;
+  b->PS = PS;
+  b->pad = pad;
+  b->prof = prof;
   b->smax = smax;
-  // HDL column-0 rule differs from the plain recurrence only if a match can pay for a gap open
-  b->col0 = (smax > o + e) ? 1 : 0;
+  b->col0 = col0;
   b->dirty = false;
   return SW_OK;
 }
@@ -298,9 +318,7 @@ static sw_status range_check(sw_bank* b, uint32_t max_len) {
 }
 
 static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
-                        const uint32_t* d_lens, size_t n, uint32_t max_len, int32_t* d_scores,
-                        hipStream_t st) {
-  HIPOK(b, b->queue.reserve(16));
+                        const uint32_t* d_lens, size_t n, int32_t* d_scores, hipStream_t st) {
   sw_bank::Ev ev{};
   if (b->timing) {
     HIPOK(b, hipEventCreate(&ev.a));
@@ -308,12 +326,13 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
     HIPOK(b, hipEventCreate(&ev.c));
     HIPOK(b, hipEventRecord(ev.a, st));
   }
-  // no separate feeder kernel any more: the score kernel streams the codes itself, so the
-  // "pack" interval (a..b) is empty and kept only for ABI stability
+  // no separate feeder kernel: the score kernel streams the codes itself, so the "pack"
+  // interval (a..b) is empty and kept only for ABI stability
   if (b->timing) HIPOK(b, hipEventRecord(ev.b, st));
-  HIPOK(b, swk_launch_score_dna(b->R, b->RB, b->col0, d_res, d_offs, d_lens, n, b->queue.p,
-                                b->qtab.p, b->W, b->nv, b->S, b->O, b->E, d_scores, max_len,
-                                b->grid_cap, st));
+  HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof,
+                            b->cfg.gap_model == SW_GAP_GOTOH ? 1 : 0, d_res, d_offs, d_lens, n,
+                            b->qtab.p, b->nv, b->S, b->O, b->E, b->PS, b->pad, b->W, d_scores,
+                            st));
   if (b->timing) {
     HIPOK(b, hipEventRecord(ev.c, st));
     b->events.push_back(ev);
@@ -332,7 +351,7 @@ extern "C" sw_status sw_score_batch_device(sw_bank* b, const uint8_t* d_res,
   if (st != SW_OK) return st;
   if ((st = range_check(b, max_len)) != SW_OK) return st;
   HIPOK(b, hipSetDevice(b->device));
-  return launch(b, d_res, d_offs, d_lens, n, max_len, d_scores,
+  return launch(b, d_res, d_offs, d_lens, n, d_scores,
                 stream ? reinterpret_cast<hipStream_t>(stream) : b->stream);
 }
 
@@ -380,7 +399,7 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const u
   HIPOK(b, hipMemcpyAsync(b->res.p, hres.data(), hres.size(), hipMemcpyHostToDevice, b->stream));
   HIPOK(b, hipMemcpyAsync(b->offs.p, hoffs.data(), n * 8, hipMemcpyHostToDevice, b->stream));
   HIPOK(b, hipMemcpyAsync(b->lens.p, hlens.data(), n * 4, hipMemcpyHostToDevice, b->stream));
-  st = launch(b, b->res.p, b->offs.p, b->lens.p, n, max_len, b->scores.p, b->stream);
+  st = launch(b, b->res.p, b->offs.p, b->lens.p, n, b->scores.p, b->stream);
   if (st != SW_OK) return st;
   std::vector<int32_t> sorted(n);
   HIPOK(b, hipMemcpyAsync(sorted.data(), b->scores.p, n * 4, hipMemcpyDeviceToHost, b->stream));

@@ -42,16 +42,40 @@ __device__ __forceinline__ u16x2 vsubs(u16x2 a, u16x2 b) {
 
 
 
-// One column of R rows for one wave.  ZDOWN: HDL column-0 rule (G passed down = 0).
-// RB: rows per scheduling group (a sched_barrier every RB rows bounds how far the scheduler
-// may defer the H/best updates behind the G chain, i.e. register pressure).
-template <int R, int RB, bool ZDOWN>
-__device__ __forceinline__ void column(const uint32_t (&tab)[R], uint32_t nv, uint32_t selw,
-                                       u16x2& diag, u16x2& upG, u16x2 (&Hl)[R], u16x2 (&Gl)[R],
-                                       u16x2& best, u16x2 S2, u16x2 O2, u16x2 E2) {
+// ---- substitution lookup: p = S - s(q_row, t) for both targets of the lane --------------
+// LUT mode (DNA): the row's query letter is wave-uniform, its 4-entry row of (S - s) is one
+// SGPR; codes 4..7 (N and padding) read `nv`.  One v_perm_b32 per row.
+template <int R>
+struct LutLookup {
+  const uint32_t (&tab)[R];
+  uint32_t nv, selw;
+  __device__ __forceinline__ u16x2 operator()(int r) const {
+    return as_u16x2(__builtin_amdgcn_perm(nv, tab[r], selw));
+  }
+};
+// Profile mode (any alphabet): per column each lane reads the wave's R profile bytes for its
+// two target letters from LDS (query profile QP[letter][row]); one v_perm_b32 per row
+// interleaves them into the two u16 halves.
+template <int R>
+struct ProfLookup {
+  uint32_t lo[R / 4], hi[R / 4];
+  __device__ __forceinline__ u16x2 operator()(int r) const {
+    const uint32_t sel = (uint32_t)(r & 3) | ((uint32_t)(4 + (r & 3)) << 16) | 0x0C000C00u;
+    return as_u16x2(__builtin_amdgcn_perm(hi[r >> 2], lo[r >> 2], sel));
+  }
+};
+
+// ---- one column of R rows, merged gap matrix (the ScoreBank PE) --------------------------
+// ZDOWN: HDL column-0 rule (G passed down = 0).  RB: rows per scheduling group (a
+// sched_barrier every RB rows bounds how far the scheduler may defer the H/best updates
+// behind the G chain, i.e. register pressure).
+template <int R, int RB, bool ZDOWN, class LK>
+__device__ __forceinline__ void column_merged(const LK& lk, u16x2& diag, u16x2& upG,
+                                              u16x2 (&Hl)[R], u16x2 (&Gl)[R], u16x2& best,
+                                              u16x2 S2, u16x2 O2, u16x2 E2) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const u16x2 p = as_u16x2(__builtin_amdgcn_perm(nv, tab[r], selw));
+    const u16x2 p = lk(r);
     const u16x2 M = vsubs(diag, p);
     const u16x2 I = vsubs(vmax(upG, Gl[r]), E2);
     const u16x2 Hn = vmax(M, I) + S2;
@@ -65,6 +89,31 @@ __device__ __forceinline__ void column(const uint32_t (&tab)[R], uint32_t nv, ui
   }
 }
 
+// ---- one column of R rows, Gotoh (separate E/F; ssearch36 semantics) ---------------------
+//   E(i,j) = max(H(i,j-1) - o - e, E(i,j-1) - e)     F(i,j) = max(H(i-1,j) - o - e, F(i-1,j) - e)
+//   H(i,j) = max(0, H(i-1,j-1) + s, E, F)            (E, F clamped at 0: exact, H >= 0)
+// OES = o + e + S because stored H~ = H + S.  12 VALU per lane per 2 cells.
+template <int R, int RB, class LK>
+__device__ __forceinline__ void column_gotoh(const LK& lk, u16x2& diag, u16x2& upH, u16x2& upF,
+                                             u16x2 (&Hl)[R], u16x2 (&El)[R], u16x2& best,
+                                             u16x2 S2, u16x2 OES2, u16x2 E2) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const u16x2 p = lk(r);
+    const u16x2 M = vsubs(diag, p);
+    const u16x2 Ei = vmax(vsubs(Hl[r], OES2), vsubs(El[r], E2));
+    const u16x2 Fi = vmax(vsubs(upH, OES2), vsubs(upF, E2));
+    const u16x2 Hn = vmax(vmax(M, Ei), Fi) + S2;
+    best = vmax(best, M);
+    diag = Hl[r];
+    Hl[r] = Hn;
+    El[r] = Ei;
+    upH = Hn;
+    upF = Fi;
+    if ((r % RB) == RB - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // The lane's two targets of the current tile.
 struct Lane2 {
   const uint8_t* plo;
@@ -73,9 +122,11 @@ struct Lane2 {
 };
 
 // Raw codes of columns [8c, 8c+8) of both targets (x,y = bytes 0-3, 4-7).  Past a target's
-// end the code is 4 (N): s(*, N) <= 0, so padding can only lower a score.  `full` (uniform):
-// every lane has >= 8 codes left in both targets -> two unaligned 8-byte loads.
-__device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint2& lo, uint2& hi) {
+// end the code is `pad` (LUT mode: 4 = N, s(*, N) <= 0; profile mode: a row of S - s = 255),
+// so padding can only lower a score.  `full` (uniform): every lane has >= 8 codes left in
+// both targets -> two unaligned 8-byte loads.
+__device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint32_t pad,
+                                         uint2& lo, uint2& hi) {
   const uint32_t j0 = (uint32_t)c * 8;
   if (full) {
     lo = *reinterpret_cast<const uint2*>(t.plo + j0);
@@ -87,8 +138,8 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint2
       const uint32_t j = j0 + k;
       const uint32_t a = t.plo[j < t.llo ? j : 0];
       const uint32_t h = t.phi[j < t.lhi ? j : 0];
-      b[0][k] = j < t.llo ? a : 4u;
-      b[1][k] = j < t.lhi ? h : 4u;
+      b[0][k] = j < t.llo ? a : pad;
+      b[1][k] = j < t.lhi ? h : pad;
     }
     lo.x = b[0][0] | b[0][1] << 8 | b[0][2] << 16 | b[0][3] << 24;
     lo.y = b[0][4] | b[0][5] << 8 | b[0][6] << 16 | b[0][7] << 24;
@@ -124,18 +175,26 @@ __device__ __forceinline__ void tile_chunks(const Lane2& t, size_t tlo, size_t t
   nfull = (int)(__builtin_amdgcn_readfirstlane(Lmin) / 8);
 }
 
+// Kernel arguments (one struct, passed by value).
+struct ScoreArgs {
+  const uint8_t* res;     // target codes, any byte alignment
+  const uint64_t* offs;   // target k = res[offs[k] .. offs[k] + lens[k])
+  const uint32_t* lens;
+  size_t n;
+  const uint32_t* qtab;   // LUT: W*R row words | PROF: (alpha+1) x PS bytes of S - s
+  uint32_t nv;            // LUT: 4 x (S - s(*, N)) for codes 4..7
+  uint32_t S, O, E;       // shift (>= max s), -gap_open, -gap_extend
+  uint32_t PS;            // PROF: profile row stride in bytes (multiple of 16, >= W*R)
+  uint32_t pad;           // code used past a target's end (LUT: 4 = N; PROF: alpha = 0xFF row)
+  int32_t* scores;
+};
+
 // Score kernel: one workgroup = one tile of 128 targets x the whole query (W waves x R rows).
 // Wave w processes chunk c (8 columns) at phase c + w; one __syncthreads per phase orders the
 // LDS ring hand-off wave w -> w+1 (the RTL's PE-to-PE registers).
-//   qtab   W*R row LUTs: byte b = S - s(q_i, b) for codes b = 0..3; pad rows 0xFFFFFFFF
-//   nv     4 x (S - s(*, N)) for target codes 4..7
-//   S,O,E  shift (>= max s), -gap_open, -gap_extend
-// LDS: best[128] | edge[2][64] | ring[(W-1)][2][8][64] {H~, G}
-template <int R, int RB, bool COL0>
-__global__ void __launch_bounds__(R >= 64 ? 512 : 1024)
-    score_dna(const uint8_t* __restrict__ res, const uint64_t* __restrict__ offs,
-              const uint32_t* __restrict__ lens, size_t n, const uint32_t* __restrict__ qtab,
-              uint32_t nv, uint32_t S, uint32_t O, uint32_t E, int32_t* __restrict__ scores) {
+// LDS: best[128] | edge[2][64] | ring[(W-1)][2][8][64] {H~, G or F} | PROF: profile
+template <int R, int RB, bool COL0, bool PROF, bool GOTOH>
+__global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
   constexpr int C = 8;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
@@ -144,50 +203,66 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024)
   uint32_t* bestsh = smem;                                   // 128 words
   uint2* edge = reinterpret_cast<uint2*>(smem + SWB_TILE);   // 2 x 64: top boundary | sink
   uint2* ring = edge + 128;
+  uint8_t* prof = reinterpret_cast<uint8_t*>(ring + (size_t)(W > 1 ? W - 1 : 0) * 2 * C * 64);
 
   const int tile = blockIdx.x;
+  const size_t n = a.n;
   const size_t tlo = (size_t)tile * SWB_TILE + lane, thi = tlo + 64;
-  const Lane2 cur = lane_targets(res, offs, lens, n, tile, lane);
+  const Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane);
   int nch, nfull;
   tile_chunks(cur, tlo, thi, n, nch, nfull);
+  const uint32_t S = a.S;
 
   if (wave == 0) {
     bestsh[lane] = 0;
     bestsh[lane + 64] = 0;
-    edge[lane] = make_uint2(S | (S << 16), 0u);  // row -1: H~ = S, G = 0
+    edge[lane] = make_uint2(S | (S << 16), 0u);  // row -1: H~ = S, G/F = 0
   }
-  // nv in a VGPR so each v_perm_b32 takes its row LUT straight from an SGPR (one scalar
-  // operand per VOP3 on gfx950).
-  asm volatile("" : "+v"(nv));
-  uint32_t tab[R];
+  uint32_t nv = a.nv;
+  uint32_t tab[PROF ? 1 : R];
+  if constexpr (PROF) {
+    // query profile -> LDS (the ScoringModule's query + penalty registers)
+    const uint32_t words = (a.pad + 1) * a.PS / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+      reinterpret_cast<uint4*>(prof)[i] = src[i];
+  } else {
+    // nv in a VGPR so each v_perm_b32 takes its row LUT straight from an SGPR (one scalar
+    // operand per VOP3 on gfx950).
+    asm volatile("" : "+v"(nv));
 #pragma unroll
-  for (int r = 0; r < R; ++r) tab[r] = __builtin_amdgcn_readfirstlane(qtab[wave * R + r]);
+    for (int r = 0; r < R; ++r) tab[r] = __builtin_amdgcn_readfirstlane(a.qtab[wave * R + r]);
+  }
   const u16x2 S2 = {(unsigned short)S, (unsigned short)S};
-  const u16x2 O2 = {(unsigned short)O, (unsigned short)O};
-  const u16x2 E2 = {(unsigned short)E, (unsigned short)E};
+  const u16x2 O2 = {(unsigned short)a.O, (unsigned short)a.O};
+  const u16x2 E2 = {(unsigned short)a.E, (unsigned short)a.E};
+  const uint32_t oes = a.O + a.E + S;
+  const u16x2 OES2 = {(unsigned short)oes, (unsigned short)oes};
 
-  u16x2 Hl[R], Gl[R];
+  u16x2 Hl[R], Xl[R];  // H~ and G (merged) or E (Gotoh) of the column to the left
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     Hl[r] = S2;
-    Gl[r] = (u16x2){0, 0};
+    Xl[r] = (u16x2){0, 0};
   }
   u16x2 best = {0, 0};
   u16x2 prevUpH = S2;  // H~(row above, column -1) = S
   uint2 rlo, rhi;      // raw codes of the next chunk (prefetched one phase ahead)
-  load_raw(cur, 0, nfull > 0, rlo, rhi);
+  load_raw(cur, 0, nfull > 0, a.pad, rlo, rhi);
   __syncthreads();
 
   // branch-free hand-off: wave 0 reads the constant top boundary, the last wave writes into a
   // sink, both with column stride 0 (branches here split the column loop into blocks and LLVM
   // then sinks the H updates across columns, blowing up register pressure)
   const int istride = wave > 0 ? 64 : 0, ostride = wave < W - 1 ? 64 : 0;
+  const uint32_t pbase = (uint32_t)wave * R;
+  const uint32_t padc = a.pad;
   const int nph = nch + W - 1;
   for (int ph = 0; ph < nph; ++ph) {
     const int c = ph - wave;
     if (c >= 0 && c < nch) {
       const uint2 clo = rlo, chi = rhi;
-      if (c + 1 < nch) load_raw(cur, c + 1, c + 1 < nfull, rlo, rhi);
+      if (c + 1 < nch) load_raw(cur, c + 1, c + 1 < nfull, a.pad, rlo, rhi);
       const int slot = c & 1;
       const uint2* rin = wave > 0 ? ring + ((size_t)((wave - 1) * 2 + slot) * C) * 64 + lane
                                   : edge + lane;
@@ -197,24 +272,53 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024)
 #pragma unroll
       for (int jj = 0; jj < C; ++jj) {
         const u16x2 upH = as_u16x2(rv.x);
-        u16x2 upG = as_u16x2(rv.y);
+        u16x2 upX = as_u16x2(rv.y);
         if (jj + 1 < C) rv = rin[(jj + 1) * istride];  // one column ahead
         u16x2 diag = prevUpH;
         prevUpH = upH;
-        // selector: byte 0 = code of the low target, byte 2 = code of the high target
-        const uint32_t sel = (uint32_t)(jj & 3) | ((uint32_t)(4 + (jj & 3)) << 16) | 0x0C000C00u;
-        const uint32_t selw =
-            __builtin_amdgcn_perm(jj < 4 ? chi.x : chi.y, jj < 4 ? clo.x : clo.y, sel) |
-            0x0C000C00u;
-        __builtin_amdgcn_sched_barrier(0);
-        if (COL0 && jj == 0 && c == 0)
-          column<R, RB, true>(tab, nv, selw, diag, upG, Hl, Gl, best, S2, O2, E2);
-        else
-          column<R, RB, false>(tab, nv, selw, diag, upG, Hl, Gl, best, S2, O2, E2);
+        const uint32_t wlo = jj < 4 ? clo.x : clo.y, whi = jj < 4 ? chi.x : chi.y;
+        if constexpr (PROF) {
+          ProfLookup<R> lk;
+          const uint32_t blo = min((wlo >> (8 * (jj & 3))) & 0xFFu, padc);
+          const uint32_t bhi = min((whi >> (8 * (jj & 3))) & 0xFFu, padc);
+          const uint4* plo = reinterpret_cast<const uint4*>(prof + blo * a.PS + pbase);
+          const uint4* phi = reinterpret_cast<const uint4*>(prof + bhi * a.PS + pbase);
+#pragma unroll
+          for (int q = 0; q < R / 16; ++q) {
+            const uint4 x = plo[q], y = phi[q];
+            lk.lo[4 * q] = x.x; lk.lo[4 * q + 1] = x.y; lk.lo[4 * q + 2] = x.z;
+            lk.lo[4 * q + 3] = x.w;
+            lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z;
+            lk.hi[4 * q + 3] = y.w;
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (GOTOH) {
+            u16x2 uH = upH;
+            column_gotoh<R, RB>(lk, diag, uH, upX, Hl, Xl, best, S2, OES2, E2);
+          } else if (COL0 && jj == 0 && c == 0) {
+            column_merged<R, RB, true>(lk, diag, upX, Hl, Xl, best, S2, O2, E2);
+          } else {
+            column_merged<R, RB, false>(lk, diag, upX, Hl, Xl, best, S2, O2, E2);
+          }
+        } else {
+          // selector: byte 0 = code of the low target, byte 2 = code of the high target
+          const uint32_t sel =
+              (uint32_t)(jj & 3) | ((uint32_t)(4 + (jj & 3)) << 16) | 0x0C000C00u;
+          const LutLookup<R> lk{tab, nv, __builtin_amdgcn_perm(whi, wlo, sel) | 0x0C000C00u};
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (GOTOH) {
+            u16x2 uH = upH;
+            column_gotoh<R, RB>(lk, diag, uH, upX, Hl, Xl, best, S2, OES2, E2);
+          } else if (COL0 && jj == 0 && c == 0) {
+            column_merged<R, RB, true>(lk, diag, upX, Hl, Xl, best, S2, O2, E2);
+          } else {
+            column_merged<R, RB, false>(lk, diag, upX, Hl, Xl, best, S2, O2, E2);
+          }
+        }
         // pin the running max once per column: otherwise LLVM re-associates the max over the
         // whole phase into a tree and keeps every M live
         asm volatile("" : "+v"(best));
-        rout[jj * ostride] = make_uint2(as_u32(Hl[R - 1]), as_u32(upG));
+        rout[jj * ostride] = make_uint2(as_u32(Hl[R - 1]), as_u32(upX));
       }
     }
     __syncthreads();
@@ -224,18 +328,17 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024)
   atomicMax(&bestsh[lane + 64], (uint32_t)best.y);
   __syncthreads();
   if (wave == 0) {
-    if (tlo < n) scores[tlo] = (int32_t)bestsh[lane];
-    if (thi < n) scores[thi] = (int32_t)bestsh[lane + 64];
+    if (tlo < n) a.scores[tlo] = (int32_t)bestsh[lane];
+    if (thi < n) a.scores[thi] = (int32_t)bestsh[lane + 64];
   }
 }
 
-template <int R, int RB, bool COL0>
-static hipError_t launch_score(const uint8_t* res, const uint64_t* offs, const uint32_t* lens,
-                               size_t n, const uint32_t* qtab, int W, uint32_t nv, uint32_t S,
-                               uint32_t O, uint32_t E, int32_t* scores, hipStream_t st) {
-  const size_t ntiles = (n + SWB_TILE - 1) / SWB_TILE;
-  const size_t lds = SWB_TILE * 4 + (size_t)(128 + (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8;
-  auto fn = &score_dna<R, RB, COL0>;
+template <int R, int RB, bool COL0, bool PROF, bool GOTOH>
+static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st) {
+  const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE;
+  const size_t lds = SWB_TILE * 4 + (size_t)(128 + (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8 +
+                     (PROF ? prof_bytes : 0);
+  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -243,45 +346,43 @@ static hipError_t launch_score(const uint8_t* res, const uint64_t* offs, const u
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(fn, dim3((unsigned)ntiles), dim3(64 * W), (unsigned)lds, st, res, offs,
-                     lens, n, qtab, nv, S, O, E, scores);
+  if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL(fn, dim3((unsigned)ntiles), dim3(64 * W), (unsigned)lds, st, a);
   return hipGetLastError();
 }
 
 }  // namespace swk
 
-// Variants compiled in: (R, RB) — rows per wave, rows per scheduling group.  The host picks R
-// from the query length (SWBANK_R / SWBANK_RB override it for tuning).
-#define SWK_VARIANTS(X) \
-  X(16, 4)              \
-  X(32, 4)              \
-  X(32, 8)              \
-  X(64, 4)
+// Variants compiled in: (R, RB, COL0, PROF, GOTOH).  The host picks R from the query length
+// (SWBANK_R / SWBANK_RB override it for tuning).
+#define SWK_VARIANTS(X)                                                                     \
+  X(16, 4, 0, 0, 0) X(16, 4, 1, 0, 0) X(32, 4, 0, 0, 0) X(32, 4, 1, 0, 0) X(32, 8, 0, 0, 0) \
+  X(64, 4, 0, 0, 0) X(64, 4, 1, 0, 0)                                                        \
+  X(16, 4, 0, 0, 1) X(32, 4, 0, 0, 1) X(64, 4, 0, 0, 1)                                      \
+  X(16, 4, 0, 1, 0) X(16, 4, 1, 1, 0) X(32, 4, 0, 1, 0) X(32, 4, 1, 1, 0) X(64, 4, 0, 1, 0)  \
+  X(64, 4, 1, 1, 0)                                                                          \
+  X(16, 4, 0, 1, 1) X(32, 4, 0, 1, 1) X(64, 4, 0, 1, 1)
 
-extern "C" int swk_has_variant(int R, int RB) {
-#define SWK_HAS(RR, BB) \
-  if (R == RR && RB == BB) return 1;
+extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh) {
+#define SWK_HAS(RR, BB, C0, PF, GT) \
+  if (R == RR && RB == BB && col0 == C0 && prof == PF && gotoh == GT) return 1;
   SWK_VARIANTS(SWK_HAS)
 #undef SWK_HAS
   return 0;
 }
 
-extern "C" hipError_t swk_launch_score_dna(int R, int RB, int col0, const uint8_t* res,
-                                           const uint64_t* offs, const uint32_t* lens, size_t n,
-                                           unsigned* queue, const uint32_t* qtab, int W,
-                                           uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
-                                           int32_t* scores, uint32_t max_len, int grid_cap,
-                                           hipStream_t st) {
+extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh,
+                                       const uint8_t* res, const uint64_t* offs,
+                                       const uint32_t* lens, size_t n, const uint32_t* qtab,
+                                       uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
+                                       uint32_t PS, uint32_t pad, int W, int32_t* scores,
+                                       hipStream_t st) {
   if (n == 0) return hipSuccess;
-  (void)queue;  // reserved for a persistent (tile-queue) variant
-  (void)max_len;
-  (void)grid_cap;
-#define SWK_CASE(RR, BB)                                                                     \
-  if (R == RR && RB == BB)                                                                   \
-    return col0 ? swk::launch_score<RR, BB, true>(res, offs, lens, n, qtab, W, nv, S, O, E,   \
-                                                  scores, st)                                \
-                : swk::launch_score<RR, BB, false>(res, offs, lens, n, qtab, W, nv, S, O, E,  \
-                                                   scores, st);
+  const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores};
+  const uint32_t prof_bytes = (pad + 1) * PS;
+#define SWK_CASE(RR, BB, C0, PF, GT)                                                   \
+  if (R == RR && RB == BB && col0 == C0 && prof == PF && gotoh == GT)                  \
+    return swk::launch_score<RR, BB, (C0 != 0), (PF != 0), (GT != 0)>(a, W, prof_bytes, st);
   SWK_VARIANTS(SWK_CASE)
 #undef SWK_CASE
   return hipErrorInvalidValue;

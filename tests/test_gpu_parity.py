@@ -194,3 +194,95 @@ def test_cli_reproduces_transcript():
         got[name.lstrip(">")] = int(score)
     want = {t: s for src, lib, q, t, s in O.load_ref_scores() if lib == "data100.fa"}
     assert all(got[t] == s for t, s in want.items()) and len(want) == 99
+
+
+# ---- Gotoh / protein / profile-mode kernels ---------------------------------------------
+def _load_generated():
+    import json
+    return json.load(open(os.path.join(O.GOLDEN, "generated.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", _load_generated(), ids=lambda c: c["name"])
+def test_generated_golden(case):
+    """configs[3]/[4] shapes and merged!=Gotoh parameters (fixtures from the pinned oracle)."""
+    prot = case["alphabet"] == "protein"
+    alphabet = S.ALPHABET_PROTEIN if prot else S.ALPHABET_DNA
+    model = S.GAP_GOTOH if case["gap_model"] == "gotoh" else S.GAP_MERGED
+    with S.ScoreBank(alphabet=alphabet, gap_model=model) as bank:
+        if prot:
+            bank.set_matrix(O.BLOSUM62, case["gap_open"], case["gap_extend"])
+        else:
+            bank.set_penalties(*case["match_mismatch"], case["gap_open"], case["gap_extend"])
+        bank.load_query(S.encode(case["query"], alphabet))
+        got = bank.score_targets([S.encode(t, alphabet) for t in case["targets"]])
+    assert got.tolist() == case["scores"]
+
+
+@pytest.mark.parametrize("params", [(5, -4, -12, -4), (5, -4, -10, -1), (2, -3, -5, -2),
+                                    (1, -1, -1, -1)])
+@pytest.mark.parametrize("qlen", [1, 17, 32, 64, 100, 150, 256, 512])
+def test_gotoh_dna_random_vs_oracle(params, qlen):
+    rng = np.random.default_rng(qlen * 7 + params[3])
+    q, seqs = _random_case(rng, qlen, 260, 300)
+    with S.ScoreBank(gap_model=S.GAP_GOTOH) as bank:
+        bank.set_penalties(*params)
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(params[0], params[1]), params[2],
+                         params[3], O.GAP_GOTOH)
+    assert (got == want).all()
+
+
+@pytest.mark.parametrize("model", [S.GAP_MERGED, S.GAP_GOTOH])
+@pytest.mark.parametrize("gaps", [(-11, -1), (-10, -2), (-2, -1)])
+@pytest.mark.parametrize("qlen", [5, 33, 200, 512])
+def test_protein_random_vs_oracle(model, gaps, qlen):
+    rng = np.random.default_rng(qlen + 100 * model - gaps[0])
+    q = rng.integers(0, 24, qlen, dtype=np.uint8)
+    seqs = [rng.integers(0, 24, int(rng.integers(0, 400)), dtype=np.uint8) for _ in range(200)]
+    for k in range(0, 200, 8):  # homologous targets
+        seqs[k] = q[rng.integers(0, max(1, qlen // 2)):][:300].copy()
+        seqs[k][::7] = rng.integers(0, 20, len(seqs[k][::7]))
+    with S.ScoreBank(alphabet=S.ALPHABET_PROTEIN, gap_model=model) as bank:
+        bank.set_matrix(O.BLOSUM62, *gaps)
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.BLOSUM62, gaps[0], gaps[1], model)
+    assert (got == want).all()
+
+
+@pytest.mark.parametrize("model", [S.GAP_MERGED, S.GAP_GOTOH])
+def test_dna_profile_mode_equals_lut_mode(model, monkeypatch):
+    """The query-profile (LDS) lookup and the SGPR-LUT lookup are interchangeable."""
+    rng = np.random.default_rng(31)
+    q, seqs = _random_case(rng, 128, 300, 200)
+    outs = []
+    for prof in ("0", "1"):
+        monkeypatch.setenv("SWBANK_PROFILE", prof)
+        with S.ScoreBank(gap_model=model) as bank:
+            bank.set_penalties(5, -4, -10, -1)
+            bank.load_query(q)
+            outs.append(bank.score_targets(seqs))
+    assert (outs[0] == outs[1]).all()
+    res, offs, lens = O.pack_residues(seqs)
+    assert (outs[0] == O.score_batch(q, res, offs, lens, O.dna_matrix(), -10, -1, model)).all()
+
+
+def test_custom_dna_matrix_routes_to_profile_kernel():
+    """A DNA matrix with a non-uniform N column cannot use the 4-entry LUT; it must still be
+    exact (profile kernel)."""
+    m = O.dna_matrix(5, -4).copy()
+    m[4, :] = -1
+    m[:, 4] = -1
+    m[4, 4] = 2
+    m[0, 1] = m[1, 0] = -2  # transition/transversion-like asymmetry in the 4x4 block
+    rng = np.random.default_rng(8)
+    q, seqs = _random_case(rng, 77, 200, 150, p_n=0.1)
+    with S.ScoreBank() as bank:
+        bank.set_matrix(m, -12, -4)
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    assert (got == O.score_batch(q, res, offs, lens, m, -12, -4)).all()
