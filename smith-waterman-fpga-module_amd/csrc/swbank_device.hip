@@ -22,7 +22,8 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        const uint32_t* lens, size_t n, const uint32_t* qtab,
                                        uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
-                                       hipStream_t st);
+                                       const void* edge_in, void* edge_out, uint32_t ecols,
+                                       int accum, hipStream_t st);
 
 namespace {
 int env_int(const char* name, int dflt) {
@@ -74,7 +75,10 @@ struct sw_bank {
   int R = 32, RB = 4, W = 1, col0 = 0, prof = 0;
   uint32_t S = 0, O = 0, E = 0, nv = 0, PS = 0, pad = 4;
   int32_t smax = 0;
-  DevBuf<uint32_t> qtab;  // LUT words or query-profile bytes
+  DevBuf<uint32_t> qtab;  // LUT words or query-profile bytes, per query segment
+  struct Seg { int W; size_t off; };  // rows = W*R (last may be shorter), qtab word offset
+  std::vector<Seg> segs;
+  DevBuf<uint2> edge[2];  // bottom rows handed from segment to segment
 
   // workspaces
   DevBuf<uint8_t> res;
@@ -165,6 +169,8 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   double pm, sm;
   (void)sw_bank_timing(b, &nl, &pm, &sm);
   b->qtab.release();
+  b->edge[0].release();
+  b->edge[1].release();
   b->res.release();
   b->offs.release();
   b->lens.release();
@@ -251,40 +257,52 @@ static sw_status prepare(sw_bank* b) {
   const int prof = (env_int("SWBANK_PROFILE", 0) || !lut) ? 1 : 0;
 
   const int qlen = (int)b->query.size();
-  // Rows per wave: 32 (16 for tiny queries, 64 past 16 waves).  SWBANK_R / SWBANK_RB override
-  // (tuning only; must name a compiled variant).
+  // Rows per wave: 32 (16 for tiny queries).  Queries longer than one workgroup (512 rows)
+  // run as segments of SWBANK_SEG rows (default 256), each segment's bottom row handed to
+  // the next through HBM.  SWBANK_R / SWBANK_RB / SWBANK_SEG override (tuning only).
   int R = qlen <= 16 ? 16 : 32, RB = 4;
-  if ((qlen + R - 1) / R > 16) R = 64;
+  int seg_rows = qlen > 512 ? env_int("SWBANK_SEG", 256) : std::max(qlen, 1);
   R = env_int("SWBANK_R", R);
   RB = env_int("SWBANK_RB", RB);
+  if (seg_rows % R != 0 && seg_rows < qlen)
+    return fail(b, SW_ERR_ARG, "segment rows %d not a multiple of R=%d", seg_rows, R);
   // the HDL column-0 rule differs from the plain recurrence only if a match pays for a gap
   const int col0 = (!gotoh && smax > o + e) ? 1 : 0;
   if (!swk_has_variant(R, RB, col0, prof, gotoh ? 1 : 0))
     return fail(b, SW_ERR_UNSUPPORTED, "no kernel variant R=%d RB=%d col0=%d prof=%d gotoh=%d", R,
                 RB, col0, prof, (int)gotoh);
-  const int W = std::max(1, (qlen + R - 1) / R);
-  if (W * 64 > (R >= 64 ? 512 : 1024))
-    return fail(b, SW_ERR_UNSUPPORTED, "query length %d too long for one bank", qlen);
+  const int Wseg = std::max(1, (seg_rows + R - 1) / R);
+  if (Wseg * 64 > (R >= 64 ? 512 : 1024))
+    return fail(b, SW_ERR_UNSUPPORTED, "segment of %d rows too tall for one workgroup", seg_rows);
 
+  // per segment: LUT words (W*R) or a query profile ((A+1) x PS bytes), concatenated
   std::vector<uint32_t> tab;
-  uint32_t PS = 0, pad = 4, nv = 0;
-  if (!prof) {
-    tab.assign((size_t)W * R, 0xFFFFFFFFu);
-    for (int i = 0; i < qlen; ++i) {
-      uint32_t w = 0;
-      for (int c = 0; c < 4; ++c) w |= (uint32_t)(uint8_t)(S - m[b->query[i] * A + c]) << (8 * c);
-      tab[i] = w;
+  std::vector<sw_bank::Seg> segs;
+  const uint32_t PS = prof ? (uint32_t)((Wseg * R + 15) / 16 * 16) : 0;
+  const uint32_t pad = prof ? (uint32_t)A : 4u;  // profile letter A = padding row (all 0xFF)
+  const uint32_t nv = prof ? 0u : (uint32_t)(uint8_t)(S - sN) * 0x01010101u;
+  for (int r0 = 0; r0 < std::max(qlen, 1); r0 += seg_rows) {
+    const int rows = std::min(seg_rows, std::max(qlen, 1) - r0);
+    const int W = std::max(1, (rows + R - 1) / R);
+    segs.push_back({W, tab.size()});
+    if (!prof) {
+      const size_t base = tab.size();
+      tab.resize(base + (size_t)W * R, 0xFFFFFFFFu);
+      for (int i = 0; i < rows && r0 + i < qlen; ++i) {
+        uint32_t w = 0;
+        for (int c = 0; c < 4; ++c)
+          w |= (uint32_t)(uint8_t)(S - m[b->query[r0 + i] * A + c]) << (8 * c);
+        tab[base + i] = w;
+      }
+    } else {
+      std::vector<uint8_t> qp((size_t)(A + 1) * PS, 0xFF);
+      for (int c = 0; c < A; ++c)
+        for (int i = 0; i < rows && r0 + i < qlen; ++i)
+          qp[(size_t)c * PS + i] = (uint8_t)(S - m[b->query[r0 + i] * A + c]);
+      const size_t base = tab.size();
+      tab.resize(base + qp.size() / 4);
+      std::memcpy(tab.data() + base, qp.data(), qp.size());
     }
-    nv = (uint32_t)(uint8_t)(S - sN) * 0x01010101u;
-  } else {
-    PS = (uint32_t)((W * R + 15) / 16 * 16);
-    pad = (uint32_t)A;  // letter A = padding row (all 0xFF)
-    std::vector<uint8_t> qp((size_t)(A + 1) * PS, 0xFF);
-    for (int c = 0; c < A; ++c)
-      for (int i = 0; i < qlen; ++i)
-        qp[(size_t)c * PS + i] = (uint8_t)(S - m[b->query[i] * A + c]);
-    tab.resize(qp.size() / 4);
-    std::memcpy(tab.data(), qp.data(), qp.size());
   }
   HIPOK(b, hipSetDevice(b->device));
   HIPOK(b, b->qtab.reserve(tab.size()));
@@ -293,7 +311,8 @@ static sw_status prepare(sw_bank* b) {
   HIPOK(b, hipStreamSynchronize(b->stream));
   b->R = R;
   b->RB = RB;
-  b->W = W;
+  b->W = segs[0].W;
+  b->segs = segs;
   b->S = (uint32_t)S;
   b->O = (uint32_t)o;
   b->E = (uint32_t)e;
@@ -318,7 +337,8 @@ static sw_status range_check(sw_bank* b, uint32_t max_len) {
 }
 
 static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
-                        const uint32_t* d_lens, size_t n, int32_t* d_scores, hipStream_t st) {
+                        const uint32_t* d_lens, size_t n, uint32_t max_len, int32_t* d_scores,
+                        hipStream_t st) {
   sw_bank::Ev ev{};
   if (b->timing) {
     HIPOK(b, hipEventCreate(&ev.a));
@@ -329,10 +349,23 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   // no separate feeder kernel: the score kernel streams the codes itself, so the "pack"
   // interval (a..b) is empty and kept only for ABI stability
   if (b->timing) HIPOK(b, hipEventRecord(ev.b, st));
-  HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof,
-                            b->cfg.gap_model == SW_GAP_GOTOH ? 1 : 0, d_res, d_offs, d_lens, n,
-                            b->qtab.p, b->nv, b->S, b->O, b->E, b->PS, b->pad, b->W, d_scores,
-                            st));
+  const size_t nseg = b->segs.size();
+  const uint32_t ecols = (max_len + 7) / 8 * 8;
+  if (nseg > 1) {
+    const size_t ntiles = (n + SWB_TILE - 1) / SWB_TILE;
+    const size_t words = std::max<size_t>(1, ntiles * ecols * 64);
+    HIPOK(b, b->edge[0].reserve(words));
+    HIPOK(b, b->edge[1].reserve(words));
+  }
+  for (size_t s = 0; s < nseg; ++s) {
+    const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
+    void* eout = s + 1 < nseg ? b->edge[s & 1].p : nullptr;
+    HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof,
+                              b->cfg.gap_model == SW_GAP_GOTOH ? 1 : 0, d_res, d_offs, d_lens, n,
+                              b->qtab.p + b->segs[s].off, b->nv, b->S, b->O, b->E, b->PS,
+                              b->pad, b->segs[s].W, d_scores, ein, eout, ecols, s > 0 ? 1 : 0,
+                              st));
+  }
   if (b->timing) {
     HIPOK(b, hipEventRecord(ev.c, st));
     b->events.push_back(ev);
@@ -351,7 +384,7 @@ extern "C" sw_status sw_score_batch_device(sw_bank* b, const uint8_t* d_res,
   if (st != SW_OK) return st;
   if ((st = range_check(b, max_len)) != SW_OK) return st;
   HIPOK(b, hipSetDevice(b->device));
-  return launch(b, d_res, d_offs, d_lens, n, d_scores,
+  return launch(b, d_res, d_offs, d_lens, n, max_len, d_scores,
                 stream ? reinterpret_cast<hipStream_t>(stream) : b->stream);
 }
 
@@ -399,7 +432,7 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const u
   HIPOK(b, hipMemcpyAsync(b->res.p, hres.data(), hres.size(), hipMemcpyHostToDevice, b->stream));
   HIPOK(b, hipMemcpyAsync(b->offs.p, hoffs.data(), n * 8, hipMemcpyHostToDevice, b->stream));
   HIPOK(b, hipMemcpyAsync(b->lens.p, hlens.data(), n * 4, hipMemcpyHostToDevice, b->stream));
-  st = launch(b, b->res.p, b->offs.p, b->lens.p, n, b->scores.p, b->stream);
+  st = launch(b, b->res.p, b->offs.p, b->lens.p, n, max_len, b->scores.p, b->stream);
   if (st != SW_OK) return st;
   std::vector<int32_t> sorted(n);
   HIPOK(b, hipMemcpyAsync(sorted.data(), b->scores.p, n * 4, hipMemcpyDeviceToHost, b->stream));

@@ -2,8 +2,9 @@
 #ifndef SWBANK_INTERNAL_H
 #define SWBANK_INTERNAL_H
 
-/* Longest query one bank holds resident: 16 waves x 32 rows (or 8 x 64). */
-#define SWB_MAX_QUERY 512u
+/* Longest query a bank accepts; past 512 rows it runs as segments of SWBANK_SEG rows whose
+ * bottom rows are handed on through HBM. */
+#define SWB_MAX_QUERY 8192u
 /* Targets per workgroup tile: 64 lanes x 2 packed u16 halves (the PE "toggle" pair). */
 #define SWB_TILE 128
 /* Selector byte that reads 0xFF from v_perm_b32 (padding: substitution = S - 255 < 0). */

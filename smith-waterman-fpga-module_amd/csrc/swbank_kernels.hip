@@ -186,13 +186,33 @@ struct ScoreArgs {
   uint32_t S, O, E;       // shift (>= max s), -gap_open, -gap_extend
   uint32_t PS;            // PROF: profile row stride in bytes (multiple of 16, >= W*R)
   uint32_t pad;           // code used past a target's end (LUT: 4 = N; PROF: alpha = 0xFF row)
-  int32_t* scores;
+  int32_t* scores;        // out; with `accum` also in (best of the previous query segments)
+  // Query segments (queries longer than one workgroup's rows): the bottom row {H~, G/F} of
+  // the previous segment comes in through edge_in, this segment's goes out through edge_out;
+  // layout [tile][ecols][64 lanes] uint2 (coalesced 512 B per column).
+  const uint2* edge_in;
+  uint2* edge_out;
+  uint32_t ecols;
+  uint32_t accum;
 };
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef __attribute__((address_space(1))) void* glob_void_ptr;
+
+// 4 KB (8 columns x 64 lanes x uint2) global -> LDS by one wave: 4 LDS-DMA instructions of
+// 16 B per lane, lane-linear (the source layout is already [col][lane]).
+__device__ __forceinline__ void dma_edge_chunk(const uint2* src, uint2* dst, int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    __builtin_amdgcn_global_load_lds((glob_void_ptr)(src + q * 128 + lane * 2),
+                                     (lds_void_ptr)(dst + q * 128), 16, 0, 0);
+}
 
 // Score kernel: one workgroup = one tile of 128 targets x the whole query (W waves x R rows).
 // Wave w processes chunk c (8 columns) at phase c + w; one __syncthreads per phase orders the
 // LDS ring hand-off wave w -> w+1 (the RTL's PE-to-PE registers).
-// LDS: best[128] | edge[2][64] | ring[(W-1)][2][8][64] {H~, G or F} | PROF: profile
+// LDS: best[128] | bnd[64] | sink[8][64] | ein[2][8][64] (segments) |
+//      ring[(W-1)][2][8][64] {H~, G or F} | PROF: profile
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
   constexpr int C = 8;
@@ -200,9 +220,12 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int W = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
+  const bool seg_in = a.edge_in != nullptr, seg_out = a.edge_out != nullptr;
   uint32_t* bestsh = smem;                                   // 128 words
-  uint2* edge = reinterpret_cast<uint2*>(smem + SWB_TILE);   // 2 x 64: top boundary | sink
-  uint2* ring = edge + 128;
+  uint2* bnd = reinterpret_cast<uint2*>(smem + SWB_TILE);    // row -1 boundary {S, 0}
+  uint2* sink = bnd + 64;                                    // last wave's bottom row, 8 cols
+  uint2* ein = sink + C * 64;                                // previous segment, 2 x 8 cols
+  uint2* ring = ein + (seg_in ? 2 * C * 64 : 0);
   uint8_t* prof = reinterpret_cast<uint8_t*>(ring + (size_t)(W > 1 ? W - 1 : 0) * 2 * C * 64);
 
   const int tile = blockIdx.x;
@@ -216,7 +239,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   if (wave == 0) {
     bestsh[lane] = 0;
     bestsh[lane + 64] = 0;
-    edge[lane] = make_uint2(S | (S << 16), 0u);  // row -1: H~ = S, G/F = 0
+    bnd[lane] = make_uint2(S | (S << 16), 0u);  // row -1: H~ = S, G/F = 0
+    if (seg_in)  // the previous segment's bottom row of chunk 0
+      dma_edge_chunk(a.edge_in + (size_t)tile * a.ecols * 64, ein, lane);
   }
   uint32_t nv = a.nv;
   uint32_t tab[PROF ? 1 : R];
@@ -251,10 +276,11 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   load_raw(cur, 0, nfull > 0, a.pad, rlo, rhi);
   __syncthreads();
 
-  // branch-free hand-off: wave 0 reads the constant top boundary, the last wave writes into a
-  // sink, both with column stride 0 (branches here split the column loop into blocks and LLVM
-  // then sinks the H updates across columns, blowing up register pressure)
-  const int istride = wave > 0 ? 64 : 0, ostride = wave < W - 1 ? 64 : 0;
+  // branch-free hand-off: wave 0 reads the top boundary (constant, stride 0, or the previous
+  // segment's row), the last wave writes into an LDS sink (branches inside the column loop
+  // split it into blocks and LLVM then sinks the H updates across columns, blowing up
+  // register pressure)
+  const int istride = (wave > 0 || seg_in) ? 64 : 0, ostride = (wave < W - 1 || seg_out) ? 64 : 0;
   const uint32_t pbase = (uint32_t)wave * R;
   const uint32_t padc = a.pad;
   const int nph = nch + W - 1;
@@ -264,10 +290,13 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       const uint2 clo = rlo, chi = rhi;
       if (c + 1 < nch) load_raw(cur, c + 1, c + 1 < nfull, a.pad, rlo, rhi);
       const int slot = c & 1;
+      if (seg_in && wave == 0 && c + 1 < nch)  // prefetch the next chunk's boundary row
+        dma_edge_chunk(a.edge_in + ((size_t)tile * a.ecols + (size_t)(c + 1) * C) * 64,
+                       ein + (size_t)((c + 1) & 1) * C * 64, lane);
       const uint2* rin = wave > 0 ? ring + ((size_t)((wave - 1) * 2 + slot) * C) * 64 + lane
-                                  : edge + lane;
+                                  : (seg_in ? ein + (size_t)slot * C * 64 : bnd) + lane;
       uint2* rout = wave < W - 1 ? ring + ((size_t)(wave * 2 + slot) * C) * 64 + lane
-                                 : edge + 64 + lane;
+                                 : sink + lane;
       uint2 rv = rin[0];
 #pragma unroll
       for (int jj = 0; jj < C; ++jj) {
@@ -320,6 +349,11 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         asm volatile("" : "+v"(best));
         rout[jj * ostride] = make_uint2(as_u32(Hl[R - 1]), as_u32(upX));
       }
+      if (seg_out && wave == W - 1) {  // this segment's bottom row -> the next segment
+        uint2* dst = a.edge_out + ((size_t)tile * a.ecols + (size_t)c * C) * 64 + lane;
+#pragma unroll
+        for (int jj = 0; jj < C; ++jj) dst[jj * 64] = sink[jj * 64 + lane];
+      }
     }
     __syncthreads();
   }
@@ -328,15 +362,22 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   atomicMax(&bestsh[lane + 64], (uint32_t)best.y);
   __syncthreads();
   if (wave == 0) {
-    if (tlo < n) a.scores[tlo] = (int32_t)bestsh[lane];
-    if (thi < n) a.scores[thi] = (int32_t)bestsh[lane + 64];
+    int32_t blo = (int32_t)bestsh[lane], bhi = (int32_t)bestsh[lane + 64];
+    if (a.accum) {  // best over the previous query segments
+      if (tlo < n) blo = max(blo, a.scores[tlo]);
+      if (thi < n) bhi = max(bhi, a.scores[thi]);
+    }
+    if (tlo < n) a.scores[tlo] = blo;
+    if (thi < n) a.scores[thi] = bhi;
   }
 }
 
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH>
 static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st) {
   const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE;
-  const size_t lds = SWB_TILE * 4 + (size_t)(128 + (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8 +
+  const size_t lds = SWB_TILE * 4 +
+                     (size_t)(64 + 8 * 64 + (a.edge_in ? 2 * 8 * 64 : 0) +
+                              (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8 +
                      (PROF ? prof_bytes : 0);
   auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH>;
   static bool attr_set = false;
@@ -376,9 +417,12 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        const uint32_t* lens, size_t n, const uint32_t* qtab,
                                        uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
-                                       hipStream_t st) {
+                                       const void* edge_in, void* edge_out, uint32_t ecols,
+                                       int accum, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores};
+  const swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
+                         O,    E,    PS,   pad, scores, static_cast<const uint2*>(edge_in),
+                         static_cast<uint2*>(edge_out), ecols, (uint32_t)accum};
   const uint32_t prof_bytes = (pad + 1) * PS;
 #define SWK_CASE(RR, BB, C0, PF, GT)                                                   \
   if (R == RR && RB == BB && col0 == C0 && prof == PF && gotoh == GT)                  \

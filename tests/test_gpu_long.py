@@ -1,0 +1,85 @@
+"""GPU parity for long queries: past 512 rows the query runs as segments of SWBANK_SEG rows
+whose bottom rows are handed on through HBM (LDS-DMA in, plain stores out)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import swbank as S
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_case(rng, qlen, ntargets, maxlen, p_n=0.02):
+    q = rng.integers(0, 4, qlen, dtype=np.uint8)
+    q[rng.random(qlen) < p_n] = 4
+    seqs = []
+    for _ in range(ntargets):
+        t = rng.integers(0, 4, int(rng.integers(0, maxlen + 1)), dtype=np.uint8)
+        t[rng.random(len(t)) < p_n] = 4
+        seqs.append(t)
+    return q, seqs
+
+
+@pytest.mark.parametrize("model", [S.GAP_MERGED, S.GAP_GOTOH])
+@pytest.mark.parametrize("qlen", [513, 700, 1000, 2048])
+def test_long_query_dna_vs_oracle(model, qlen):
+    rng = np.random.default_rng(qlen + model)
+    q, seqs = _random_case(rng, qlen, 140, 400)
+    for k in range(0, 140, 5):
+        a = int(rng.integers(0, qlen - 300))
+        seqs[k] = q[a:a + int(rng.integers(50, 300))].copy()
+        seqs[k][::9] = rng.integers(0, 4, len(seqs[k][::9]))
+    with S.ScoreBank(gap_model=model) as bank:
+        bank.set_penalties(5, -4, -10, -1)
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -10, -1, model)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), int(lens[i]), int(got[i]), int(want[i])) for i in bad[:8]]
+
+
+@pytest.mark.parametrize("seg", ["64", "128", "512"])
+def test_long_query_segment_sizes_agree(seg, monkeypatch):
+    rng = np.random.default_rng(3)
+    q, seqs = _random_case(rng, 900, 200, 200)
+    monkeypatch.setenv("SWBANK_SEG", seg)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(5, -4, -12, -4)
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    assert (got == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
+
+
+def test_long_query_protein_col0_rule():
+    """merged model, BLOSUM62 with -2/-1: max(s)=11 > o+e, so the HDL column-0 rule is live in
+    every segment."""
+    rng = np.random.default_rng(12)
+    q = rng.integers(0, 20, 800, dtype=np.uint8)
+    seqs = [rng.integers(0, 20, int(rng.integers(1, 300)), dtype=np.uint8) for _ in range(130)]
+    with S.ScoreBank(alphabet=S.ALPHABET_PROTEIN) as bank:
+        bank.set_matrix(O.BLOSUM62, -2, -1)
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    assert (got == O.score_batch(q, res, offs, lens, O.BLOSUM62, -2, -1)).all()
+
+
+def test_generated_golden_swapped_orientation():
+    """configs[3] orientation the bench uses: the 1-kbp target as the bank query, the 150-bp
+    read as the batch.  Both gap models are symmetric under transposition at these parameters
+    (no column-0 rule in play), so the fixture scores must come back unchanged."""
+    cases = {c["name"]: c for c in
+             json.load(open(os.path.join(O.GOLDEN, "generated.json")))["cases"]}
+    for name, model in (("dna150x1000_merged", S.GAP_MERGED),
+                        ("dna150x1000_gotoh_10_1", S.GAP_GOTOH)):
+        c = cases[name]
+        with S.ScoreBank(gap_model=model) as bank:
+            bank.set_penalties(*c["match_mismatch"], c["gap_open"], c["gap_extend"])
+            for t, want in zip(c["targets"][:12], c["scores"][:12]):
+                bank.load_query(S.encode(t))
+                assert bank.score_targets([S.encode(c["query"])]).tolist() == [want]
