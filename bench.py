@@ -1,15 +1,22 @@
 #!/usr/bin/env python3
 """bench.py — GCUPS of the MI355X Smith-Waterman score bank (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2], the 1-GPU GCUPS config; north_star "100 bp x 500 bp
-batches"): the reference query ``data/query100.fa`` (128 bp, committed as a fixture) scored
-against a data500-shaped batch — ``--reps`` copies of 499 synthetic, seeded, uniform ACGT
-128-bp targets per GPU (``data/generate.py:6-23`` shape; splitmix64, seed 1000+rank).
+Default workload (BASELINE.json configs[2], the 1-GPU GCUPS config; north_star "100 bp x
+500 bp batches"): the reference query ``data/query100.fa`` (128 bp, committed as a fixture)
+scored against a data500-shaped batch — ``--reps`` copies of 499 synthetic, seeded, uniform
+ACGT 128-bp targets per GPU (``data/generate.py:6-23`` shape; splitmix64, seed 1000+rank).
 Penalties 5/-4/-12/-4 (data/smith-waterman.py:6-10), merged gap model (the ScoreBank PE).
 
-A step = one pass of the hot path over the batch: feeder (pack) kernel + score kernel on
-inputs already resident in HBM, plus — at N>1 — the RCCL gather of the int32 score vector
-to rank 0 (the only collective; pairs are sharded, scaling is weak).
+Other workloads (``--workload``), same JSON line:
+  reads150x1k    configs[3]: per GPU ``--reads`` synthetic 150-bp reads x a fixed slice of
+                 ``--slice`` 1-kbp targets (every read x every target of the slice); each
+                 1-kbp target is the bank query (4 segments of 256 rows), the reads the batch.
+  protein512x1k  configs[4]: a 512-aa query x ``--ptargets`` 1-kaa targets per GPU,
+                 BLOSUM62, gap -11/-1, Gotoh (ssearch36 semantics), uniform 20-letter residues.
+
+A step = one pass of the hot path over the batch (score kernel launches) on inputs already
+resident in HBM, plus — at N>1 — the RCCL gather of the int32 score vector to rank 0 (the
+only collective; pairs are sharded, scaling is weak).
 
 Launch: ``python bench.py [--gpus N --steps K --warmup W]``; for N>1 under
 ``torch.distributed.run`` (one process per GPU, RCCL).  Rank 0 prints ONE JSON line.
@@ -32,7 +39,8 @@ sys.path.insert(0, REPO)
 CUS, SIMD_PER_CU, LANES_PER_SIMD_CLK, CLK_GHZ = 256, 4, 32, 2.4
 VALU_PEAK_TOPS_U16 = CUS * SIMD_PER_CU * LANES_PER_SIMD_CLK * 2 * CLK_GHZ / 1e3  # 157.3
 HBM_PEAK_GBS = 8000.0
-OPS_PER_CELL = 10  # 1 select, 6 max, 3 add per cell of the §8.0 recurrence
+# integer ops per cell — merged: 1 select, 6 max, 3 add; Gotoh: 11
+OPS_PER_CELL = {"merged": 10, "gotoh": 11}
 PEN = (5, -4, -12, -4)
 
 
@@ -41,9 +49,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="q100xdata500",
+                    choices=["q100xdata500", "reads150x1k", "protein512x1k"])
     ap.add_argument("--reps", type=int, default=2048,
-                    help="copies of the 499-target data500 batch per GPU")
+                    help="q100xdata500: copies of the 499-target data500 batch per GPU")
     ap.add_argument("--target-len", type=int, default=128)
+    ap.add_argument("--reads", type=int, default=131072, help="reads150x1k: reads per GPU")
+    ap.add_argument("--slice", type=int, default=16, help="reads150x1k: 1-kbp targets")
+    ap.add_argument("--ptargets", type=int, default=12500, help="protein512x1k: per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="wall budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--profile-only", action="store_true",
@@ -56,10 +69,10 @@ def load_query():
     return encode_dna(read_fasta(golden_fasta("query100.fa"))[0][1])
 
 
-def make_targets(seed: int, n: int, L: int) -> np.ndarray:
-    """n x L uniform ACGT codes from a splitmix64 stream (same generator as the tests)."""
+def make_codes(seed: int, n: int, L: int, alpha: int = 4) -> np.ndarray:
+    """n x L uniform codes from a splitmix64 stream (same generator as the tests)."""
     from oracle.oracle import random_codes
-    return random_codes(seed, n * L, 4).reshape(n, L)
+    return random_codes(seed, n * L, alpha).reshape(n, L)
 
 
 def pmc_traffic(workload: str):
@@ -72,6 +85,68 @@ def pmc_traffic(workload: str):
     except (OSError, ValueError):
         pass
     return None
+
+
+class Workload:
+    """One rank's share: a list of (bank, query) jobs over one resident batch."""
+
+    def __init__(self, args, rank, dev, S, torch):
+        self.args = args
+        w = args.workload
+        if w == "q100xdata500":
+            q = load_query()
+            n, L = 499 * args.reps, args.target_len
+            self.batch = make_codes(1000 + rank, n, L)
+            self.queries = [q]
+            self.bank = S.ScoreBank(device=dev.index)
+            self.bank.set_penalties(*PEN)
+            self.model = "merged"
+            self.name = f"query100x{n}x{L}"
+            self.desc = (f"query100.fa (128 bp) x data500-shaped batch: {args.reps} x 499 "
+                         f"synthetic {L}-bp ACGT targets per GPU (BASELINE configs[2])")
+            self.params = {"penalties": list(PEN), "gap_model": "merged (ScoreBank PE)"}
+        elif w == "reads150x1k":
+            n, L = args.reads, 150
+            self.batch = make_codes(2000 + rank, n, L)
+            self.queries = list(make_codes(77, args.slice, 1000))  # the fixed 1-kbp slice
+            self.bank = S.ScoreBank(device=dev.index)
+            self.bank.set_penalties(*PEN)
+            self.model = "merged"
+            self.name = f"reads150x{n}x1k{args.slice}"
+            self.desc = (f"{n} synthetic 150-bp reads per GPU x a slice of {args.slice} "
+                         f"synthetic 1-kbp targets (BASELINE configs[3]); target = bank query "
+                         f"(4 x 256-row segments), reads = batch")
+            self.params = {"penalties": list(PEN), "gap_model": "merged (ScoreBank PE)"}
+        else:
+            n, L = args.ptargets, 1000
+            self.batch = make_codes(3000 + rank, n, L, 20)
+            self.queries = [make_codes(99, 1, 512, 20)[0]]
+            self.bank = S.ScoreBank(device=dev.index, alphabet=S.ALPHABET_PROTEIN,
+                                    gap_model=S.GAP_GOTOH)
+            from oracle.oracle import BLOSUM62
+            self.bank.set_matrix(BLOSUM62, -11, -1)
+            self.model = "gotoh"
+            self.name = f"protein512x{n}x1k"
+            self.desc = (f"512-aa query x {n} synthetic 1-kaa targets per GPU, BLOSUM62, "
+                         f"gap -11/-1, Gotoh (BASELINE configs[4])")
+            self.params = {"matrix": "BLOSUM62", "gap_open": -11, "gap_extend": -1,
+                           "gap_model": "gotoh (ssearch36)"}
+        self.n, self.L = n, L
+        self.d_res = torch.from_numpy(self.batch.reshape(-1)).to(dev)
+        self.d_offs = torch.arange(n, dtype=torch.int64, device=dev) * L
+        self.d_lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+        self.d_sc = torch.zeros((len(self.queries), n), dtype=torch.int32, device=dev)
+        if len(self.queries) == 1:
+            self.bank.load_query(self.queries[0])
+        self.cells = sum(len(q) for q in self.queries) * n * L
+
+    def run(self, stream):
+        for k, q in enumerate(self.queries):
+            if len(self.queries) > 1:
+                self.bank.load_query(q)  # ld_sequence: a new query for the same batch
+            self.bank.score_batch_device(self.d_res.data_ptr(), self.d_offs.data_ptr(),
+                                         self.d_lens.data_ptr(), self.n, self.L,
+                                         self.d_sc[k].data_ptr(), stream)
 
 
 def main():
@@ -91,34 +166,23 @@ def main():
 
     import swbank as S
 
-    q = load_query()
-    n = 499 * args.reps
-    L = args.target_len
-    tg = make_targets(1000 + rank, n, L)
-    d_res = torch.from_numpy(tg.reshape(-1)).to(dev)
-    d_offs = torch.arange(n, dtype=torch.int64, device=dev) * L
-    d_lens = torch.full((n,), L, dtype=torch.int32, device=dev)
-    d_sc = torch.zeros(n, dtype=torch.int32, device=dev)
-    gather = [torch.empty_like(d_sc) for _ in range(world)] if (world > 1 and rank == 0) else None
-
-    bank = S.ScoreBank(device=dev.index)
-    bank.set_penalties(*PEN)
-    bank.load_query(q)
+    wl = Workload(args, rank, dev, S, torch)
+    gather = ([torch.empty_like(wl.d_sc) for _ in range(world)]
+              if (world > 1 and rank == 0) else None)
     stream = torch.cuda.current_stream()
 
     def step():
-        bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,
-                                d_sc.data_ptr(), stream.cuda_stream)
+        wl.run(stream.cuda_stream)
         if world > 1:
-            dist.gather(d_sc, gather_list=gather, dst=0)
+            dist.gather(wl.d_sc, gather_list=gather, dst=0)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    bank.timing()  # drop warmup events
-    bank.set_timing(True)
+    wl.bank.timing()  # drop warmup events
+    wl.bank.set_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -126,15 +190,15 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    bank.set_timing(False)
-    launches, pack_ms, score_ms = bank.timing()
+    wl.bank.set_timing(False)
+    launches, pack_ms, score_ms = wl.bank.timing()
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    cells_rank = n * L * len(q)
+    cells_rank = wl.cells
     value = world * cells_rank * args.steps / elapsed / 1e9
     if args.profile_only:
         if rank == 0:
@@ -143,12 +207,16 @@ def main():
             dist.destroy_process_group()
         return
 
-    score_s = score_ms / max(launches, 1) / 1e3
-    pack_s = pack_ms / max(launches, 1) / 1e3
-    workload = f"query100x{n}x{L}"
-    achieved_tops = OPS_PER_CELL * cells_rank / score_s / 1e12
-    alg_bytes = n * (L + 4) + len(q)  # 1 B per residue read once + 4 B per score written
-    traffic = pmc_traffic(workload)
+    # score-kernel time per step (one "launch" = one sw_score_batch_device call, which may
+    # run several segment kernels for long queries)
+    calls_per_step = len(wl.queries)
+    score_s = score_ms / max(launches, 1) / 1e3 * calls_per_step
+    pack_s = pack_ms / max(launches, 1) / 1e3 * calls_per_step
+    ops = OPS_PER_CELL[wl.model]
+    achieved_tops = ops * cells_rank / score_s / 1e12
+    # algorithmic bytes: 1 B per residue read once per query + 4 B per score written
+    alg_bytes = len(wl.queries) * wl.n * (wl.L + 4) + sum(len(q) for q in wl.queries)
+    traffic = pmc_traffic(wl.name)
 
     out = {
         "metric": "GCUPS",
@@ -164,13 +232,12 @@ def main():
         "dtype": "u16",
         "data": "synthetic",
         "config": {
-            "workload": f"query100.fa (128 bp) x data500-shaped batch: {args.reps} x 499 "
-                        f"synthetic {L}-bp ACGT targets per GPU (BASELINE configs[2])",
-            "query_len": int(len(q)),
-            "targets_per_gpu": n,
-            "target_len": L,
-            "penalties": list(PEN),
-            "gap_model": "merged (ScoreBank PE)",
+            "workload": wl.desc,
+            "query_len": [int(len(q)) for q in wl.queries][:1][0],
+            "queries": len(wl.queries),
+            "targets_per_gpu": wl.n,
+            "target_len": wl.L,
+            **wl.params,
             "parallelism": f"dp{world}: pairs sharded, RCCL gather of scores to rank 0",
         },
         "kernel_ms": {"pack": round(pack_s * 1e3, 4), "score": round(score_s * 1e3, 4)},
@@ -178,7 +245,7 @@ def main():
             "bound": "valu",
             "achieved": round(achieved_tops, 2),
             "peak": round(VALU_PEAK_TOPS_U16, 1),
-            "unit": "Tops/s (u16 int ops, 10 per cell)",
+            "unit": f"Tops/s (u16 int ops, {ops} per cell)",
             "frac": round(achieved_tops / VALU_PEAK_TOPS_U16, 4),
             "traffic": traffic,
         },
@@ -193,12 +260,13 @@ def main():
         "cpu_baseline": None,
     }
 
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"], out["parity_sample"] = cpu_baseline(q, tg, d_sc, L, args.cpu_seconds)
+    if rank == 0 and world == 1 and args.cpu_seconds > 0 and args.workload == "q100xdata500":
+        out["cpu_baseline"], out["parity_sample"] = cpu_baseline(
+            wl.queries[0], wl.batch, wl.d_sc[0], wl.L, args.cpu_seconds)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
-    bank.close()
+    wl.bank.close()
     if world > 1:
         dist.destroy_process_group()
 

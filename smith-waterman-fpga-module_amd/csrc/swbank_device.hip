@@ -17,6 +17,11 @@
 #include "swbank_internal.h"
 
 extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh);
+extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, const uint8_t* res,
+                                      const uint64_t* offs, const uint32_t* lens, size_t n,
+                                      const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
+                                      uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
+                                      hipStream_t st);
 extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh,
                                        const uint8_t* res, const uint64_t* offs,
                                        const uint32_t* lens, size_t n, const uint32_t* qtab,
@@ -79,6 +84,10 @@ struct sw_bank {
   struct Seg { int W; size_t off; };  // rows = W*R (last may be shorter), qtab word offset
   std::vector<Seg> segs;
   DevBuf<uint2> edge[2];  // bottom rows handed from segment to segment
+  // wave kernel (few targets, query <= 1024 rows): lane l owns rows [lK, lK+K)
+  int wK = 0;              // 0: query too long for the wave kernel
+  uint32_t wPS = 0;
+  DevBuf<uint32_t> wtab;   // LUT: 64K row words | PROF: (A+1) x 64K profile bytes
 
   // workspaces
   DevBuf<uint8_t> res;
@@ -169,6 +178,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   double pm, sm;
   (void)sw_bank_timing(b, &nl, &pm, &sm);
   b->qtab.release();
+  b->wtab.release();
   b->edge[0].release();
   b->edge[1].release();
   b->res.release();
@@ -304,7 +314,36 @@ static sw_status prepare(sw_bank* b) {
       std::memcpy(tab.data() + base, qp.data(), qp.size());
     }
   }
+  // wave-kernel layout of the same query (rows padded to 64K)
+  std::vector<uint32_t> wt;
+  int wK = qlen <= 256 ? 4 : qlen <= 512 ? 8 : qlen <= 1024 ? 16 : 0;
+  uint32_t wPS = 0;
+  if (wK) {
+    const int rows = 64 * wK;
+    if (!prof) {
+      wt.assign((size_t)rows, 0xFFFFFFFFu);
+      for (int i = 0; i < qlen; ++i) {
+        uint32_t w = 0;
+        for (int c = 0; c < 4; ++c) w |= (uint32_t)(uint8_t)(S - m[b->query[i] * A + c]) << (8 * c);
+        wt[i] = w;
+      }
+    } else {
+      wPS = (uint32_t)rows;
+      std::vector<uint8_t> qp((size_t)(A + 1) * wPS, 0xFF);
+      for (int c = 0; c < A; ++c)
+        for (int i = 0; i < qlen; ++i) qp[(size_t)c * wPS + i] = (uint8_t)(S - m[b->query[i] * A + c]);
+      wt.resize(qp.size() / 4);
+      std::memcpy(wt.data(), qp.data(), qp.size());
+    }
+  }
   HIPOK(b, hipSetDevice(b->device));
+  if (wK) {
+    HIPOK(b, b->wtab.reserve(wt.size()));
+    HIPOK(b, hipMemcpyAsync(b->wtab.p, wt.data(), wt.size() * 4, hipMemcpyHostToDevice,
+                            b->stream));
+  }
+  b->wK = wK;
+  b->wPS = wPS;
   HIPOK(b, b->qtab.reserve(tab.size()));
   HIPOK(b, hipMemcpyAsync(b->qtab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice,
                           b->stream));
@@ -351,13 +390,25 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   if (b->timing) HIPOK(b, hipEventRecord(ev.b, st));
   const size_t nseg = b->segs.size();
   const uint32_t ecols = (max_len + 7) / 8 * 8;
-  if (nseg > 1) {
-    const size_t ntiles = (n + SWB_TILE - 1) / SWB_TILE;
+  const size_t ntiles = (n + SWB_TILE - 1) / SWB_TILE;
+  // Kernel choice: the tile kernel needs many 128-target tiles to fill 256 CUs (each tile is
+  // one workgroup of W waves); with few targets the wave kernel (one wave per 2 targets,
+  // lanes = query rows) has 64x more parallelism.  SWBANK_KERNEL=tile|wave forces one.
+  const char* kforce = std::getenv("SWBANK_KERNEL");
+  bool use_wave = b->wK > 0 && ntiles * (size_t)b->segs[0].W < 4096;
+  if (kforce && std::strcmp(kforce, "tile") == 0) use_wave = false;
+  if (kforce && std::strcmp(kforce, "wave") == 0 && b->wK > 0) use_wave = true;
+  if (use_wave) {
+    HIPOK(b, swk_launch_wave(b->wK, b->col0, b->prof, b->cfg.gap_model == SW_GAP_GOTOH ? 1 : 0,
+                             d_res, d_offs, d_lens, n, b->wtab.p, b->nv, b->S, b->O, b->E,
+                             b->wPS, b->pad, d_scores, st));
+  }
+  if (!use_wave && nseg > 1) {
     const size_t words = std::max<size_t>(1, ntiles * ecols * 64);
     HIPOK(b, b->edge[0].reserve(words));
     HIPOK(b, b->edge[1].reserve(words));
   }
-  for (size_t s = 0; s < nseg; ++s) {
+  for (size_t s = 0; !use_wave && s < nseg; ++s) {
     const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
     void* eout = s + 1 < nseg ? b->edge[s & 1].p : nullptr;
     HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof,

@@ -392,6 +392,191 @@ static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, h
   return hipGetLastError();
 }
 
+// ========================================================================================
+// Wave kernel: the north-star wavefront form, for batches with few targets (few tiles) and
+// queries up to 1024 rows.  One wave scores two targets (the u16 halves) against the whole
+// query; lane l owns query rows [lK, lK+K).  Step t: lane l computes column t - l for its K
+// rows (an anti-diagonal of K-row blocks across the wave); the bottom row {H~, G/F} and the
+// two target codes move one lane down per step with DPP wave_shr:1 (the RTL's M_out/I_out/
+// data_out from PE i to PE i+1); lane 0 takes row -1 = {S, 0} and the next codes of the
+// target stream.  A lane that has not reached column 0 yet (or is past the end) sees padding
+// codes and boundary inputs, which leave the boundary state unchanged — no masking needed.
+template <int K>
+struct ProfLookupK {
+  uint32_t lo[K / 4], hi[K / 4];
+  __device__ __forceinline__ u16x2 operator()(int r) const {
+    const uint32_t sel = (uint32_t)(r & 3) | ((uint32_t)(4 + (r & 3)) << 16) | 0x0C000C00u;
+    return as_u16x2(__builtin_amdgcn_perm(hi[r >> 2], lo[r >> 2], sel));
+  }
+};
+template <int K>
+struct LaneLutLookup {  // per-lane row LUTs (the lane's own query rows) in VGPRs
+  const uint32_t (&lut)[K];
+  uint32_t nv, selw;
+  __device__ __forceinline__ u16x2 operator()(int r) const {
+    return as_u16x2(__builtin_amdgcn_perm(nv, lut[r], selw));
+  }
+};
+
+// merged column with a per-lane column-0 mask (zmask = 0 in the lane's column 0)
+template <int R, int RB, class LK>
+__device__ __forceinline__ void column_merged_mask(const LK& lk, u16x2& diag, u16x2& upG,
+                                                   u16x2 (&Hl)[R], u16x2 (&Gl)[R], u16x2& best,
+                                                   u16x2 S2, u16x2 O2, u16x2 E2, uint32_t zmask) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const u16x2 p = lk(r);
+    const u16x2 M = vsubs(diag, p);
+    const u16x2 I = vsubs(vmax(upG, Gl[r]), E2);
+    const u16x2 Hn = vmax(M, I) + S2;
+    const u16x2 Gn = vmax(vsubs(M, O2), I);
+    best = vmax(best, M);
+    diag = Hl[r];
+    Hl[r] = Hn;
+    Gl[r] = Gn;
+    upG = as_u16x2(as_u32(Gn) & zmask);
+    if ((r % RB) == RB - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__device__ __forceinline__ uint32_t dpp_shr1(uint32_t lane0_value, uint32_t v) {
+  return __builtin_amdgcn_update_dpp(lane0_value, v, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+}
+
+// qtab (wave layout): LUT: 64*K row words | PROF: (pad+1) x PS bytes, PS = 64*K.
+template <int K, bool COL0, bool PROF, bool GOTOH>
+__global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
+  const int lane = threadIdx.x & 63;
+  if constexpr (PROF) {
+    const uint32_t words = (a.pad + 1) * a.PS / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+      reinterpret_cast<uint4*>(prof)[i] = src[i];
+    __syncthreads();
+  }
+  const size_t pair = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t tA = 2 * pair, tB = tA + 1;
+  const size_t n = a.n;
+  if (tA >= n) return;  // whole wave
+  const uint32_t LA = a.lens[tA], LB = tB < n ? a.lens[tB] : 0u;
+  const uint8_t* pA = a.res + (LA ? a.offs[tA] : 0);
+  const uint8_t* pB = a.res + (LB ? a.offs[tB] : 0);
+  const int Lmax = (int)__builtin_amdgcn_readfirstlane(max(LA, LB));
+  const uint32_t S = a.S, pad = a.pad;
+  const u16x2 S2 = {(unsigned short)S, (unsigned short)S};
+  const u16x2 O2 = {(unsigned short)a.O, (unsigned short)a.O};
+  const u16x2 E2 = {(unsigned short)a.E, (unsigned short)a.E};
+  const uint32_t oes = a.O + a.E + S;
+  const u16x2 OES2 = {(unsigned short)oes, (unsigned short)oes};
+  const uint32_t padsel = pad | (pad << 16) | 0x0C000C00u;
+
+  uint32_t lut[PROF ? 1 : K];
+  if constexpr (!PROF) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) lut[k] = a.qtab[lane * K + k];
+  }
+  const uint32_t nv = a.nv;
+  const uint8_t* prow = prof + lane * K;  // this lane's rows in every profile letter row
+
+  u16x2 Hl[K], Xl[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    Hl[k] = S2;
+    Xl[k] = (u16x2){0, 0};
+  }
+  u16x2 best = {0, 0};
+  u16x2 prevUpH = S2;
+  uint32_t botH = as_u32(S2), botX = 0u, let = padsel, buf = padsel;
+
+  const int nsteps = Lmax + 63;
+  for (int t = 0; t < nsteps; ++t) {
+    if ((t & 63) == 0) {  // next 64 columns of both targets, one code pair per lane
+      const uint32_t c = (uint32_t)t + lane;
+      const uint32_t x = c < LA ? (uint32_t)pA[c] : pad;
+      const uint32_t y = c < LB ? (uint32_t)pB[c] : pad;
+      buf = min(x, pad) | (min(y, pad) << 16) | 0x0C000C00u;
+    }
+    const uint32_t inj = __builtin_amdgcn_readlane(buf, t & 63);
+    const u16x2 upH = as_u16x2(dpp_shr1(as_u32(S2), botH));
+    u16x2 upX = as_u16x2(dpp_shr1(0u, botX));
+    let = dpp_shr1(inj, let);
+    u16x2 diag = prevUpH;
+    prevUpH = upH;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PROF) {
+      ProfLookupK<K> lk;
+      const uint32_t blo = let & 0xFFu, bhi = (let >> 16) & 0xFFu;
+      if constexpr (K == 4) {
+        lk.lo[0] = *reinterpret_cast<const uint32_t*>(prow + blo * a.PS);
+        lk.hi[0] = *reinterpret_cast<const uint32_t*>(prow + bhi * a.PS);
+      } else if constexpr (K == 8) {
+        const uint2 x = *reinterpret_cast<const uint2*>(prow + blo * a.PS);
+        const uint2 y = *reinterpret_cast<const uint2*>(prow + bhi * a.PS);
+        lk.lo[0] = x.x; lk.lo[1] = x.y; lk.hi[0] = y.x; lk.hi[1] = y.y;
+      } else {
+        const uint4 x = *reinterpret_cast<const uint4*>(prow + blo * a.PS);
+        const uint4 y = *reinterpret_cast<const uint4*>(prow + bhi * a.PS);
+        lk.lo[0] = x.x; lk.lo[1] = x.y; lk.lo[2] = x.z; lk.lo[3] = x.w;
+        lk.hi[0] = y.x; lk.hi[1] = y.y; lk.hi[2] = y.z; lk.hi[3] = y.w;
+      }
+      if constexpr (GOTOH) {
+        u16x2 uH = upH;
+        column_gotoh<K, 4>(lk, diag, uH, upX, Hl, Xl, best, S2, OES2, E2);
+      } else if constexpr (COL0) {
+        column_merged_mask<K, 4>(lk, diag, upX, Hl, Xl, best, S2, O2, E2,
+                                 t == lane ? 0u : 0xFFFFFFFFu);
+      } else {
+        column_merged<K, 4, false>(lk, diag, upX, Hl, Xl, best, S2, O2, E2);
+      }
+    } else {
+      const LaneLutLookup<K> lk{lut, nv, let};
+      if constexpr (GOTOH) {
+        u16x2 uH = upH;
+        column_gotoh<K, 4>(lk, diag, uH, upX, Hl, Xl, best, S2, OES2, E2);
+      } else if constexpr (COL0) {
+        column_merged_mask<K, 4>(lk, diag, upX, Hl, Xl, best, S2, O2, E2,
+                                 t == lane ? 0u : 0xFFFFFFFFu);
+      } else {
+        column_merged<K, 4, false>(lk, diag, upX, Hl, Xl, best, S2, O2, E2);
+      }
+    }
+    asm volatile("" : "+v"(best));
+    botH = as_u32(Hl[K - 1]);
+    botX = as_u32(upX);
+  }
+  // max over the wave's rows, per target
+  uint32_t bx = best.x, by = best.y;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    bx = max(bx, (uint32_t)__shfl_xor((int)bx, off));
+    by = max(by, (uint32_t)__shfl_xor((int)by, off));
+  }
+  if (lane == 0) {
+    a.scores[tA] = (int32_t)bx;
+    if (tB < n) a.scores[tB] = (int32_t)by;
+  }
+}
+
+template <int K, bool COL0, bool PROF, bool GOTOH>
+static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream_t st) {
+  const size_t pairs = (a.n + 1) / 2;
+  const size_t blocks = (pairs + 3) / 4;
+  const size_t lds = PROF ? prof_bytes : 0;
+  auto fn = &score_wave<K, COL0, PROF, GOTOH>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(256), (unsigned)lds, st, a);
+  return hipGetLastError();
+}
+
 }  // namespace swk
 
 // Variants compiled in: (R, RB, COL0, PROF, GOTOH).  The host picks R from the query length
@@ -429,5 +614,27 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
     return swk::launch_score<RR, BB, (C0 != 0), (PF != 0), (GT != 0)>(a, W, prof_bytes, st);
   SWK_VARIANTS(SWK_CASE)
 #undef SWK_CASE
+  return hipErrorInvalidValue;
+}
+
+#define SWK_WAVE_VARIANTS(X)                                                              \
+  X(4, 0, 0, 0) X(4, 1, 0, 0) X(4, 0, 0, 1) X(4, 0, 1, 0) X(4, 1, 1, 0) X(4, 0, 1, 1)     \
+  X(8, 0, 0, 0) X(8, 1, 0, 0) X(8, 0, 0, 1) X(8, 0, 1, 0) X(8, 1, 1, 0) X(8, 0, 1, 1)     \
+  X(16, 0, 0, 0) X(16, 1, 0, 0) X(16, 0, 0, 1) X(16, 0, 1, 0) X(16, 1, 1, 0) X(16, 0, 1, 1)
+
+extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, const uint8_t* res,
+                                      const uint64_t* offs, const uint32_t* lens, size_t n,
+                                      const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
+                                      uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
+                                      hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
+                         nullptr, nullptr, 0u, 0u};
+  const uint32_t prof_bytes = (pad + 1) * PS;
+#define SWK_WCASE(KK, C0, PF, GT)                                                  \
+  if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                          \
+    return swk::launch_wave<KK, (C0 != 0), (PF != 0), (GT != 0)>(a, prof_bytes, st);
+  SWK_WAVE_VARIANTS(SWK_WCASE)
+#undef SWK_WCASE
   return hipErrorInvalidValue;
 }

@@ -12,6 +12,15 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["tile", "wave"])
+def kernel_choice(request, monkeypatch):
+    """Run every parity test through both score kernels: the tile kernel (waves = row blocks,
+    lanes = targets) and the wave kernel (lanes = rows, DPP hand-off).  The wave kernel takes
+    queries up to 1024 rows; longer ones fall back to the tile kernel."""
+    monkeypatch.setenv("SWBANK_KERNEL", request.param)
+    return request.param
+
+
 def _random_case(rng, qlen, ntargets, maxlen, p_n=0.02):
     q = rng.integers(0, 4, qlen, dtype=np.uint8)
     q[rng.random(qlen) < p_n] = 4

@@ -14,6 +14,15 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True, params=["tile", "wave"])
+def kernel_choice(request, monkeypatch):
+    """Run every parity test through both score kernels: the tile kernel (waves = row blocks,
+    lanes = targets) and the wave kernel (lanes = rows, DPP hand-off).  The wave kernel takes
+    queries up to 1024 rows; longer ones fall back to the tile kernel."""
+    monkeypatch.setenv("SWBANK_KERNEL", request.param)
+    return request.param
+
 REF = (5, -4, -12, -4)
 
 
