@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Sweep compiled score-kernel variants (SWBANK_R / SWBANK_C / SWBANK_RB) on the bench workload
+"""Sweep compiled score-kernel variants (SWBANK_R / SWBANK_RB / SWBANK_F16) on the bench workload
 in ONE process (interleaved rounds, cdna_hip_programming.md §5.4 rule 24) and check that every
 variant returns identical scores (and a sample against the oracle).
 
@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--variants", nargs="*",
-                    default=["32,4", "16,4", "32,8", "64,4"])
+                    default=["32,4", "32,4,u16", "16,4", "32,8", "64,4"],
+                    help="R,RB[,u16]: u16 forces the u16 arithmetic (SWBANK_F16=0)")
     args = ap.parse_args()
     import torch
 
@@ -52,8 +53,9 @@ def main():
     results = {v: [] for v in args.variants}
     for rnd in range(args.rounds):
         for v in args.variants:
-            R, RB = v.split(",")
+            R, RB, *mode = v.split(",")
             os.environ["SWBANK_R"], os.environ["SWBANK_RB"] = R, RB
+            os.environ["SWBANK_F16"] = "0" if mode == ["u16"] else "1"
             bank.load_query(q)  # re-prepare with the new variant
             bank.set_timing(False)
             bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,

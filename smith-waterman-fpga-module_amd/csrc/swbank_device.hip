@@ -16,13 +16,13 @@
 #include "swbank.h"
 #include "swbank_internal.h"
 
-extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh);
+extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh, int f16);
 extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, const uint8_t* res,
                                       const uint64_t* offs, const uint32_t* lens, size_t n,
                                       const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
                                       hipStream_t st);
-extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh,
+extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh, int f16,
                                        const uint8_t* res, const uint64_t* offs,
                                        const uint32_t* lens, size_t n, const uint32_t* qtab,
                                        uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
@@ -81,6 +81,12 @@ struct sw_bank {
   uint32_t S = 0, O = 0, E = 0, nv = 0, PS = 0, pad = 4;
   int32_t smax = 0;
   DevBuf<uint32_t> qtab;  // LUT words or query-profile bytes, per query segment
+  // f16 tile kernel (DNA LUT, merged gaps): LUT bytes are f16 high bytes; used for a batch
+  // whose score bound fits f16's exact integers (|x| <= 2048)
+  bool f16 = false;
+  uint32_t nv16 = 0;
+  int32_t f16_neg = 0;     // most negative intermediate: -(o + 2e + |min s|)
+  DevBuf<uint32_t> qtab16;
   struct Seg { int W; size_t off; };  // rows = W*R (last may be shorter), qtab word offset
   std::vector<Seg> segs;
   DevBuf<uint2> edge[2];  // bottom rows handed from segment to segment
@@ -178,6 +184,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   double pm, sm;
   (void)sw_bank_timing(b, &nl, &pm, &sm);
   b->qtab.release();
+  b->qtab16.release();
   b->wtab.release();
   b->edge[0].release();
   b->edge[1].release();
@@ -278,7 +285,7 @@ static sw_status prepare(sw_bank* b) {
     return fail(b, SW_ERR_ARG, "segment rows %d not a multiple of R=%d", seg_rows, R);
   // the HDL column-0 rule differs from the plain recurrence only if a match pays for a gap
   const int col0 = (!gotoh && smax > o + e) ? 1 : 0;
-  if (!swk_has_variant(R, RB, col0, prof, gotoh ? 1 : 0))
+  if (!swk_has_variant(R, RB, col0, prof, gotoh ? 1 : 0, 0))
     return fail(b, SW_ERR_UNSUPPORTED, "no kernel variant R=%d RB=%d col0=%d prof=%d gotoh=%d", R,
                 RB, col0, prof, (int)gotoh);
   const int Wseg = std::max(1, (seg_rows + R - 1) / R);
@@ -314,6 +321,37 @@ static sw_status prepare(sw_bank* b) {
       std::memcpy(tab.data() + base, qp.data(), qp.size());
     }
   }
+  // f16 variant of the LUT: each substitution score must be an f16 whose low byte is 0
+  // (|s| <= 8 or a coarser even value), so the byte perm yields the exact f16 bits
+  auto f16_hi = [](int v, uint8_t* out) {
+    const _Float16 h = (_Float16)(float)v;
+    const uint16_t bits = __builtin_bit_cast(uint16_t, h);
+    *out = (uint8_t)(bits >> 8);
+    return (bits & 0xFFu) == 0 && (int)(float)h == v;
+  };
+  bool f16 = !prof && !gotoh && swk_has_variant(R, RB, col0, 0, 0, 1) != 0;
+  std::vector<uint32_t> tab16;
+  uint8_t hN = 0;
+  f16 = f16 && f16_hi(sN, &hN);
+  for (int i = 0; f16 && i < A * A; ++i) {
+    uint8_t h;
+    f16 = f16_hi(m[i], &h);
+  }
+  if (f16) {
+    tab16.assign(tab.size(), 0xE8E8E8E8u);  // padding rows: -2048
+    for (const sw_bank::Seg& sg : segs) {
+      const int r0 = (int)(&sg - segs.data()) * seg_rows;
+      for (int i = 0; i < sg.W * R && r0 + i < qlen && i < seg_rows; ++i) {
+        uint32_t w = 0;
+        for (int c = 0; c < 4; ++c) {
+          uint8_t h;
+          f16_hi(m[b->query[r0 + i] * A + c], &h);
+          w |= (uint32_t)h << (8 * c);
+        }
+        tab16[sg.off + i] = w;
+      }
+    }
+  }
   // wave-kernel layout of the same query (rows padded to 64K)
   std::vector<uint32_t> wt;
   int wK = qlen <= 256 ? 4 : qlen <= 512 ? 8 : qlen <= 1024 ? 16 : 0;
@@ -347,7 +385,15 @@ static sw_status prepare(sw_bank* b) {
   HIPOK(b, b->qtab.reserve(tab.size()));
   HIPOK(b, hipMemcpyAsync(b->qtab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice,
                           b->stream));
+  if (f16) {
+    HIPOK(b, b->qtab16.reserve(tab16.size()));
+    HIPOK(b, hipMemcpyAsync(b->qtab16.p, tab16.data(), tab16.size() * 4, hipMemcpyHostToDevice,
+                            b->stream));
+  }
   HIPOK(b, hipStreamSynchronize(b->stream));
+  b->f16 = f16;
+  b->nv16 = (uint32_t)hN * 0x01010101u;
+  b->f16_neg = -(o + 2 * e + (S - smin));
   b->R = R;
   b->RB = RB;
   b->W = segs[0].W;
@@ -408,12 +454,21 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
     HIPOK(b, b->edge[0].reserve(words));
     HIPOK(b, b->edge[1].reserve(words));
   }
+  // f16 arithmetic (8 VALU per 2 cells instead of 9) when every value the recurrence can
+  // reach is an exact f16 integer: the positive bound min(|q|, max|t|) * max(s) + max(s)
+  // and the most negative intermediate both within 2048
+  const uint64_t top = std::min<uint64_t>(b->query.size(), max_len) * (uint64_t)std::max(0, b->smax) +
+                       (uint64_t)std::max(0, b->smax);
+  const bool use_f16 = b->f16 && top <= 2048u && b->f16_neg >= -2048 &&
+                       env_int("SWBANK_F16", 1) != 0;  // SWBANK_F16=0: u16 kernel (tests)
   for (size_t s = 0; !use_wave && s < nseg; ++s) {
     const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
     void* eout = s + 1 < nseg ? b->edge[s & 1].p : nullptr;
     HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof,
-                              b->cfg.gap_model == SW_GAP_GOTOH ? 1 : 0, d_res, d_offs, d_lens, n,
-                              b->qtab.p + b->segs[s].off, b->nv, b->S, b->O, b->E, b->PS,
+                              b->cfg.gap_model == SW_GAP_GOTOH ? 1 : 0, use_f16 ? 1 : 0, d_res,
+                              d_offs, d_lens, n,
+                              (use_f16 ? b->qtab16.p : b->qtab.p) + b->segs[s].off,
+                              use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E, b->PS,
                               b->pad, b->segs[s].W, d_scores, ein, eout, ecols, s > 0 ? 1 : 0,
                               st));
   }

@@ -89,6 +89,45 @@ __device__ __forceinline__ void column_merged(const LK& lk, u16x2& diag, u16x2& 
   }
 }
 
+// ---- one column of R rows, merged gap matrix, f16 arithmetic ------------------------------
+// Exact for integer scores |x| <= 2048 (the host routes a batch here only when the score
+// bound allows it, and when every substitution score is an f16 whose low byte is 0, so a
+// one-byte LUT entry is its high byte).  Signed arithmetic needs no clamps and no shift,
+// and v_pk_maximum3_f16 takes three inputs:
+//   D = H(i-1,j-1) + s      I = max(Tup, Tleft)      H = max(0, D, I)
+//   T = max(-o-e, D-o-e, I-e)  (= G - e, the gap value the right and lower neighbours see)
+// 8 VALU per lane per 2 cells (u16 form: 9).  Negative values never reach a positive one.
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f16x2 as_f16x2(u16x2 x) { return __builtin_bit_cast(f16x2, x); }
+__device__ __forceinline__ u16x2 as_u16x2(f16x2 x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ f16x2 fmax2(f16x2 a, f16x2 b) {
+  return __builtin_elementwise_maximum(a, b);
+}
+template <int R, int RB, bool ZDOWN, class LK>
+__device__ __forceinline__ void column_merged_f16(const LK& lk, u16x2& diag_, u16x2& upT_,
+                                                  u16x2 (&Hl)[R], u16x2 (&Tl)[R], u16x2& best_,
+                                                  f16x2 NOE2, f16x2 NE2) {
+  f16x2 diag = as_f16x2(diag_), upT = as_f16x2(upT_), best = as_f16x2(best_);
+  const f16x2 Z = {(_Float16)0, (_Float16)0};
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const f16x2 sc = as_f16x2(lk(r));
+    const f16x2 D = diag + sc;
+    const f16x2 I = fmax2(upT, as_f16x2(Tl[r]));
+    const f16x2 H = fmax2(fmax2(D, Z), I);
+    const f16x2 T = fmax2(fmax2(D + NOE2, NOE2), I + NE2);
+    best = fmax2(best, H);
+    diag = as_f16x2(Hl[r]);
+    Hl[r] = as_u16x2(H);
+    Tl[r] = as_u16x2(T);
+    upT = ZDOWN ? NOE2 : T;
+    if ((r % RB) == RB - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+  diag_ = as_u16x2(diag);
+  upT_ = as_u16x2(upT);
+  best_ = as_u16x2(best);
+}
+
 // ---- one column of R rows, Gotoh (separate E/F; ssearch36 semantics) ---------------------
 //   E(i,j) = max(H(i,j-1) - o - e, E(i,j-1) - e)     F(i,j) = max(H(i-1,j) - o - e, F(i-1,j) - e)
 //   H(i,j) = max(0, H(i-1,j-1) + s, E, F)            (E, F clamped at 0: exact, H >= 0)
@@ -213,7 +252,7 @@ __device__ __forceinline__ void dma_edge_chunk(const uint2* src, uint2* dst, int
 // LDS ring hand-off wave w -> w+1 (the RTL's PE-to-PE registers).
 // LDS: best[128] | bnd[64] | sink[8][64] | ein[2][8][64] (segments) |
 //      ring[(W-1)][2][8][64] {H~, G or F} | PROF: profile
-template <int R, int RB, bool COL0, bool PROF, bool GOTOH>
+template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
   constexpr int C = 8;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -239,7 +278,10 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   if (wave == 0) {
     bestsh[lane] = 0;
     bestsh[lane + 64] = 0;
-    bnd[lane] = make_uint2(S | (S << 16), 0u);  // row -1: H~ = S, G/F = 0
+    // row -1: u16 H~ = S, G/F = 0 | f16 H = 0, T = -(o+e)
+    const _Float16 noe = (_Float16)(-(float)(a.O + a.E));
+    const uint32_t noe2 = __builtin_bit_cast(uint32_t, (f16x2){noe, noe});
+    bnd[lane] = F16 ? make_uint2(0u, noe2) : make_uint2(S | (S << 16), 0u);
     if (seg_in)  // the previous segment's bottom row of chunk 0
       dma_edge_chunk(a.edge_in + (size_t)tile * a.ecols * 64, ein, lane);
   }
@@ -263,15 +305,18 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const u16x2 E2 = {(unsigned short)a.E, (unsigned short)a.E};
   const uint32_t oes = a.O + a.E + S;
   const u16x2 OES2 = {(unsigned short)oes, (unsigned short)oes};
+  const _Float16 fnoe = (_Float16)(-(float)(a.O + a.E)), fne = (_Float16)(-(float)a.E);
+  const f16x2 NOE2 = {fnoe, fnoe}, NE2 = {fne, fne};
 
-  u16x2 Hl[R], Xl[R];  // H~ and G (merged) or E (Gotoh) of the column to the left
+  // H~ and G (merged) / E (Gotoh) / T (f16) of the column to the left
+  u16x2 Hl[R], Xl[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    Hl[r] = S2;
-    Xl[r] = (u16x2){0, 0};
+    Hl[r] = F16 ? (u16x2){0, 0} : S2;
+    Xl[r] = F16 ? as_u16x2(NOE2) : (u16x2){0, 0};
   }
   u16x2 best = {0, 0};
-  u16x2 prevUpH = S2;  // H~(row above, column -1) = S
+  u16x2 prevUpH = F16 ? (u16x2){0, 0} : S2;  // H(row above, column -1)
   uint2 rlo, rhi;      // raw codes of the next chunk (prefetched one phase ahead)
   load_raw(cur, 0, nfull > 0, a.pad, rlo, rhi);
   __syncthreads();
@@ -333,6 +378,20 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           // selector: byte 0 = code of the low target, byte 2 = code of the high target
           const uint32_t sel =
               (uint32_t)(jj & 3) | ((uint32_t)(4 + (jj & 3)) << 16) | 0x0C000C00u;
+          if constexpr (F16) {
+            // selector bytes {0x0C, code_lo, 0x0C, code_hi}: the LUT byte is the f16 high byte
+            const uint32_t sel16 =
+                0x0Cu | ((uint32_t)(jj & 3) << 8) | (0x0Cu << 16) | ((uint32_t)(4 + (jj & 3)) << 24);
+            const LutLookup<R> lk{tab, nv, __builtin_amdgcn_perm(whi, wlo, sel16) | 0x000C000Cu};
+            __builtin_amdgcn_sched_barrier(0);
+            if (COL0 && jj == 0 && c == 0)
+              column_merged_f16<R, RB, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+            else
+              column_merged_f16<R, RB, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+            asm volatile("" : "+v"(best));
+            rout[jj * ostride] = make_uint2(as_u32(Hl[R - 1]), as_u32(upX));
+            continue;
+          }
           const LutLookup<R> lk{tab, nv, __builtin_amdgcn_perm(whi, wlo, sel) | 0x0C000C00u};
           __builtin_amdgcn_sched_barrier(0);
           if constexpr (GOTOH) {
@@ -363,6 +422,10 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   __syncthreads();
   if (wave == 0) {
     int32_t blo = (int32_t)bestsh[lane], bhi = (int32_t)bestsh[lane + 64];
+    if constexpr (F16) {  // f16 bit patterns of non-negative integers -> int
+      blo = (int32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)blo);
+      bhi = (int32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)bhi);
+    }
     if (a.accum) {  // best over the previous query segments
       if (tlo < n) blo = max(blo, a.scores[tlo]);
       if (thi < n) bhi = max(bhi, a.scores[thi]);
@@ -372,14 +435,14 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   }
 }
 
-template <int R, int RB, bool COL0, bool PROF, bool GOTOH>
+template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16>
 static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st) {
   const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE;
   const size_t lds = SWB_TILE * 4 +
                      (size_t)(64 + 8 * 64 + (a.edge_in ? 2 * 8 * 64 : 0) +
                               (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8 +
                      (PROF ? prof_bytes : 0);
-  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH>;
+  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -579,25 +642,26 @@ static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream
 
 }  // namespace swk
 
-// Variants compiled in: (R, RB, COL0, PROF, GOTOH).  The host picks R from the query length
-// (SWBANK_R / SWBANK_RB override it for tuning).
-#define SWK_VARIANTS(X)                                                                     \
-  X(16, 4, 0, 0, 0) X(16, 4, 1, 0, 0) X(32, 4, 0, 0, 0) X(32, 4, 1, 0, 0) X(32, 8, 0, 0, 0) \
-  X(64, 4, 0, 0, 0) X(64, 4, 1, 0, 0)                                                        \
-  X(16, 4, 0, 0, 1) X(32, 4, 0, 0, 1) X(64, 4, 0, 0, 1)                                      \
-  X(16, 4, 0, 1, 0) X(16, 4, 1, 1, 0) X(32, 4, 0, 1, 0) X(32, 4, 1, 1, 0) X(64, 4, 0, 1, 0)  \
-  X(64, 4, 1, 1, 0)                                                                          \
-  X(16, 4, 0, 1, 1) X(32, 4, 0, 1, 1) X(64, 4, 0, 1, 1)
+// Variants compiled in: (R, RB, COL0, PROF, GOTOH, F16).  The host picks R from the query
+// length (SWBANK_R / SWBANK_RB override it for tuning).
+#define SWK_VARIANTS(X)                                                                       \
+  X(16, 4, 0, 0, 0, 0) X(16, 4, 1, 0, 0, 0) X(32, 4, 0, 0, 0, 0) X(32, 4, 1, 0, 0, 0)         \
+  X(32, 8, 0, 0, 0, 0) X(64, 4, 0, 0, 0, 0) X(64, 4, 1, 0, 0, 0)                              \
+  X(16, 4, 0, 0, 1, 0) X(32, 4, 0, 0, 1, 0) X(64, 4, 0, 0, 1, 0)                              \
+  X(16, 4, 0, 1, 0, 0) X(16, 4, 1, 1, 0, 0) X(32, 4, 0, 1, 0, 0) X(32, 4, 1, 1, 0, 0)         \
+  X(64, 4, 0, 1, 0, 0) X(64, 4, 1, 1, 0, 0)                                                   \
+  X(16, 4, 0, 1, 1, 0) X(32, 4, 0, 1, 1, 0) X(64, 4, 0, 1, 1, 0)                              \
+  X(16, 4, 0, 0, 0, 1) X(16, 4, 1, 0, 0, 1) X(32, 4, 0, 0, 0, 1) X(64, 4, 0, 0, 0, 1)
 
-extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh) {
-#define SWK_HAS(RR, BB, C0, PF, GT) \
-  if (R == RR && RB == BB && col0 == C0 && prof == PF && gotoh == GT) return 1;
+extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh, int f16) {
+#define SWK_HAS(RR, BB, C0, PF, GT, FH) \
+  if (R == RR && RB == BB && col0 == C0 && prof == PF && gotoh == GT && f16 == FH) return 1;
   SWK_VARIANTS(SWK_HAS)
 #undef SWK_HAS
   return 0;
 }
 
-extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh,
+extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh, int f16,
                                        const uint8_t* res, const uint64_t* offs,
                                        const uint32_t* lens, size_t n, const uint32_t* qtab,
                                        uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
@@ -609,9 +673,10 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                          O,    E,    PS,   pad, scores, static_cast<const uint2*>(edge_in),
                          static_cast<uint2*>(edge_out), ecols, (uint32_t)accum};
   const uint32_t prof_bytes = (pad + 1) * PS;
-#define SWK_CASE(RR, BB, C0, PF, GT)                                                   \
-  if (R == RR && RB == BB && col0 == C0 && prof == PF && gotoh == GT)                  \
-    return swk::launch_score<RR, BB, (C0 != 0), (PF != 0), (GT != 0)>(a, W, prof_bytes, st);
+#define SWK_CASE(RR, BB, C0, PF, GT, FH)                                                      \
+  if (R == RR && RB == BB && col0 == C0 && prof == PF && gotoh == GT && f16 == FH)            \
+    return swk::launch_score<RR, BB, (C0 != 0), (PF != 0), (GT != 0), (FH != 0)>(a, W,        \
+                                                                               prof_bytes, st);
   SWK_VARIANTS(SWK_CASE)
 #undef SWK_CASE
   return hipErrorInvalidValue;

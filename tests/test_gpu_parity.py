@@ -15,13 +15,18 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["tile", "wave"])
+@pytest.fixture(autouse=True, params=["tile", "tile-u16", "wave"])
 def kernel_choice(request, monkeypatch):
-    """Run every parity test through both score kernels: the tile kernel (waves = row blocks,
-    lanes = targets) and the wave kernel (lanes = rows, DPP hand-off).  The wave kernel takes
-    queries up to 1024 rows; longer ones fall back to the tile kernel."""
-    monkeypatch.setenv("SWBANK_KERNEL", request.param)
+    """Run every parity test through each score kernel: the tile kernel (waves = row blocks,
+    lanes = targets) with its f16 arithmetic where the batch's score bound allows it
+    ("tile") and forced to u16 ("tile-u16"), and the wave kernel (lanes = rows, DPP
+    hand-off).  The wave kernel takes queries up to 1024 rows; longer ones fall back to
+    the tile kernel."""
+    kern = request.param.split("-")[0]
+    monkeypatch.setenv("SWBANK_KERNEL", kern)
+    monkeypatch.setenv("SWBANK_F16", "0" if request.param == "tile-u16" else "1")
     return request.param
+
 
 REF = (5, -4, -12, -4)
 
@@ -120,6 +125,30 @@ def test_edge_shapes(bank):
     got = bank.score_targets(seqs)
     res, offs, lens = O.pack_residues(seqs)
     assert (got == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
+
+
+@pytest.mark.parametrize("qlen", [200, 407, 408, 409, 410, 512])
+@pytest.mark.parametrize("match", [5, 8, 9, 16])
+def test_f16_bound_edges(bank, qlen, match):
+    """Scores at and past the f16 kernel's exact range: the host takes the f16 tile kernel
+    only while min(|q|, max|t|) * max(s) + max(s) <= 2048 and every substitution score is an
+    f16 with a zero low byte (match 9 is not: u16 kernel); perfect and near-perfect matches
+    put the optimum right at the bound."""
+    rng = np.random.default_rng(qlen * 7 + match)
+    q = rng.integers(0, 4, qlen, dtype=np.uint8)
+    near = q.copy()
+    near[qlen // 2] = (near[qlen // 2] + 1) % 4
+    gapped = np.concatenate([q[:qlen // 3], q[qlen // 3 + 2:]])
+    seqs = [q, near, gapped, q[: qlen // 2], rng.integers(0, 4, qlen, dtype=np.uint8)]
+    seqs += [q] * 130  # a second tile
+    params = (match, -4, -12, -4)
+    bank.set_penalties(*params)
+    bank.load_query(q)
+    got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(match, -4), -12, -4)
+    assert got[0] == match * qlen
+    assert (got == want).all(), [(i, int(got[i]), int(want[i])) for i in np.nonzero(got != want)[0][:8]]
 
 
 def test_errors(bank):
