@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--variants", nargs="*",
                     default=["32,4", "32,4,u16", "16,4", "32,8", "64,4"],
-                    help="R,RB[,u16]: u16 forces the u16 arithmetic (SWBANK_F16=0)")
+                    help="R,RB[,u16] tile-kernel variants (u16: SWBANK_F16=0) or wave")
     args = ap.parse_args()
     import torch
 
@@ -53,9 +53,13 @@ def main():
     results = {v: [] for v in args.variants}
     for rnd in range(args.rounds):
         for v in args.variants:
-            R, RB, *mode = v.split(",")
-            os.environ["SWBANK_R"], os.environ["SWBANK_RB"] = R, RB
-            os.environ["SWBANK_F16"] = "0" if mode == ["u16"] else "1"
+            if v == "wave":
+                os.environ["SWBANK_KERNEL"] = "wave"
+            else:
+                R, RB, *mode = v.split(",")
+                os.environ["SWBANK_R"], os.environ["SWBANK_RB"] = R, RB
+                os.environ["SWBANK_F16"] = "0" if mode == ["u16"] else "1"
+                os.environ["SWBANK_KERNEL"] = "tile"
             bank.load_query(q)  # re-prepare with the new variant
             bank.set_timing(False)
             bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,

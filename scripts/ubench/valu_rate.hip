@@ -26,6 +26,24 @@ __global__ void __launch_bounds__(256) k(uint32_t* out, uint32_t seed, unsigned 
         a[i] = max(a[i], b) + 1u;
       } else if (KIND == 2) {  // v_perm_b32 + v_add
         a[i] = __builtin_amdgcn_perm(b, a[i], 0x0c010c00u) + 1u;
+      } else if (KIND == 4) {  // v_add_f32 + v_max_f32
+        float x = __builtin_bit_cast(float, a[i]);
+        x = __builtin_fmaxf(x + 1.5f, __builtin_bit_cast(float, b));
+        a[i] = __builtin_bit_cast(uint32_t, x);
+      } else if (KIND == 5) {  // v_fma_f32 x 2
+        float x = __builtin_bit_cast(float, a[i]);
+        x = __builtin_fmaf(x, 0.999f, 0.5f);
+        x = __builtin_fmaf(x, 1.001f, -0.25f);
+        a[i] = __builtin_bit_cast(uint32_t, x);
+      } else if (KIND == 6) {  // v_pk_add_f16 + v_pk_maximum3_f16
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        h2 x = __builtin_bit_cast(h2, a[i]), y = __builtin_bit_cast(h2, b);
+        x = x + (h2){(_Float16)1, (_Float16)1};
+        x = __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y),
+                                          (h2){(_Float16)-3, (_Float16)-3});
+        a[i] = __builtin_bit_cast(uint32_t, x);
+      } else if (KIND == 7) {  // v_max3_u32 + v_add_u32
+        a[i] = max(max(a[i], b), b ^ 5u) + 1u;
       } else {  // v_pk_sub_u16 clamp + v_pk_add_u16
         u16x2 x = __builtin_bit_cast(u16x2, a[i]), y = __builtin_bit_cast(u16x2, b);
         a[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x, y) + (u16x2){7, 7});
@@ -70,11 +88,15 @@ void run(const char* name, int blocks) {
 }
 
 int main() {
-  for (int blocks : {1024, 2048, 8192}) {
+  for (int blocks : {2048, 8192}) {
     run<0>("v_pk_max_u16+v_pk_add_u16", blocks);
     run<1>("v_max_u32+v_add_u32", blocks);
     run<2>("v_perm_b32+v_add_u32", blocks);
     run<3>("v_pk_sub_u16_clamp+v_pk_add_u16", blocks);
+    run<4>("v_add_f32+v_max_f32", blocks);
+    run<5>("v_fma_f32+v_fma_f32", blocks);
+    run<6>("v_pk_add_f16+v_pk_maximum3_f16", blocks);
+    run<7>("v_max3_u32+v_add_u32", blocks);
   }
   return 0;
 }

@@ -439,9 +439,11 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   const size_t ntiles = (n + SWB_TILE - 1) / SWB_TILE;
   // Kernel choice: the tile kernel needs many 128-target tiles to fill 256 CUs (each tile is
   // one workgroup of W waves); with few targets the wave kernel (one wave per 2 targets,
-  // lanes = query rows) has 64x more parallelism.  SWBANK_KERNEL=tile|wave forces one.
+  // lanes = query rows) has 64x more parallelism.  Crossover measured on MI355X (128-row query,
+  // 128-bp targets): wave kernel ahead below ~190 tiles x 4 waves, tile kernel above (the tile
+  // kernel reaches ~1 resident wave per SIMD there).  SWBANK_KERNEL=tile|wave forces one.
   const char* kforce = std::getenv("SWBANK_KERNEL");
-  bool use_wave = b->wK > 0 && ntiles * (size_t)b->segs[0].W < 4096;
+  bool use_wave = b->wK > 0 && ntiles * (size_t)b->segs[0].W < 768;
   if (kforce && std::strcmp(kforce, "tile") == 0) use_wave = false;
   if (kforce && std::strcmp(kforce, "wave") == 0 && b->wK > 0) use_wave = true;
   if (use_wave) {

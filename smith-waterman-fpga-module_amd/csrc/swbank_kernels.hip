@@ -27,6 +27,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "swbank_internal.h"
 
 namespace swk {
@@ -126,6 +129,61 @@ __device__ __forceinline__ void column_merged_f16(const LK& lk, u16x2& diag_, u1
   diag_ = as_u16x2(diag);
   upT_ = as_u16x2(upT);
   best_ = as_u16x2(best);
+}
+
+// Same column, hand-ordered: each row is one asm block whose dependent packed ops are never
+// adjacent (gfx950 needs a wait state between a VOP3P write and a dependent VOP3P read, and
+// LLVM's order of this chain left ~2.5 s_nop per row).  Per row r, with D_r = diag + s_r
+// already computed by row r-1's block:
+//   I = max(Tup, Tl) ; DN = D + NOE ; IN = I + NE ; H = max(D, 0, I) ; T = max(DN, NOE, IN)
+//   [best = max(best, H_prev, H) every second row] ; s' = perm(LUT_{r+1}) ; D' = Hl[r] + s'
+#ifndef SWK_F16_ASM
+#define SWK_F16_ASM 1
+#endif
+#include "swbank_f16_rows.inc"
+#define SWK_F16_OPS(B)                                                                        \
+  [h0] "+v"(Hl[B]), [h1] "+v"(Hl[B + 1]), [h2] "+v"(Hl[B + 2]), [h3] "+v"(Hl[B + 3]),          \
+      [h4] "+v"(Hl[B + 4]), [h5] "+v"(Hl[B + 5]), [h6] "+v"(Hl[B + 6]), [h7] "+v"(Hl[B + 7]),  \
+      [t0] "+v"(Tl[B]), [t1] "+v"(Tl[B + 1]), [t2] "+v"(Tl[B + 2]), [t3] "+v"(Tl[B + 3]),      \
+      [t4] "+v"(Tl[B + 4]), [t5] "+v"(Tl[B + 5]), [t6] "+v"(Tl[B + 6]), [t7] "+v"(Tl[B + 7]),  \
+      [Da] "+v"(Da), [Db] "=&v"(Db), [S1] "=&v"(S1), [X] "=&v"(X), [DN] "=&v"(DN),             \
+      [IN] "=&v"(IN), [best] "+v"(best)
+#define SWK_F16_INS(B)                                                                        \
+  [up] "v"(up), [nv] "v"(nv), [sel] "v"(selw), [noe] "s"(noe), [ne] "s"(ne),                 \
+      [tb0] "s"(tab[B + 1]), [tb1] "s"(tab[B + 2]), [tb2] "s"(tab[B + 3]),                    \
+      [tb3] "s"(tab[B + 4]), [tb4] "s"(tab[B + 5]), [tb5] "s"(tab[B + 6]),                    \
+      [tb6] "s"(tab[B + 7]), [tb7] "s"(tab[(B + 8) < R ? B + 8 : R - 1])
+template <int R, bool ZDOWN>
+__device__ __forceinline__ void column_merged_f16_asm(const uint32_t (&tab)[R], uint32_t nv,
+                                                      uint32_t selw, u16x2& diag_, u16x2& upT_,
+                                                      u16x2 (&Hl)[R], u16x2 (&Tl)[R],
+                                                      u16x2& best_, uint32_t noe, uint32_t ne) {
+  static_assert(R % 8 == 0, "rows come in blocks of 8");
+  uint32_t Da, Db, S1, X, DN, IN;
+  u16x2 best = best_, up = upT_;
+  asm volatile(
+      "v_perm_b32 %[Da], %[nv], %[t0], %[sel]\n\t"
+      "v_pk_add_f16 %[Da], %[dg], %[Da]"
+      : [Da] "=&v"(Da)
+      : [nv] "v"(nv), [t0] "s"(tab[0]), [sel] "v"(selw), [dg] "v"(diag_));
+#pragma unroll
+  for (int b = 0; b < R; b += 8) {
+    if (b + 8 < R) {
+      if constexpr (ZDOWN)
+        asm volatile(SWK_F16_BLOCK_Z1_L0 : SWK_F16_OPS(b) : SWK_F16_INS(b));
+      else
+        asm volatile(SWK_F16_BLOCK_Z0_L0 : SWK_F16_OPS(b) : SWK_F16_INS(b));
+    } else {
+      if constexpr (ZDOWN)
+        asm volatile(SWK_F16_BLOCK_Z1_L1 : SWK_F16_OPS(b) : SWK_F16_INS(b));
+      else
+        asm volatile(SWK_F16_BLOCK_Z0_L1 : SWK_F16_OPS(b) : SWK_F16_INS(b));
+    }
+    up = ZDOWN ? as_u16x2(noe) : Tl[b + 7];
+  }
+  (void)Db; (void)S1; (void)X; (void)DN; (void)IN;
+  upT_ = up;
+  best_ = best;
 }
 
 // ---- one column of R rows, Gotoh (separate E/F; ssearch36 semantics) ---------------------
@@ -247,10 +305,24 @@ __device__ __forceinline__ void dma_edge_chunk(const uint2* src, uint2* dst, int
                                      (lds_void_ptr)(dst + q * 128), 16, 0, 0);
 }
 
-// Score kernel: one workgroup = one tile of 128 targets x the whole query (W waves x R rows).
-// Wave w processes chunk c (8 columns) at phase c + w; one __syncthreads per phase orders the
-// LDS ring hand-off wave w -> w+1 (the RTL's PE-to-PE registers).
-// LDS: best[128] | bnd[64] | sink[8][64] | ein[2][8][64] (segments) |
+// Chunk count of a tile (uniform), from the lengths alone.
+__device__ __forceinline__ int tile_nch(const uint32_t* lens, size_t n, int tile, int lane) {
+  const size_t a = (size_t)tile * SWB_TILE + lane, b = a + 64;
+  uint32_t L = max(a < n ? lens[a] : 0u, b < n ? lens[b] : 0u);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) L = max(L, (uint32_t)__shfl_xor((int)L, off));
+  return max(1, (int)((__builtin_amdgcn_readfirstlane(L) + 7) / 8));
+}
+
+// Score kernel (persistent pipeline).  A workgroup of W waves x R rows holds the query (or
+// one segment of it) and scores the tiles of 128 targets blockIdx.x, blockIdx.x + G, ...
+// (G = gridDim.x) as ONE stream of 8-column chunks: wave w processes the workgroup's global
+// chunk g at phase g + w, so the wave pipeline fills and drains once per workgroup instead of
+// once per tile.  One __syncthreads per phase orders the LDS ring hand-off wave w -> w+1 (the
+// RTL's PE-to-PE registers).  A wave that finishes its part of the k-th tile folds its running
+// max into bestsh[k % W]; the last wave, which finishes that tile W-1 phases after wave 0,
+// writes the scores and clears the slot (wave 0 reuses it for tile k + W, >= W phases later).
+// LDS: bestsh[W][128] | bnd[64] | sink[8][64] | ein[2][8][64] (segments) |
 //      ring[(W-1)][2][8][64] {H~, G or F} | PROF: profile
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
@@ -260,28 +332,32 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int W = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
   const bool seg_in = a.edge_in != nullptr, seg_out = a.edge_out != nullptr;
-  uint32_t* bestsh = smem;                                   // 128 words
-  uint2* bnd = reinterpret_cast<uint2*>(smem + SWB_TILE);    // row -1 boundary {S, 0}
-  uint2* sink = bnd + 64;                                    // last wave's bottom row, 8 cols
-  uint2* ein = sink + C * 64;                                // previous segment, 2 x 8 cols
+  uint32_t* bestsh = smem;                                       // W x 128 words
+  uint2* bnd = reinterpret_cast<uint2*>(smem + W * SWB_TILE);    // row -1 boundary
+  uint2* sink = bnd + 64;                                        // last wave's bottom row
+  uint2* ein = sink + C * 64;                                    // previous segment, 2 x 8 cols
   uint2* ring = ein + (seg_in ? 2 * C * 64 : 0);
   uint8_t* prof = reinterpret_cast<uint8_t*>(ring + (size_t)(W > 1 ? W - 1 : 0) * 2 * C * 64);
 
-  const int tile = blockIdx.x;
   const size_t n = a.n;
-  const size_t tlo = (size_t)tile * SWB_TILE + lane, thi = tlo + 64;
-  const Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane);
+  const int ntiles = (int)((n + SWB_TILE - 1) / SWB_TILE);
+  const int G = (int)gridDim.x;
+  int total = 0;  // chunks of all this workgroup's tiles: every wave runs total + W - 1 phases
+  for (int t = blockIdx.x; t < ntiles; t += G) total += tile_nch(a.lens, n, t, lane);
+
+  int tile = blockIdx.x;
+  Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane);
   int nch, nfull;
-  tile_chunks(cur, tlo, thi, n, nch, nfull);
+  tile_chunks(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
+              nfull);
   const uint32_t S = a.S;
 
+  for (int i = threadIdx.x; i < W * SWB_TILE; i += blockDim.x) bestsh[i] = 0;
+  // row -1: u16 H~ = S, G/F = 0 | f16 H = 0, T = -(o+e)
+  const _Float16 fnoe = (_Float16)(-(float)(a.O + a.E)), fne = (_Float16)(-(float)a.E);
+  const f16x2 NOE2 = {fnoe, fnoe}, NE2 = {fne, fne};
   if (wave == 0) {
-    bestsh[lane] = 0;
-    bestsh[lane + 64] = 0;
-    // row -1: u16 H~ = S, G/F = 0 | f16 H = 0, T = -(o+e)
-    const _Float16 noe = (_Float16)(-(float)(a.O + a.E));
-    const uint32_t noe2 = __builtin_bit_cast(uint32_t, (f16x2){noe, noe});
-    bnd[lane] = F16 ? make_uint2(0u, noe2) : make_uint2(S | (S << 16), 0u);
+    bnd[lane] = F16 ? make_uint2(0u, as_u32(as_u16x2(NOE2))) : make_uint2(S | (S << 16), 0u);
     if (seg_in)  // the previous segment's bottom row of chunk 0
       dma_edge_chunk(a.edge_in + (size_t)tile * a.ecols * 64, ein, lane);
   }
@@ -305,18 +381,18 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const u16x2 E2 = {(unsigned short)a.E, (unsigned short)a.E};
   const uint32_t oes = a.O + a.E + S;
   const u16x2 OES2 = {(unsigned short)oes, (unsigned short)oes};
-  const _Float16 fnoe = (_Float16)(-(float)(a.O + a.E)), fne = (_Float16)(-(float)a.E);
-  const f16x2 NOE2 = {fnoe, fnoe}, NE2 = {fne, fne};
+  const u16x2 H0 = F16 ? (u16x2){0, 0} : S2;          // H of row/column -1
+  const u16x2 X0 = F16 ? as_u16x2(NOE2) : (u16x2){0, 0};  // G/E/T of column -1
 
   // H~ and G (merged) / E (Gotoh) / T (f16) of the column to the left
   u16x2 Hl[R], Xl[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    Hl[r] = F16 ? (u16x2){0, 0} : S2;
-    Xl[r] = F16 ? as_u16x2(NOE2) : (u16x2){0, 0};
+    Hl[r] = H0;
+    Xl[r] = X0;
   }
   u16x2 best = {0, 0};
-  u16x2 prevUpH = F16 ? (u16x2){0, 0} : S2;  // H(row above, column -1)
+  u16x2 prevUpH = H0;  // H(row above, column -1)
   uint2 rlo, rhi;      // raw codes of the next chunk (prefetched one phase ahead)
   load_raw(cur, 0, nfull > 0, a.pad, rlo, rhi);
   __syncthreads();
@@ -328,16 +404,28 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int istride = (wave > 0 || seg_in) ? 64 : 0, ostride = (wave < W - 1 || seg_out) ? 64 : 0;
   const uint32_t pbase = (uint32_t)wave * R;
   const uint32_t padc = a.pad;
-  const int nph = nch + W - 1;
+  int c = 0, k = 0;           // chunk within the current tile, tile ordinal in this workgroup
+  int nch_n = 1, nfull_n = 0;  // the next tile's chunk counts
+  const int nph = total + W - 1;
   for (int ph = 0; ph < nph; ++ph) {
-    const int c = ph - wave;
-    if (c >= 0 && c < nch) {
+    const int g = ph - wave;
+    if (g >= 0 && g < total) {
       const uint2 clo = rlo, chi = rhi;
-      if (c + 1 < nch) load_raw(cur, c + 1, c + 1 < nfull, a.pad, rlo, rhi);
-      const int slot = c & 1;
-      if (seg_in && wave == 0 && c + 1 < nch)  // prefetch the next chunk's boundary row
-        dma_edge_chunk(a.edge_in + ((size_t)tile * a.ecols + (size_t)(c + 1) * C) * 64,
-                       ein + (size_t)((c + 1) & 1) * C * 64, lane);
+      const bool last = c + 1 == nch;
+      const int ntile = tile + G;
+      if (!last) {
+        load_raw(cur, c + 1, c + 1 < nfull, a.pad, rlo, rhi);
+      } else if (ntile < ntiles) {  // first chunk of the next tile
+        cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane);
+        tile_chunks(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
+                    n, nch_n, nfull_n);
+        load_raw(cur, 0, nfull_n > 0, a.pad, rlo, rhi);
+      }
+      const int slot = g & 1;
+      if (seg_in && wave == 0 && (!last || ntile < ntiles))  // next chunk's boundary row
+        dma_edge_chunk(a.edge_in + ((size_t)(last ? ntile : tile) * a.ecols +
+                                    (size_t)(last ? 0 : c + 1) * C) * 64,
+                       ein + (size_t)((g + 1) & 1) * C * 64, lane);
       const uint2* rin = wave > 0 ? ring + ((size_t)((wave - 1) * 2 + slot) * C) * 64 + lane
                                   : (seg_in ? ein + (size_t)slot * C * 64 : bnd) + lane;
       uint2* rout = wave < W - 1 ? ring + ((size_t)(wave * 2 + slot) * C) * 64 + lane
@@ -374,24 +462,29 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           } else {
             column_merged<R, RB, false>(lk, diag, upX, Hl, Xl, best, S2, O2, E2);
           }
+        } else if constexpr (F16) {
+          // selector bytes {0x0C, code_lo, 0x0C, code_hi}: the LUT byte is the f16 high byte
+          const uint32_t sel16 = 0x0Cu | ((uint32_t)(jj & 3) << 8) | (0x0Cu << 16) |
+                                 ((uint32_t)(4 + (jj & 3)) << 24);
+          const uint32_t selw = __builtin_amdgcn_perm(whi, wlo, sel16) | 0x000C000Cu;
+#if SWK_F16_ASM
+          const uint32_t noe = as_u32(as_u16x2(NOE2)), ne = as_u32(as_u16x2(NE2));
+          if (COL0 && jj == 0 && c == 0)
+            column_merged_f16_asm<R, true>(tab, nv, selw, diag, upX, Hl, Xl, best, noe, ne);
+          else
+            column_merged_f16_asm<R, false>(tab, nv, selw, diag, upX, Hl, Xl, best, noe, ne);
+#else
+          const LutLookup<R> lk{tab, nv, selw};
+          __builtin_amdgcn_sched_barrier(0);
+          if (COL0 && jj == 0 && c == 0)
+            column_merged_f16<R, RB, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+          else
+            column_merged_f16<R, RB, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+#endif
         } else {
           // selector: byte 0 = code of the low target, byte 2 = code of the high target
           const uint32_t sel =
               (uint32_t)(jj & 3) | ((uint32_t)(4 + (jj & 3)) << 16) | 0x0C000C00u;
-          if constexpr (F16) {
-            // selector bytes {0x0C, code_lo, 0x0C, code_hi}: the LUT byte is the f16 high byte
-            const uint32_t sel16 =
-                0x0Cu | ((uint32_t)(jj & 3) << 8) | (0x0Cu << 16) | ((uint32_t)(4 + (jj & 3)) << 24);
-            const LutLookup<R> lk{tab, nv, __builtin_amdgcn_perm(whi, wlo, sel16) | 0x000C000Cu};
-            __builtin_amdgcn_sched_barrier(0);
-            if (COL0 && jj == 0 && c == 0)
-              column_merged_f16<R, RB, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
-            else
-              column_merged_f16<R, RB, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
-            asm volatile("" : "+v"(best));
-            rout[jj * ostride] = make_uint2(as_u32(Hl[R - 1]), as_u32(upX));
-            continue;
-          }
           const LutLookup<R> lk{tab, nv, __builtin_amdgcn_perm(whi, wlo, sel) | 0x0C000C00u};
           __builtin_amdgcn_sched_barrier(0);
           if constexpr (GOTOH) {
@@ -413,32 +506,69 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
 #pragma unroll
         for (int jj = 0; jj < C; ++jj) dst[jj * 64] = sink[jj * 64 + lane];
       }
+      if (last) {  // this wave's part of tile k is done
+        uint32_t* bs = bestsh + (k % W) * SWB_TILE;
+        atomicMax(&bs[lane], (uint32_t)best.x);
+        atomicMax(&bs[lane + 64], (uint32_t)best.y);
+        if (wave == W - 1) {  // every other wave folded tile k in an earlier phase
+          const size_t tlo = (size_t)tile * SWB_TILE + lane, thi = tlo + 64;
+          int32_t blo = (int32_t)bs[lane], bhi = (int32_t)bs[lane + 64];
+          bs[lane] = 0;
+          bs[lane + 64] = 0;
+          if constexpr (F16) {  // f16 bit patterns of non-negative integers -> int
+            blo = (int32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)blo);
+            bhi = (int32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)bhi);
+          }
+          if (a.accum) {  // best over the previous query segments
+            if (tlo < n) blo = max(blo, a.scores[tlo]);
+            if (thi < n) bhi = max(bhi, a.scores[thi]);
+          }
+          if (tlo < n) a.scores[tlo] = blo;
+          if (thi < n) a.scores[thi] = bhi;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          Hl[r] = H0;
+          Xl[r] = X0;
+        }
+        best = (u16x2){0, 0};
+        prevUpH = H0;
+        tile = ntile;
+        nch = nch_n;
+        nfull = nfull_n;
+        c = 0;
+        ++k;
+      } else {
+        ++c;
+      }
     }
     __syncthreads();
   }
+}
 
-  atomicMax(&bestsh[lane], (uint32_t)best.x);
-  atomicMax(&bestsh[lane + 64], (uint32_t)best.y);
-  __syncthreads();
-  if (wave == 0) {
-    int32_t blo = (int32_t)bestsh[lane], bhi = (int32_t)bestsh[lane + 64];
-    if constexpr (F16) {  // f16 bit patterns of non-negative integers -> int
-      blo = (int32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)blo);
-      bhi = (int32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)bhi);
-    }
-    if (a.accum) {  // best over the previous query segments
-      if (tlo < n) blo = max(blo, a.scores[tlo]);
-      if (thi < n) bhi = max(bhi, a.scores[thi]);
-    }
-    if (tlo < n) a.scores[tlo] = blo;
-    if (thi < n) a.scores[thi] = bhi;
-  }
+// Workgroups for a persistent launch: as many as fit on the device at once (occupancy x CUs),
+// then evened out so every workgroup gets the same number of tiles (+-1).  SWBANK_GRID=0 gives
+// one workgroup per tile; SWBANK_GRID=m caps the resident workgroups per CU at m (tuning).
+static unsigned persistent_grid(const void* fn, size_t ntiles, int threads, size_t lds) {
+  int dev = 0, cus = 0, occ = 0;
+  const char* env = std::getenv("SWBANK_GRID");
+  const int cap = (env && *env) ? std::atoi(env) : -1;
+  if (cap == 0) return (unsigned)ntiles;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, threads, lds) != hipSuccess ||
+      cus <= 0 || occ <= 0)
+    return (unsigned)ntiles;
+  if (cap > 0) occ = std::min(occ, cap);
+  const size_t slots = (size_t)cus * occ;
+  const size_t rounds = (ntiles + slots - 1) / slots;
+  return (unsigned)((ntiles + rounds - 1) / rounds);
 }
 
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16>
 static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st) {
   const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE;
-  const size_t lds = SWB_TILE * 4 +
+  const size_t lds = (size_t)W * SWB_TILE * 4 +
                      (size_t)(64 + 8 * 64 + (a.edge_in ? 2 * 8 * 64 : 0) +
                               (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8 +
                      (PROF ? prof_bytes : 0);
@@ -451,7 +581,8 @@ static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, h
     attr_set = true;
   }
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL(fn, dim3((unsigned)ntiles), dim3(64 * W), (unsigned)lds, st, a);
+  const unsigned grid = persistent_grid(reinterpret_cast<const void*>(fn), ntiles, 64 * W, lds);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * W), (unsigned)lds, st, a);
   return hipGetLastError();
 }
 
