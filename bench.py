@@ -36,11 +36,21 @@ sys.path.insert(0, os.path.join(REPO, "smith-waterman-fpga-module_amd"))
 sys.path.insert(0, REPO)
 
 # MI355X constants (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
-CUS, SIMD_PER_CU, LANES_PER_SIMD_CLK, CLK_GHZ = 256, 4, 32, 2.4
-VALU_PEAK_TOPS_U16 = CUS * SIMD_PER_CU * LANES_PER_SIMD_CLK * 2 * CLK_GHZ / 1e3  # 157.3
+CUS, SIMD_PER_CU, CLK_GHZ = 256, 4, 2.4
 HBM_PEAK_GBS = 8000.0
-# integer ops per cell — merged: 1 select, 6 max, 3 add; Gotoh: 11
-OPS_PER_CELL = {"merged": 10, "gotoh": 11}
+# VALU issue bound.  Packed 16-bit VALU ops (v_pk_*_f16/u16) and v_perm_b32 issue one wave64
+# instruction per 4 cycles per SIMD (scripts/ubench/valu_rate.hip on MI355X: 0.244-0.27
+# wave-instr/SIMD/cycle at 2.4 GHz; f32 ops reach 0.44).  One instruction advances one query
+# row for the lane's 2 targets, so a wave-instruction row covers 128 cells.  Instructions per
+# row of the kernel's column body (csrc/swbank_kernels.hip): f16 merged 7.5 (perm, 3 add,
+# 3.5 max3), u16 merged 9, u16 Gotoh 12.
+VALU_ISSUE_PER_SIMD_CLK = 0.25
+VALU_INSTR_PER_ROW = {"f16": 7.5, "u16": 9.0, "u16-gotoh": 12.0}
+
+
+def valu_peak_gcups(mode: str) -> float:
+    per_row = VALU_INSTR_PER_ROW[mode]
+    return CUS * SIMD_PER_CU * CLK_GHZ * VALU_ISSUE_PER_SIMD_CLK * 128 / per_row
 PEN = (5, -4, -12, -4)
 
 
@@ -212,8 +222,11 @@ def main():
     calls_per_step = len(wl.queries)
     score_s = score_ms / max(launches, 1) / 1e3 * calls_per_step
     pack_s = pack_ms / max(launches, 1) / 1e3 * calls_per_step
-    ops = OPS_PER_CELL[wl.model]
-    achieved_tops = ops * cells_rank / score_s / 1e12
+    kernel = wl.bank.last_kernel()
+    arith = "f16" if " f16" in kernel else "u16"
+    mode = arith if wl.model == "merged" else "u16-gotoh"
+    kernel_gcups = cells_rank / score_s / 1e9
+    peak_gcups = valu_peak_gcups(mode)
     # algorithmic bytes: 1 B per residue read once per query + 4 B per score written
     alg_bytes = len(wl.queries) * wl.n * (wl.L + 4) + sum(len(q) for q in wl.queries)
     traffic = pmc_traffic(wl.name)
@@ -229,7 +242,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u16",
+        "dtype": arith,
         "data": "synthetic",
         "config": {
             "workload": wl.desc,
@@ -240,13 +253,15 @@ def main():
             **wl.params,
             "parallelism": f"dp{world}: pairs sharded, RCCL gather of scores to rank 0",
         },
+        "kernel": kernel,
         "kernel_ms": {"pack": round(pack_s * 1e3, 4), "score": round(score_s * 1e3, 4)},
         "roofline": {
             "bound": "valu",
-            "achieved": round(achieved_tops, 2),
-            "peak": round(VALU_PEAK_TOPS_U16, 1),
-            "unit": f"Tops/s (u16 int ops, {ops} per cell)",
-            "frac": round(achieved_tops / VALU_PEAK_TOPS_U16, 4),
+            "achieved": round(kernel_gcups, 1),
+            "peak": round(peak_gcups, 1),
+            "unit": (f"GCUPS (VALU issue bound: {VALU_INSTR_PER_ROW[mode]} packed instr per "
+                     f"128 cells, 4 cyc/instr/SIMD, 1024 SIMDs at {CLK_GHZ} GHz)"),
+            "frac": round(kernel_gcups / peak_gcups, 4),
             "traffic": traffic,
         },
         "roofline_hbm": {

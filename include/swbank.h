@@ -132,6 +132,10 @@ sw_status sw_bank_set_timing(sw_bank *bank, int32_t enable);
 /* Synchronises on the recorded events and returns the launches and the summed device
  * milliseconds of the feeder (pack) and score kernels since the previous call. */
 sw_status sw_bank_timing(sw_bank *bank, uint64_t *launches, double *pack_ms, double *score_ms);
+/* Which kernel the last score call ran, e.g. "tile f16 R=32 W=4 segs=1 grid=998" or
+ * "wave u16 K=4" (empty before the first call).  No reference counterpart: the RTL has one
+ * datapath; this lets tests and profiles confirm the path taken. */
+const char *sw_last_kernel(const sw_bank *bank);
 
 /* ---- host-side helpers (no device needed) ---------------------------------------------- */
 /* ASCII -> codes for the alphabet; returns n. */

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -100,6 +101,8 @@ struct sw_bank {
   DevBuf<uint64_t> offs;
   DevBuf<uint32_t> lens;
   DevBuf<int32_t> scores;
+
+  char last_kernel[96] = {0};
 
   // profiling
   bool timing = false;
@@ -198,6 +201,8 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
 
 extern "C" const char* sw_last_error(const sw_bank* b) { return b ? b->err : "null bank"; }
 
+extern "C" const char* sw_last_kernel(const sw_bank* b) { return b ? b->last_kernel : ""; }
+
 static sw_status set_matrix_impl(sw_bank* b, const int8_t* m, int alpha, int32_t go,
                                  int32_t ge) {
   if (go > 0 || ge > 0 || go < -32767 || ge < -32767)
@@ -274,17 +279,21 @@ static sw_status prepare(sw_bank* b) {
   const int prof = (env_int("SWBANK_PROFILE", 0) || !lut) ? 1 : 0;
 
   const int qlen = (int)b->query.size();
-  // Rows per wave: 32 (16 for tiny queries).  Queries longer than one workgroup (512 rows)
-  // run as segments of SWBANK_SEG rows (default 256), each segment's bottom row handed to
-  // the next through HBM.  SWBANK_R / SWBANK_RB / SWBANK_SEG override (tuning only).
-  int R = qlen <= 16 ? 16 : 32, RB = 4;
-  int seg_rows = qlen > 512 ? env_int("SWBANK_SEG", 256) : std::max(qlen, 1);
-  R = env_int("SWBANK_R", R);
-  RB = env_int("SWBANK_RB", RB);
-  if (seg_rows % R != 0 && seg_rows < qlen)
-    return fail(b, SW_ERR_ARG, "segment rows %d not a multiple of R=%d", seg_rows, R);
   // the HDL column-0 rule differs from the plain recurrence only if a match pays for a gap
   const int col0 = (!gotoh && smax > o + e) ? 1 : 0;
+  // Rows per wave: 32 for the merged DNA LUT kernels; 16 for tiny queries and for the
+  // Gotoh / profile / column-0 variants, whose 32-row columns do not fit 128 VGPRs (the
+  // occupancy-4 budget) without spilling.  Queries longer than one workgroup (16 waves) run
+  // as segments of SWBANK_SEG rows (default 256), each segment's bottom row handed to the
+  // next through HBM.  SWBANK_R / SWBANK_RB / SWBANK_SEG override (tuning only).
+  int R = (qlen <= 16 || gotoh || prof || col0) ? 16 : 32, RB = 4;
+  R = env_int("SWBANK_R", R);
+  RB = env_int("SWBANK_RB", RB);
+  const int max_rows = (R >= 64 ? 8 : 16) * R;
+  int seg_rows = qlen > max_rows ? env_int("SWBANK_SEG", std::min(256, max_rows))
+                                 : std::max(qlen, 1);
+  if (seg_rows % R != 0 && seg_rows < qlen)
+    return fail(b, SW_ERR_ARG, "segment rows %d not a multiple of R=%d", seg_rows, R);
   if (!swk_has_variant(R, RB, col0, prof, gotoh ? 1 : 0, 0))
     return fail(b, SW_ERR_UNSUPPORTED, "no kernel variant R=%d RB=%d col0=%d prof=%d gotoh=%d", R,
                 RB, col0, prof, (int)gotoh);
@@ -295,7 +304,11 @@ static sw_status prepare(sw_bank* b) {
   // per segment: LUT words (W*R) or a query profile ((A+1) x PS bytes), concatenated
   std::vector<uint32_t> tab;
   std::vector<sw_bank::Seg> segs;
-  const uint32_t PS = prof ? (uint32_t)((Wseg * R + 15) / 16 * 16) : 0;
+  // profile row stride: a multiple of 16 B that is 16 mod 256, so the 16-B reads of lanes
+  // holding different letters fall in different LDS banks (a stride of 0 mod 256 puts every
+  // letter row on the same 4 banks)
+  uint32_t PS = prof ? (uint32_t)((Wseg * R + 15) / 16 * 16) : 0;
+  if (prof) PS += (16u + 256u - PS % 256u) % 256u;
   const uint32_t pad = prof ? (uint32_t)A : 4u;  // profile letter A = padding row (all 0xFF)
   const uint32_t nv = prof ? 0u : (uint32_t)(uint8_t)(S - sN) * 0x01010101u;
   for (int r0 = 0; r0 < std::max(qlen, 1); r0 += seg_rows) {
@@ -437,17 +450,41 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   const size_t nseg = b->segs.size();
   const uint32_t ecols = (max_len + 7) / 8 * 8;
   const size_t ntiles = (n + SWB_TILE - 1) / SWB_TILE;
-  // Kernel choice: the tile kernel needs many 128-target tiles to fill 256 CUs (each tile is
-  // one workgroup of W waves); with few targets the wave kernel (one wave per 2 targets,
-  // lanes = query rows) has 64x more parallelism.  Crossover measured on MI355X (128-row query,
-  // 128-bp targets): wave kernel ahead below ~190 tiles x 4 waves, tile kernel above (the tile
-  // kernel reaches ~1 resident wave per SIMD there).  SWBANK_KERNEL=tile|wave forces one.
+  const bool gotoh = b->cfg.gap_model == SW_GAP_GOTOH;
+  // f16 arithmetic (8 VALU per 2 cells instead of 9) when every value the recurrence can
+  // reach is an exact f16 integer: the positive bound min(|q|, max|t|) * max(s) + max(s)
+  // and the most negative intermediate both within 2048
+  const uint64_t top = std::min<uint64_t>(b->query.size(), max_len) * (uint64_t)std::max(0, b->smax) +
+                       (uint64_t)std::max(0, b->smax);
+  const bool use_f16 = b->f16 && top <= 2048u && b->f16_neg >= -2048 &&
+                       env_int("SWBANK_F16", 1) != 0;  // SWBANK_F16=0: u16 kernel (tests)
+  // Kernel choice by a throughput model calibrated on MI355X (scripts/kernel_choice.py):
+  //  tile kernel: base rate x fraction of the 256 CUs holding a tile x f(waves per SIMD),
+  //    f = min(1, 0.45 + 0.15 w), x 0.85 when the query runs as several segments;
+  //  wave kernel (queries <= 1024 rows): base rate x row fill (query / 64K lanes' rows) x
+  //    column fill (L / (L + 63): the 63-step skew of the lane pipeline).
+  // Base GCUPS: tile f16 9000, u16 merged 7400, u16 Gotoh 5800, profile merged 6500,
+  // profile Gotoh 5600; wave merged 6500, Gotoh 5000.  SWBANK_KERNEL=tile|wave forces one.
+  const double tiles = (double)ntiles, W = b->segs[0].W;
+  const double cu_frac = std::min(1.0, tiles / 256.0);
+  const double wps = std::min(4.0, std::max(1.0, std::ceil(tiles / 256.0)) * W / 4.0);
+  const double tile_base = use_f16 ? 9000 : b->prof ? (gotoh ? 5600 : 6500) : gotoh ? 5800 : 7400;
+  const double tile_est = tile_base * cu_frac * std::min(1.0, 0.45 + 0.15 * wps) *
+                          (nseg > 1 ? 0.85 : 1.0);
+  double wave_est = 0;
+  if (b->wK > 0) {
+    const double rowfill = (double)b->query.size() / (64.0 * b->wK);
+    const double colfill = max_len / (max_len + 63.0);
+    wave_est = (gotoh ? 5000 : 6500) * rowfill * colfill;
+  }
   const char* kforce = std::getenv("SWBANK_KERNEL");
-  bool use_wave = b->wK > 0 && ntiles * (size_t)b->segs[0].W < 768;
+  bool use_wave = b->wK > 0 && wave_est > tile_est;
   if (kforce && std::strcmp(kforce, "tile") == 0) use_wave = false;
   if (kforce && std::strcmp(kforce, "wave") == 0 && b->wK > 0) use_wave = true;
   if (use_wave) {
-    HIPOK(b, swk_launch_wave(b->wK, b->col0, b->prof, b->cfg.gap_model == SW_GAP_GOTOH ? 1 : 0,
+    snprintf(b->last_kernel, sizeof(b->last_kernel), "wave %s K=%d",
+             b->prof ? "u16-profile" : "u16", b->wK);
+    HIPOK(b, swk_launch_wave(b->wK, b->col0, b->prof, gotoh ? 1 : 0,
                              d_res, d_offs, d_lens, n, b->wtab.p, b->nv, b->S, b->O, b->E,
                              b->wPS, b->pad, d_scores, st));
   }
@@ -456,13 +493,9 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
     HIPOK(b, b->edge[0].reserve(words));
     HIPOK(b, b->edge[1].reserve(words));
   }
-  // f16 arithmetic (8 VALU per 2 cells instead of 9) when every value the recurrence can
-  // reach is an exact f16 integer: the positive bound min(|q|, max|t|) * max(s) + max(s)
-  // and the most negative intermediate both within 2048
-  const uint64_t top = std::min<uint64_t>(b->query.size(), max_len) * (uint64_t)std::max(0, b->smax) +
-                       (uint64_t)std::max(0, b->smax);
-  const bool use_f16 = b->f16 && top <= 2048u && b->f16_neg >= -2048 &&
-                       env_int("SWBANK_F16", 1) != 0;  // SWBANK_F16=0: u16 kernel (tests)
+  if (!use_wave)
+    snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=%zu",
+             use_f16 ? "f16" : "u16", b->prof ? "-profile" : "", b->R, b->segs[0].W, nseg);
   for (size_t s = 0; !use_wave && s < nseg; ++s) {
     const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
     void* eout = s + 1 < nseg ? b->edge[s & 1].p : nullptr;

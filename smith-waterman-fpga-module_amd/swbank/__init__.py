@@ -39,6 +39,7 @@ EXPORTS = (
     "sw_set_penalties", "sw_set_matrix", "sw_load_query", "sw_score_batch",
     "sw_score_batch_device", "sw_best_hit", "sw_encode_ascii", "sw_pack_2bit",
     "sw_unpack_2bit", "sw_fill_matrix", "sw_bank_set_timing", "sw_bank_timing",
+    "sw_last_kernel",
 )
 
 
@@ -97,6 +98,7 @@ def lib() -> ctypes.CDLL:
         "sw_fill_matrix": (i32, [i32, i32, i32, P]),
         "sw_bank_set_timing": (i32, [P, i32]),
         "sw_bank_timing": (i32, [P, P, P, P]),
+        "sw_last_kernel": (ctypes.c_char_p, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -250,6 +252,10 @@ class ScoreBank:
     # profiling
     def set_timing(self, enable: bool = True):
         self._check(lib().sw_bank_set_timing(self._h, 1 if enable else 0))
+
+    def last_kernel(self) -> str:
+        """The kernel the last score call ran (e.g. "tile f16 R=32 W=4 segs=1 grid=998")."""
+        return lib().sw_last_kernel(self._h).decode()
 
     def timing(self) -> Tuple[int, float, float]:
         """(launches, pack_ms, score_ms) accumulated since the previous call."""

@@ -129,7 +129,7 @@ def test_edge_shapes(bank):
 
 @pytest.mark.parametrize("qlen", [200, 407, 408, 409, 410, 512])
 @pytest.mark.parametrize("match", [5, 8, 9, 16])
-def test_f16_bound_edges(bank, qlen, match):
+def test_f16_bound_edges(bank, qlen, match, kernel_choice):
     """Scores at and past the f16 kernel's exact range: the host takes the f16 tile kernel
     only while min(|q|, max|t|) * max(s) + max(s) <= 2048 and every substitution score is an
     f16 with a zero low byte (match 9 is not: u16 kernel); perfect and near-perfect matches
@@ -148,6 +148,11 @@ def test_f16_bound_edges(bank, qlen, match):
     res, offs, lens = O.pack_residues(seqs)
     want = O.score_batch(q, res, offs, lens, O.dna_matrix(match, -4), -12, -4)
     assert got[0] == match * qlen
+    if kernel_choice == "tile":
+        f16 = match != 9 and qlen * match + match <= 2048
+        assert bank.last_kernel().startswith("tile f16" if f16 else "tile u16"), bank.last_kernel()
+    elif kernel_choice == "tile-u16":
+        assert bank.last_kernel().startswith("tile u16")
     assert (got == want).all(), [(i, int(got[i]), int(want[i])) for i in np.nonzero(got != want)[0][:8]]
 
 
