@@ -38,14 +38,19 @@ sys.path.insert(0, REPO)
 # MI355X constants (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 CUS, SIMD_PER_CU, CLK_GHZ = 256, 4, 2.4
 HBM_PEAK_GBS = 8000.0
-# VALU issue bound.  Packed 16-bit VALU ops (v_pk_*_f16/u16) and v_perm_b32 issue one wave64
-# instruction per 4 cycles per SIMD (scripts/ubench/valu_rate.hip on MI355X: 0.244-0.27
-# wave-instr/SIMD/cycle at 2.4 GHz; f32 ops reach 0.44).  One instruction advances one query
-# row for the lane's 2 targets, so a wave-instruction row covers 128 cells.  Instructions per
-# row of the kernel's column body (csrc/swbank_kernels.hip): f16 merged 7.5 (perm, 3 add,
-# 3.5 max3), u16 merged 9, u16 Gotoh 12.
+# VALU roofline.  Algorithmic work = 10 ops per cell for the merged-gap
+# recurrence, 11 for Gotoh (1 select, 6 max, 3 add).  Peak = packed 16-bit VALU rate: packed
+# ops (v_pk_*_f16/u16) and v_perm_b32 issue one wave64 instruction per 4 cycles per SIMD
+# (scripts/ubench/valu_rate.hip on MI355X: 0.244-0.27 wave-instr/SIMD/cycle at 2.4 GHz; f32
+# ops reach 0.44) = 16 lanes x 2 halves per clock per SIMD -> 78.6 T ops/s.  max3 and perm fuse
+# several algorithmic ops into one instruction, so frac > 1 is possible.
+# Issue bound: one instruction advances one query row for a lane's 2 targets (128 cells per
+# wave-instruction); instructions per row of the column body (csrc/swbank_kernels.hip):
+# tile f16 merged 7.5, tile u16 merged 9, tile u16 Gotoh 11 (+0.1-0.7 of loop overhead).
+OPS_PER_CELL = {"merged": 10, "gotoh": 11}
+VALU_PEAK_TOPS_16 = CUS * SIMD_PER_CU * 16 * 2 * CLK_GHZ / 1e3  # 78.6
 VALU_ISSUE_PER_SIMD_CLK = 0.25
-VALU_INSTR_PER_ROW = {"f16": 7.5, "u16": 9.0, "u16-gotoh": 12.0}
+VALU_INSTR_PER_ROW = {"f16": 7.5, "u16": 9.0, "u16-gotoh": 11.0}
 
 
 def valu_peak_gcups(mode: str) -> float:
@@ -226,7 +231,10 @@ def main():
     arith = "f16" if " f16" in kernel else "u16"
     mode = arith if wl.model == "merged" else "u16-gotoh"
     kernel_gcups = cells_rank / score_s / 1e9
-    peak_gcups = valu_peak_gcups(mode)
+    # the issue bound is for the tile kernel's column body; the wave kernel's differs
+    peak_gcups = valu_peak_gcups(mode) if kernel.startswith("tile") else None
+    ops = OPS_PER_CELL[wl.model]
+    achieved_tops = ops * kernel_gcups / 1e3
     # algorithmic bytes: 1 B per residue read once per query + 4 B per score written
     alg_bytes = len(wl.queries) * wl.n * (wl.L + 4) + sum(len(q) for q in wl.queries)
     traffic = pmc_traffic(wl.name)
@@ -257,12 +265,15 @@ def main():
         "kernel_ms": {"pack": round(pack_s * 1e3, 4), "score": round(score_s * 1e3, 4)},
         "roofline": {
             "bound": "valu",
-            "achieved": round(kernel_gcups, 1),
-            "peak": round(peak_gcups, 1),
-            "unit": (f"GCUPS (VALU issue bound: {VALU_INSTR_PER_ROW[mode]} packed instr per "
-                     f"128 cells, 4 cyc/instr/SIMD, 1024 SIMDs at {CLK_GHZ} GHz)"),
-            "frac": round(kernel_gcups / peak_gcups, 4),
+            "achieved": round(achieved_tops, 2),
+            "peak": round(VALU_PEAK_TOPS_16, 1),
+            "unit": (f"T ops/s ({ops} algorithmic int ops per cell, SURVEY 8.2; peak = packed "
+                     f"16-bit VALU, 1024 SIMDs x 32 ops/clk x {CLK_GHZ} GHz, measured issue rate)"),
+            "frac": round(achieved_tops / VALU_PEAK_TOPS_16, 4),
             "traffic": traffic,
+            "kernel_gcups": round(kernel_gcups, 1),
+            "issue_bound_gcups": round(peak_gcups, 1) if peak_gcups else None,
+            "issue_frac": round(kernel_gcups / peak_gcups, 4) if peak_gcups else None,
         },
         "roofline_hbm": {
             "bound": "hbm",

@@ -27,7 +27,7 @@ def mean_counter(name):
     vals = []
     for f in glob.glob(os.path.join(pmc, "*", "pmc_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "score_dna" in r["Kernel_Name"] and r["Counter_Name"] == name:
+            if "score_kernel" in r["Kernel_Name"] and r["Counter_Name"] == name:
                 vals.append(float(r["Counter_Value"]))
     return sum(vals) / len(vals) if vals else None
 
