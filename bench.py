@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--reads", type=int, default=131072, help="reads150x1k: reads per GPU")
     ap.add_argument("--slice", type=int, default=16, help="reads150x1k: 1-kbp targets")
     ap.add_argument("--ptargets", type=int, default=12500, help="protein512x1k: per GPU")
+    ap.add_argument("--records", action="store_true",
+                    help="q100xdata500: feed the targets as 64-byte CAPI sequence_t records "
+                         "(2-bit codes, aligner_Header.h) instead of one code byte per base")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="wall budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--profile-only", action="store_true",
@@ -151,6 +154,12 @@ class Workload:
         self.d_offs = torch.arange(n, dtype=torch.int64, device=dev) * L
         self.d_lens = torch.full((n,), L, dtype=torch.int32, device=dev)
         self.d_sc = torch.zeros((len(self.queries), n), dtype=torch.int32, device=dev)
+        self.d_rec = None
+        if getattr(args, "records", False):
+            if w != "q100xdata500" or L > S.RECORD_MAX_BASES:
+                raise SystemExit("--records: q100xdata500 with targets <= 232 bp only")
+            self.d_rec = torch.from_numpy(S.make_records(self.batch).reshape(-1)).to(dev)
+            self.desc += "; targets as CAPI 2-bit sequence_t records"
         if len(self.queries) == 1:
             self.bank.load_query(self.queries[0])
         self.cells = sum(len(q) for q in self.queries) * n * L
@@ -159,6 +168,10 @@ class Workload:
         for k, q in enumerate(self.queries):
             if len(self.queries) > 1:
                 self.bank.load_query(q)  # ld_sequence: a new query for the same batch
+            if self.d_rec is not None:
+                self.bank.score_records_device(self.d_rec.data_ptr(), self.n,
+                                               self.d_sc[k].data_ptr(), stream)
+                continue
             self.bank.score_batch_device(self.d_res.data_ptr(), self.d_offs.data_ptr(),
                                          self.d_lens.data_ptr(), self.n, self.L,
                                          self.d_sc[k].data_ptr(), stream)
@@ -236,7 +249,8 @@ def main():
     ops = OPS_PER_CELL[wl.model]
     achieved_tops = ops * kernel_gcups / 1e3
     # algorithmic bytes: 1 B per residue read once per query + 4 B per score written
-    alg_bytes = len(wl.queries) * wl.n * (wl.L + 4) + sum(len(q) for q in wl.queries)
+    per_target = S.RECORD_BYTES if wl.d_rec is not None else wl.L
+    alg_bytes = len(wl.queries) * wl.n * (per_target + 4) + sum(len(q) for q in wl.queries)
     traffic = pmc_traffic(wl.name)
 
     out = {

@@ -120,6 +120,22 @@ sw_status sw_score_batch_device(sw_bank *bank, const uint8_t *d_residues,
                                 const uint64_t *d_offsets, const uint32_t *d_lens, size_t n,
                                 uint32_t max_len, int32_t *d_scores, void *stream);
 
+/* ---- CAPI record path: the reference host's packed wire format ---------
+ * A record is the 64-byte `sequence_t` of capi_sample_aligner/.../aligner_Header.h:19-24:
+ * { u32 ID; u16 length; u8 data[58]; } with 2-bit codes LSB-first (charTo2bit,
+ * aligner_Header.c:14-47: T=0 C=1 A=2 G=3), at most 232 bases.  main_test.c:297-314 builds
+ * such an array (query in record 0, targets after it) and hands it to the AFU through the
+ * WED; here the query comes from sw_load_query_record and every record passed to
+ * sw_score_records is a target.  DNA banks only (2 bits cannot carry N). */
+#define SW_RECORD_BYTES 64
+#define SW_RECORD_MAX_BASES 232
+sw_status sw_load_query_record(sw_bank *bank, const void *record);
+/* Host records in, unbiased scores out in input order (the kernel reads the 2-bit codes). */
+sw_status sw_score_records(sw_bank *bank, const void *records, size_t n, int32_t *scores_out);
+/* Device-resident records (n x 64 B) -> device scores, asynchronous on `stream`. */
+sw_status sw_score_records_device(sw_bank *bank, const void *d_records, size_t n,
+                                  int32_t *d_scores, void *stream);
+
 /* Best hit of the last sw_score_batch (≙ max / vld_max): the lowest index with the maximum
  * score; *best_id = ids ? ids[index] : index. */
 sw_status sw_best_hit(sw_bank *bank, const int32_t *scores, const uint64_t *ids, size_t n,

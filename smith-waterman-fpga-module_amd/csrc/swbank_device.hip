@@ -22,14 +22,14 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, cons
                                       const uint64_t* offs, const uint32_t* lens, size_t n,
                                       const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
-                                      hipStream_t st);
+                                      int packed, hipStream_t st);
 extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh, int f16,
                                        const uint8_t* res, const uint64_t* offs,
                                        const uint32_t* lens, size_t n, const uint32_t* qtab,
                                        uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                        const void* edge_in, void* edge_out, uint32_t ecols,
-                                       int accum, hipStream_t st);
+                                       int accum, int packed, hipStream_t st);
 
 namespace {
 int env_int(const char* name, int dflt) {
@@ -434,9 +434,10 @@ static sw_status range_check(sw_bank* b, uint32_t max_len) {
   return SW_OK;
 }
 
+// packed: d_res holds n 64-byte CAPI records (2-bit codes); d_offs/d_lens are unused.
 static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                         const uint32_t* d_lens, size_t n, uint32_t max_len, int32_t* d_scores,
-                        hipStream_t st) {
+                        hipStream_t st, bool packed = false) {
   sw_bank::Ev ev{};
   if (b->timing) {
     HIPOK(b, hipEventCreate(&ev.a));
@@ -486,7 +487,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
              b->prof ? "u16-profile" : "u16", b->wK);
     HIPOK(b, swk_launch_wave(b->wK, b->col0, b->prof, gotoh ? 1 : 0,
                              d_res, d_offs, d_lens, n, b->wtab.p, b->nv, b->S, b->O, b->E,
-                             b->wPS, b->pad, d_scores, st));
+                             b->wPS, b->pad, d_scores, packed ? 1 : 0, st));
   }
   if (!use_wave && nseg > 1) {
     const size_t words = std::max<size_t>(1, ntiles * ecols * 64);
@@ -505,7 +506,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                               (use_f16 ? b->qtab16.p : b->qtab.p) + b->segs[s].off,
                               use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E, b->PS,
                               b->pad, b->segs[s].W, d_scores, ein, eout, ecols, s > 0 ? 1 : 0,
-                              st));
+                              packed ? 1 : 0, st));
   }
   if (b->timing) {
     HIPOK(b, hipEventRecord(ev.c, st));
@@ -579,6 +580,79 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const u
   HIPOK(b, hipMemcpyAsync(sorted.data(), b->scores.p, n * 4, hipMemcpyDeviceToHost, b->stream));
   HIPOK(b, hipStreamSynchronize(b->stream));
   for (size_t k = 0; k < n; ++k) scores_out[order[k]] = sorted[k];
+  return SW_OK;
+}
+
+// ---- CAPI record path (row f2): sequence_t arrays as the reference host builds them ------
+static inline uint32_t record_len(const uint8_t* rec) {
+  uint16_t l;
+  std::memcpy(&l, rec + 4, 2);
+  return l;
+}
+
+extern "C" sw_status sw_load_query_record(sw_bank* b, const void* record) {
+  if (!b || !record) return SW_ERR_ARG;
+  if (b->alpha != SW_DNA_ALPHA) return fail(b, SW_ERR_UNSUPPORTED, "records carry DNA only");
+  const uint8_t* rec = static_cast<const uint8_t*>(record);
+  const uint32_t len = record_len(rec);
+  if (len > SWB_RECORD_MAX) return fail(b, SW_ERR_ARG, "record length %u > %u", len, SWB_RECORD_MAX);
+  uint32_t id;
+  std::memcpy(&id, rec, 4);
+  uint8_t codes[SWB_RECORD_MAX];
+  for (uint32_t j = 0; j < len; ++j) codes[j] = (rec[6 + j / 4] >> (2 * (j % 4))) & 3u;
+  return sw_load_query(b, id, codes, len);
+}
+
+extern "C" sw_status sw_score_records_device(sw_bank* b, const void* d_records, size_t n,
+                                             int32_t* d_scores, void* stream) {
+  if (!b) return SW_ERR_ARG;
+  if (n == 0) return SW_OK;
+  if (!d_records || !d_scores) return fail(b, SW_ERR_ARG, "null device buffer");
+  if (b->alpha != SW_DNA_ALPHA) return fail(b, SW_ERR_UNSUPPORTED, "records carry DNA only");
+  sw_status st = prepare(b);
+  if (st != SW_OK) return st;
+  // lengths live on the device: bound them by the record capacity
+  if ((st = range_check(b, SWB_RECORD_MAX)) != SW_OK) return st;
+  HIPOK(b, hipSetDevice(b->device));
+  return launch(b, static_cast<const uint8_t*>(d_records), nullptr, nullptr, n, SWB_RECORD_MAX,
+                d_scores, stream ? reinterpret_cast<hipStream_t>(stream) : b->stream, true);
+}
+
+extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
+                                      int32_t* scores_out) {
+  if (!b) return SW_ERR_ARG;
+  if (n == 0) return SW_OK;
+  if (!records || !scores_out) return fail(b, SW_ERR_ARG, "null host buffer");
+  if (b->alpha != SW_DNA_ALPHA) return fail(b, SW_ERR_UNSUPPORTED, "records carry DNA only");
+  sw_status st = prepare(b);
+  if (st != SW_OK) return st;
+  const uint8_t* recs = static_cast<const uint8_t*>(records);
+  std::vector<uint32_t> order(n);
+  std::iota(order.begin(), order.end(), 0u);
+  for (size_t k = 0; k < n; ++k)
+    if (record_len(recs + k * SWB_RECORD) > SWB_RECORD_MAX)
+      return fail(b, SW_ERR_ARG, "record %zu length %u > %u", k, record_len(recs + k * SWB_RECORD),
+                  SWB_RECORD_MAX);
+  // longest first, as sw_score_batch (PrioEncoder order)
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t c) {
+    return record_len(recs + (size_t)a * SWB_RECORD) > record_len(recs + (size_t)c * SWB_RECORD);
+  });
+  const uint32_t max_len = record_len(recs + (size_t)order[0] * SWB_RECORD);
+  if ((st = range_check(b, max_len)) != SW_OK) return st;
+  std::vector<uint8_t> sorted(n * SWB_RECORD);
+  for (size_t k = 0; k < n; ++k)
+    std::memcpy(sorted.data() + k * SWB_RECORD, recs + (size_t)order[k] * SWB_RECORD, SWB_RECORD);
+  HIPOK(b, hipSetDevice(b->device));
+  HIPOK(b, b->res.reserve(sorted.size()));
+  HIPOK(b, b->scores.reserve(n));
+  HIPOK(b, hipMemcpyAsync(b->res.p, sorted.data(), sorted.size(), hipMemcpyHostToDevice,
+                          b->stream));
+  st = launch(b, b->res.p, nullptr, nullptr, n, max_len, b->scores.p, b->stream, true);
+  if (st != SW_OK) return st;
+  std::vector<int32_t> out(n);
+  HIPOK(b, hipMemcpyAsync(out.data(), b->scores.p, n * 4, hipMemcpyDeviceToHost, b->stream));
+  HIPOK(b, hipStreamSynchronize(b->stream));
+  for (size_t k = 0; k < n; ++k) scores_out[order[k]] = out[k];
   return SW_OK;
 }
 

@@ -12,4 +12,8 @@
 /* Selector byte that reads 0x00 from v_perm_b32. */
 #define SWB_SEL_ZERO 0x0Cu
 
+/* CAPI sequence record (aligner_Header.h:19-24): u32 ID, u16 length, u8 data[58]. */
+#define SWB_RECORD 64
+#define SWB_RECORD_MAX 232u
+
 #endif

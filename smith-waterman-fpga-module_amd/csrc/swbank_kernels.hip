@@ -222,10 +222,35 @@ struct Lane2 {
 // end the code is `pad` (LUT mode: 4 = N, s(*, N) <= 0; profile mode: a row of S - s = 255),
 // so padding can only lower a score.  `full` (uniform): every lane has >= 8 codes left in
 // both targets -> two unaligned 8-byte loads.
+// 8 two-bit codes (LSB-first, charTo2bit order) -> 8 code bytes.
+__device__ __forceinline__ uint2 unpack8(uint32_t b) {
+  return make_uint2((b & 3u) | ((b << 6) & 0x300u) | ((b << 12) & 0x30000u) |
+                        ((b << 18) & 0x3000000u),
+                    ((b >> 8) & 3u) | ((b >> 2) & 0x300u) | ((b << 4) & 0x30000u) |
+                        ((b << 10) & 0x3000000u));
+}
+// Past-the-end codes of a chunk -> pad (bytes k with j0 + k >= len).
+__device__ __forceinline__ uint2 pad_tail(uint2 w, uint32_t j0, uint32_t len, uint32_t pad) {
+  const uint32_t n = len > j0 ? min(len - j0, 8u) : 0u;  // valid codes in this chunk
+  const uint64_t keep = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
+  const uint64_t v = ((uint64_t)w.y << 32 | w.x) & keep;
+  const uint64_t p = (pad * 0x0101010101010101ull) & ~keep;
+  return make_uint2((uint32_t)(v | p), (uint32_t)((v | p) >> 32));
+}
+
 __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint32_t pad,
-                                         uint2& lo, uint2& hi) {
+                                         bool packed, uint2& lo, uint2& hi) {
   const uint32_t j0 = (uint32_t)c * 8;
-  if (full) {
+  if (packed) {  // CAPI records: 2 bytes per 8 codes, always inside the 58-byte data field
+    const uint32_t x = *reinterpret_cast<const uint16_t*>(t.plo + 2 * c);
+    const uint32_t y = *reinterpret_cast<const uint16_t*>(t.phi + 2 * c);
+    lo = unpack8(x);
+    hi = unpack8(y);
+    if (!full) {
+      lo = pad_tail(lo, j0, t.llo, pad);
+      hi = pad_tail(hi, j0, t.lhi, pad);
+    }
+  } else if (full) {
     lo = *reinterpret_cast<const uint2*>(t.plo + j0);
     hi = *reinterpret_cast<const uint2*>(t.phi + j0);
   } else {
@@ -245,11 +270,20 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint3
   }
 }
 
-// Per-tile metadata of one lane (uniform tile id).
+// Per-tile metadata of one lane (uniform tile id).  packed: `res` is an array of 64-byte CAPI
+// records {u32 ID, u16 length, u8 data[58]} (aligner_Header.h:19-24).
 __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t* offs,
-                                              const uint32_t* lens, size_t n, int tile, int lane) {
+                                              const uint32_t* lens, size_t n, int tile, int lane,
+                                              bool packed) {
   Lane2 t;
   const size_t a = (size_t)tile * SWB_TILE + lane, b = a + 64;
+  if (packed) {
+    t.llo = a < n ? *reinterpret_cast<const uint16_t*>(res + a * SWB_RECORD + 4) : 0u;
+    t.lhi = b < n ? *reinterpret_cast<const uint16_t*>(res + b * SWB_RECORD + 4) : 0u;
+    t.plo = res + (a < n ? a : 0) * SWB_RECORD + 6;
+    t.phi = res + (b < n ? b : 0) * SWB_RECORD + 6;
+    return t;
+  }
   t.llo = a < n ? lens[a] : 0u;
   t.lhi = b < n ? lens[b] : 0u;
   // an empty target still needs a readable address for the branch-free slow path
@@ -291,6 +325,7 @@ struct ScoreArgs {
   uint2* edge_out;
   uint32_t ecols;
   uint32_t accum;
+  uint32_t packed;        // res = 64-byte CAPI records (2-bit codes); offs/lens unused
 };
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -306,9 +341,14 @@ __device__ __forceinline__ void dma_edge_chunk(const uint2* src, uint2* dst, int
 }
 
 // Chunk count of a tile (uniform), from the lengths alone.
-__device__ __forceinline__ int tile_nch(const uint32_t* lens, size_t n, int tile, int lane) {
+__device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens, size_t n,
+                                        int tile, int lane, bool packed) {
   const size_t a = (size_t)tile * SWB_TILE + lane, b = a + 64;
-  uint32_t L = max(a < n ? lens[a] : 0u, b < n ? lens[b] : 0u);
+  auto len = [&](size_t k) -> uint32_t {
+    if (k >= n) return 0u;
+    return packed ? *reinterpret_cast<const uint16_t*>(res + k * SWB_RECORD + 4) : lens[k];
+  };
+  uint32_t L = max(len(a), len(b));
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) L = max(L, (uint32_t)__shfl_xor((int)L, off));
   return max(1, (int)((__builtin_amdgcn_readfirstlane(L) + 7) / 8));
@@ -343,10 +383,12 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int ntiles = (int)((n + SWB_TILE - 1) / SWB_TILE);
   const int G = (int)gridDim.x;
   int total = 0;  // chunks of all this workgroup's tiles: every wave runs total + W - 1 phases
-  for (int t = blockIdx.x; t < ntiles; t += G) total += tile_nch(a.lens, n, t, lane);
+  const bool packed = a.packed != 0;
+  for (int t = blockIdx.x; t < ntiles; t += G)
+    total += tile_nch(a.res, a.lens, n, t, lane, packed);
 
   int tile = blockIdx.x;
-  Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane);
+  Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed);
   int nch, nfull;
   tile_chunks(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
               nfull);
@@ -394,7 +436,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   u16x2 best = {0, 0};
   u16x2 prevUpH = H0;  // H(row above, column -1)
   uint2 rlo, rhi;      // raw codes of the next chunk (prefetched one phase ahead)
-  load_raw(cur, 0, nfull > 0, a.pad, rlo, rhi);
+  load_raw(cur, 0, nfull > 0, a.pad, packed, rlo, rhi);
   __syncthreads();
 
   // branch-free hand-off: wave 0 reads the top boundary (constant, stride 0, or the previous
@@ -414,12 +456,12 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       const bool last = c + 1 == nch;
       const int ntile = tile + G;
       if (!last) {
-        load_raw(cur, c + 1, c + 1 < nfull, a.pad, rlo, rhi);
+        load_raw(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
       } else if (ntile < ntiles) {  // first chunk of the next tile
-        cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane);
+        cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed);
         tile_chunks(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
                     n, nch_n, nfull_n);
-        load_raw(cur, 0, nfull_n > 0, a.pad, rlo, rhi);
+        load_raw(cur, 0, nfull_n > 0, a.pad, packed, rlo, rhi);
       }
       const int slot = g & 1;
       if (seg_in && wave == 0 && (!last || ntile < ntiles))  // next chunk's boundary row
@@ -654,9 +696,15 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
   const size_t tA = 2 * pair, tB = tA + 1;
   const size_t n = a.n;
   if (tA >= n) return;  // whole wave
-  const uint32_t LA = a.lens[tA], LB = tB < n ? a.lens[tB] : 0u;
-  const uint8_t* pA = a.res + (LA ? a.offs[tA] : 0);
-  const uint8_t* pB = a.res + (LB ? a.offs[tB] : 0);
+  const bool packed = a.packed != 0;
+  const uint32_t LA = packed ? *reinterpret_cast<const uint16_t*>(a.res + tA * SWB_RECORD + 4)
+                             : a.lens[tA];
+  const uint32_t LB = tB >= n ? 0u
+                      : packed ? *reinterpret_cast<const uint16_t*>(a.res + tB * SWB_RECORD + 4)
+                               : a.lens[tB];
+  const uint8_t* pA = packed ? a.res + tA * SWB_RECORD + 6 : a.res + (LA ? a.offs[tA] : 0);
+  const uint8_t* pB = packed ? a.res + (tB < n ? tB : tA) * SWB_RECORD + 6
+                             : a.res + (LB ? a.offs[tB] : 0);
   const int Lmax = (int)__builtin_amdgcn_readfirstlane(max(LA, LB));
   const uint32_t S = a.S, pad = a.pad;
   const u16x2 S2 = {(unsigned short)S, (unsigned short)S};
@@ -688,8 +736,14 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
   for (int t = 0; t < nsteps; ++t) {
     if ((t & 63) == 0) {  // next 64 columns of both targets, one code pair per lane
       const uint32_t c = (uint32_t)t + lane;
-      const uint32_t x = c < LA ? (uint32_t)pA[c] : pad;
-      const uint32_t y = c < LB ? (uint32_t)pB[c] : pad;
+      uint32_t x = pad, y = pad;
+      if (packed) {
+        if (c < LA) x = (pA[c >> 2] >> (2 * (c & 3))) & 3u;
+        if (c < LB) y = (pB[c >> 2] >> (2 * (c & 3))) & 3u;
+      } else {
+        if (c < LA) x = pA[c];
+        if (c < LB) y = pB[c];
+      }
       buf = min(x, pad) | (min(y, pad) << 16) | 0x0C000C00u;
     }
     const uint32_t inj = __builtin_amdgcn_readlane(buf, t & 63);
@@ -798,11 +852,11 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                        const void* edge_in, void* edge_out, uint32_t ecols,
-                                       int accum, hipStream_t st) {
+                                       int accum, int packed, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                          O,    E,    PS,   pad, scores, static_cast<const uint2*>(edge_in),
-                         static_cast<uint2*>(edge_out), ecols, (uint32_t)accum};
+                         static_cast<uint2*>(edge_out), ecols, (uint32_t)accum, (uint32_t)packed};
   const uint32_t prof_bytes = (pad + 1) * PS;
 #define SWK_CASE(RR, BB, C0, PF, GT, FH)                                                      \
   if (R == RR && RB == BB && col0 == C0 && prof == PF && gotoh == GT && f16 == FH)            \
@@ -822,10 +876,10 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, cons
                                       const uint64_t* offs, const uint32_t* lens, size_t n,
                                       const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
-                                      hipStream_t st) {
+                                      int packed, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
-                         nullptr, nullptr, 0u, 0u};
+                         nullptr, nullptr, 0u, 0u, (uint32_t)packed};
   const uint32_t prof_bytes = (pad + 1) * PS;
 #define SWK_WCASE(KK, C0, PF, GT)                                                  \
   if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                          \

@@ -39,8 +39,9 @@ EXPORTS = (
     "sw_set_penalties", "sw_set_matrix", "sw_load_query", "sw_score_batch",
     "sw_score_batch_device", "sw_best_hit", "sw_encode_ascii", "sw_pack_2bit",
     "sw_unpack_2bit", "sw_fill_matrix", "sw_bank_set_timing", "sw_bank_timing",
-    "sw_last_kernel",
+    "sw_last_kernel", "sw_load_query_record", "sw_score_records", "sw_score_records_device",
 )
+RECORD_BYTES, RECORD_MAX_BASES = 64, 232
 
 
 class SwbankError(RuntimeError):
@@ -99,6 +100,9 @@ def lib() -> ctypes.CDLL:
         "sw_bank_set_timing": (i32, [P, i32]),
         "sw_bank_timing": (i32, [P, P, P, P]),
         "sw_last_kernel": (ctypes.c_char_p, [P]),
+        "sw_load_query_record": (i32, [P, P]),
+        "sw_score_records": (i32, [P, P, sz, P]),
+        "sw_score_records_device": (i32, [P, P, sz, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -142,6 +146,35 @@ def unpack_2bit(packed: np.ndarray, n: int) -> np.ndarray:
     out = np.zeros(max(n, 1), dtype=np.uint8)
     lib().sw_unpack_2bit(_p(packed), n, _p(out))
     return out[:n]
+
+
+def make_records(seqs: Sequence[np.ndarray], ids: Optional[Sequence[int]] = None) -> np.ndarray:
+    """DNA code arrays (0..3) -> CAPI `sequence_t` records, one 64-byte row each
+    (aligner_Header.h:19-24: u32 ID, u16 length, 58 bytes of 2-bit codes LSB-first)."""
+    out = np.zeros((len(seqs), RECORD_BYTES), dtype=np.uint8)
+    if isinstance(seqs, np.ndarray) and seqs.ndim == 2:  # equal lengths: vectorised
+        n, L = seqs.shape
+        if L > RECORD_MAX_BASES or (seqs.size and seqs.max() > 3):
+            raise ValueError(f"records need <= {RECORD_MAX_BASES} ACGT codes")
+        idv = np.arange(n, dtype=np.uint32) if ids is None else np.asarray(ids, np.uint32)
+        out[:, 0:4] = idv.view(np.uint8).reshape(n, 4)
+        out[:, 4:6] = np.full(n, L, np.uint16).view(np.uint8).reshape(n, 2)
+        q = np.zeros((n, (L + 3) // 4 * 4), dtype=np.uint8)
+        q[:, :L] = seqs
+        q = q.reshape(n, -1, 4)
+        out[:, 6:6 + q.shape[1]] = q[..., 0] | q[..., 1] << 2 | q[..., 2] << 4 | q[..., 3] << 6
+        return out
+    for k, sq in enumerate(seqs):
+        c = np.asarray(sq, dtype=np.uint8)
+        if len(c) > RECORD_MAX_BASES or (len(c) and c.max() > 3):
+            raise ValueError(f"record {k}: needs <= {RECORD_MAX_BASES} ACGT codes")
+        out[k, 0:4] = np.frombuffer(np.uint32(k if ids is None else ids[k]).tobytes(), np.uint8)
+        out[k, 4:6] = np.frombuffer(np.uint16(len(c)).tobytes(), np.uint8)
+        q = np.zeros((len(c) + 3) // 4 * 4, dtype=np.uint8)
+        q[:len(c)] = c
+        q = q.reshape(-1, 4)
+        out[k, 6:6 + len(q)] = q[:, 0] | q[:, 1] << 2 | q[:, 2] << 4 | q[:, 3] << 6
+    return out
 
 
 def fill_matrix(alphabet: int, match: int = 5, mismatch: int = -4) -> np.ndarray:
@@ -239,6 +272,24 @@ class ScoreBank:
         """Device pointers (ints, e.g. torch.Tensor.data_ptr()); async on `stream`."""
         self._check(lib().sw_score_batch_device(self._h, d_res, d_offs, d_lens, n, max_len,
                                                 d_scores, stream or None))
+
+    # CAPI record path (sequence_t arrays, 2-bit codes)
+    def load_query_record(self, record: np.ndarray):
+        r = np.ascontiguousarray(record, dtype=np.uint8).reshape(-1)
+        if r.size != RECORD_BYTES:
+            raise ValueError("a record is 64 bytes")
+        self._check(lib().sw_load_query_record(self._h, _p(r)))
+
+    def score_records(self, records: np.ndarray) -> np.ndarray:
+        r = np.ascontiguousarray(records, dtype=np.uint8).reshape(-1, RECORD_BYTES)
+        out = np.zeros(len(r), dtype=np.int32)
+        if len(r):
+            self._check(lib().sw_score_records(self._h, _p(r), len(r), _p(out)))
+        return out
+
+    def score_records_device(self, d_records: int, n: int, d_scores: int, stream: int = 0):
+        self._check(lib().sw_score_records_device(self._h, d_records, n, d_scores,
+                                                  stream or None))
 
     def best_hit(self, scores: np.ndarray, ids: Optional[np.ndarray] = None) -> Tuple[int, int]:
         """ScoreBank max / vld_max: (id of the best target, its score)."""

@@ -59,6 +59,23 @@ def test_pack_2bit_matches_capi_fixture():
     assert (S.unpack_2bit(S.pack_2bit(q), len(q)) == S.encode(q)).all()
 
 
+def test_records_match_capi_sequence_t():
+    """make_records builds main_test.c's sequence_t (aligner_Header.h:19-24): ID, length and
+    the charTo2bit bytes the reference host printed for query1."""
+    want = open(os.path.join(O.GOLDEN, "charto2bit_query1.hex")).read().split()
+    q = O.read_fasta(O.golden_fasta("query1.fa"))[0][1]
+    rec = S.make_records([S.encode(q)], ids=[7])
+    assert rec.shape == (1, S.RECORD_BYTES)
+    assert int.from_bytes(rec[0, 0:4].tobytes(), "little") == 7
+    assert int.from_bytes(rec[0, 4:6].tobytes(), "little") == len(q)
+    assert [f"{b:02x}" for b in rec[0, 6:6 + len(want)]] == want
+    assert not rec[0, 6 + len(want):].any()
+    with pytest.raises(ValueError):
+        S.make_records([np.zeros(233, np.uint8)])
+    with pytest.raises(ValueError):
+        S.make_records([np.array([4], np.uint8)])  # N has no 2-bit code
+
+
 REF_LIB = os.path.join(REPO, "oracle", "_ref", "libaligner_ref.so")
 
 

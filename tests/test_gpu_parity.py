@@ -329,3 +329,42 @@ def test_custom_dna_matrix_routes_to_profile_kernel():
         got = bank.score_targets(seqs)
     res, offs, lens = O.pack_residues(seqs)
     assert (got == O.score_batch(q, res, offs, lens, m, -12, -4)).all()
+
+
+def test_capi_records_path(bank, kernel_choice):
+    """Row f2: CAPI sequence_t records (2-bit codes read by the kernel) score exactly like the
+    byte path and the oracle; query from a record; lengths 0..232; device API."""
+    import torch
+
+    rng = np.random.default_rng(17)
+    bank.set_penalties(*REF)
+    q = rng.integers(0, 4, 100, dtype=np.uint8)
+    lens = [0, 1, 7, 8, 9, 100, 231, 232] + list(rng.integers(0, 233, 300))
+    seqs = [rng.integers(0, 4, int(n), dtype=np.uint8) for n in lens]
+    for k in range(10, 300, 9):  # homologous targets
+        seqs[k] = q[: min(len(q), 232)].copy()
+    recs = S.make_records(seqs)
+    bank.load_query_record(S.make_records([q])[0])
+    got = bank.score_records(recs)
+    res, offs, ln = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, ln, O.dna_matrix(5, -4), -12, -4)
+    assert (got == want).all(), np.nonzero(got != want)[0][:8]
+    assert (bank.score_targets(seqs) == want).all()
+    # device-resident records, unsorted
+    dev = torch.device("cuda", 0)
+    d_rec = torch.from_numpy(recs.reshape(-1)).to(dev)
+    d_sc = torch.zeros(len(seqs), dtype=torch.int32, device=dev)
+    bank.score_records_device(d_rec.data_ptr(), len(seqs), d_sc.data_ptr(),
+                              torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert (d_sc.cpu().numpy() == want).all()
+    # main_test_output.txt: query1 vs db18 -> result 102 (CAPI host fixture)
+    q1 = O.encode_dna(_lib_records("query1.fa")[0][1])
+    db = dict(_lib_records("data1.fa"))
+    bank.load_query_record(S.make_records([q1])[0])
+    assert bank.score_records(S.make_records([O.encode_dna(db["db18"])])).tolist() == [102]
+    # too long a record is refused
+    bad = S.make_records([np.zeros(10, np.uint8)])
+    bad[0, 4:6] = np.frombuffer(np.uint16(233).tobytes(), np.uint8)
+    with pytest.raises(S.SwbankError):
+        bank.score_records(bad)
