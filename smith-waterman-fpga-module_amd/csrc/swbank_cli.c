@@ -8,10 +8,16 @@
  *     271-285), one per library record, in library order (the RTL printed completion order).
  *
  * Usage: swbank -q query.fa -l library.fa [-p match,mismatch,open,extend] [-P] [-g]
- *               [-d device] [-o out.txt] [-T]
+ *               [-d device] [-o out.txt] [-T] [-R scores.txt]
  *   -p  penalties (default 5,-4,-12,-4: ScoreBank_v1_tb.sv:16-19, data/smith-waterman.py:6-10)
  *   -P  protein mode (BLOSUM62; -p gives only open,extend)      -g  Gotoh gap model
  *   -T  testbench transcript format "@     0ns: %10s score: \t%d"
+ *   -R  also write an ssearch36 "-R" score file (data/score500.txt layout: one line per
+ *       library record with name, length, score, record index and byte offset)
+ * FASTA: '>' starts a record (name = first token); sequence lines are concatenated; CR/LF,
+ * blank lines and lower case are accepted; bytes outside the alphabet encode to N (DNA) or X
+ * (protein), which score as mismatches (the testbench left them undefined, the CAPI host
+ * mapped them to T: unpinned by any fixture).
  * Exit status: 0 ok, 1 usage, 2 I/O, 3 library/device error.
  */
 #define _POSIX_C_SOURCE 200809L
@@ -26,19 +32,23 @@
 typedef struct {
   char **names;
   char **seqs;
+  long *offs; /* byte offset of each record's '>' line */
   size_t n, cap;
 } fasta_t;
 
-static int fasta_push(fasta_t *f, char *name) {
+static int fasta_push(fasta_t *f, char *name, long off) {
   if (f->n == f->cap) {
     size_t nc = f->cap ? 2 * f->cap : 64;
     char **nn = realloc(f->names, nc * sizeof(char *));
+    if (nn) f->names = nn;
     char **ns = realloc(f->seqs, nc * sizeof(char *));
-    if (!nn || !ns) return -1;
-    f->names = nn;
-    f->seqs = ns;
+    if (ns) f->seqs = ns;
+    long *no = realloc(f->offs, nc * sizeof(long));
+    if (no) f->offs = no;
+    if (!nn || !ns || !no) return -1;
     f->cap = nc;
   }
+  f->offs[f->n] = off;
   f->names[f->n] = name;
   f->seqs[f->n] = calloc(1, 1);
   if (!f->seqs[f->n]) return -1;
@@ -54,7 +64,9 @@ static int read_fasta(const char *path, fasta_t *f) {
   char *line = NULL;
   size_t cap = 0;
   ssize_t len;
-  while ((len = getline(&line, &cap, fp)) >= 0) {
+  long pos = 0, here;
+  while ((here = pos, len = getline(&line, &cap, fp)) >= 0) {
+    pos += (long)len;
     while (len > 0 && (line[len - 1] == '\n' || line[len - 1] == '\r' || line[len - 1] == ' '))
       line[--len] = 0;
     if (len == 0) continue;
@@ -62,11 +74,11 @@ static int read_fasta(const char *path, fasta_t *f) {
       char *p = line + 1;
       size_t k = strcspn(p, " \t");
       char *name = strndup(p, k);
-      if (!name || fasta_push(f, name)) goto fail;
+      if (!name || fasta_push(f, name, here)) goto fail;
     } else {
       if (f->n == 0) { /* bare sequence file (the CAPI host's build/query) */
         char *name = strdup("seq");
-        if (!name || fasta_push(f, name)) goto fail;
+        if (!name || fasta_push(f, name, here)) goto fail;
       }
       char **s = &f->seqs[f->n - 1];
       size_t old = strlen(*s);
@@ -88,14 +100,14 @@ fail:
 static void usage(const char *argv0) {
   fprintf(stderr,
           "usage: %s -q query.fa -l library.fa [-p match,mismatch,open,extend] [-P] [-g]\n"
-          "          [-d device] [-o out.txt] [-T]\n",
+          "          [-d device] [-o out.txt] [-T] [-R scores.txt]\n",
           argv0);
 }
 
 int main(int argc, char **argv) {
-  const char *qpath = NULL, *lpath = NULL, *opath = NULL, *pen = NULL;
+  const char *qpath = NULL, *lpath = NULL, *opath = NULL, *pen = NULL, *rpath = NULL;
   int protein = 0, gotoh = 0, device = -1, transcript = 0, opt;
-  while ((opt = getopt(argc, argv, "q:l:p:Pgd:o:Th")) != -1) {
+  while ((opt = getopt(argc, argv, "q:l:p:Pgd:o:TR:h")) != -1) {
     switch (opt) {
       case 'q': qpath = optarg; break;
       case 'l': lpath = optarg; break;
@@ -105,6 +117,7 @@ int main(int argc, char **argv) {
       case 'd': device = atoi(optarg); break;
       case 'o': opath = optarg; break;
       case 'T': transcript = 1; break;
+      case 'R': rpath = optarg; break;
       default: usage(argv[0]); return opt == 'h' ? 0 : 1;
     }
   }
@@ -192,6 +205,28 @@ int main(int argc, char **argv) {
       fprintf(out, "%s score: %d\n", nm, scores[k]);
   }
   if (opath) fclose(out);
+  if (rpath) { /* ssearch36 -R layout (data/score500.txt:1-3,502-503) */
+    FILE *rf = fopen(rpath, "w");
+    if (!rf) {
+      sw_bank_destroy(bank);
+      return 2;
+    }
+    fprintf(rf, "# swbank -R %s -q %s -l %s\n", rpath, qpath, lpath);
+    fprintf(rf, ">>>0 %zu\t%s - %zu %s\n", qlen, q.names[0], qlen, protein ? "aa" : "nt");
+    for (size_t k = 0; k < lib.n; ++k)
+      fprintf(rf,
+              "%-15s %3zu 0 -1.00000 -1.00000 %4d    0    0  1  0    0    0    0  1  0 %5zu "
+              "%8ld\n",
+              lib.names[k], strlen(lib.seqs[k]), scores[k], k, lib.offs[k]);
+    fprintf(rf, "#Algorithm : Smith-Waterman (libswbank, %s gaps, MI355X)\n",
+            gotoh ? "Gotoh" : "merged");
+    if (protein)
+      fprintf(rf, "#Parameters : BLOSUM62 matrix, open/ext: %d/%d\n", go, ge);
+    else
+      fprintf(rf, "#Parameters : +%d/%d matrix (%d:%d), open/ext: %d/%d\n", ma, mm, ma, mm, go, ge);
+    fprintf(rf, "#Query: %3d>>>%s - %zu %s\n", 0, q.names[0], qlen, protein ? "aa" : "nt");
+    fclose(rf);
+  }
   sw_bank_destroy(bank);
   free(qc);
   free(res);

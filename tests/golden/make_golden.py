@@ -18,6 +18,9 @@ What it writes (all DATA — inputs and expected outputs the reference already h
                             query1 vs the first library record the CAPI host read (``data1.fa`` db18, 128 bp).
 * ``swalign_control.tsv``  ``data/sw_testing.txt`` scores (swalign, gap = go+(k-1)*ge): a NEGATIVE control
                             (``data/sw-testing.py:31-36``); 4 of its 16 scores must differ from ours.
+* ``score500_R_lines.txt``  the 499 per-target lines of ``data/score500.txt`` verbatim (ssearch36 ``-R``
+                            layout: name, length, score, record index, byte offset), to check the CLI's
+                            ``-R`` writer byte for byte.
 * ``charto2bit_query1.hex`` the 2-bit packing the CAPI host printed for query1
                             (``build/main_test_output.txt`` "data[k]: 0x.." lines).
 
@@ -62,6 +65,11 @@ def main():
             tok = line.split()
             if len(tok) >= 6 and tok[0].startswith("db") and tok[1].isdigit():
                 rows.append(("ssearch36", lib, q, tok[0], int(tok[5])))
+
+    with open(os.path.join(HERE, "score500_R_lines.txt"), "w") as out:
+        for line in open(os.path.join(DATA, "score500.txt")):
+            if line.startswith("db"):
+                out.write(line.rstrip("\n") + "\n")
 
     capi_out = os.path.join(REF, "capi_sample_aligner", "software-C,C++", "build", "main_test_output.txt")
     txt = open(capi_out, errors="replace").read()

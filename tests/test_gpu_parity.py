@@ -239,6 +239,38 @@ def test_cli_reproduces_transcript():
     assert all(got[t] == s for t, s in want.items()) and len(want) == 99
 
 
+def test_cli_ssearch_R_writer_matches_score500(tmp_path):
+    """Row f3: `swbank -R` writes data/score500.txt's per-target lines byte for byte (name,
+    length, score, record index, byte offset in the library file)."""
+    rfile = tmp_path / "score500.txt"
+    subprocess.run([S.CLI_PATH, "-q", O.golden_fasta("query100.fa"), "-l",
+                    O.golden_fasta("data500.fa"), "-R", str(rfile), "-o", os.devnull], check=True)
+    got = [ln for ln in rfile.read_text().splitlines() if ln.startswith("db")]
+    want = open(os.path.join(O.GOLDEN, "score500_R_lines.txt")).read().splitlines()
+    assert len(got) == len(want) == 499
+    bad = [(g, w) for g, w in zip(got, want) if g != w]
+    assert not bad, bad[:3]
+
+
+def test_cli_fasta_robustness(tmp_path):
+    """Row f4: CRLF line ends, wrapped sequence lines, lower case, blank lines and header
+    descriptions parse to the same records as the reference's one-line FASTA."""
+    recs = _lib_records("data10.fa")
+    messy = tmp_path / "data10_messy.fa"
+    with open(messy, "w", newline="") as f:
+        for k, (name, seq) in enumerate(recs):
+            f.write(f">{name} some description\r\n\r\n")
+            body = seq.lower() if k % 2 else seq
+            for i in range(0, len(body), 60):
+                f.write(body[i:i + 60] + "\r\n")
+    def run(lib):
+        out = subprocess.run([S.CLI_PATH, "-q", O.golden_fasta("query100.fa"), "-l", str(lib)],
+                             capture_output=True, text=True, check=True).stdout
+        return out.splitlines()
+    assert run(messy) == run(O.golden_fasta("data10.fa"))
+    assert len(run(messy)) == len(recs)
+
+
 # ---- Gotoh / protein / profile-mode kernels ---------------------------------------------
 def _load_generated():
     import json
