@@ -164,17 +164,18 @@ class Workload:
             self.bank.load_query(self.queries[0])
         self.cells = sum(len(q) for q in self.queries) * n * L
 
-    def run(self, stream):
+    def run(self, stream, d_sc=None):
+        d_sc = self.d_sc if d_sc is None else d_sc
         for k, q in enumerate(self.queries):
             if len(self.queries) > 1:
                 self.bank.load_query(q)  # ld_sequence: a new query for the same batch
             if self.d_rec is not None:
                 self.bank.score_records_device(self.d_rec.data_ptr(), self.n,
-                                               self.d_sc[k].data_ptr(), stream)
+                                               d_sc[k].data_ptr(), stream)
                 continue
             self.bank.score_batch_device(self.d_res.data_ptr(), self.d_offs.data_ptr(),
                                          self.d_lens.data_ptr(), self.n, self.L,
-                                         self.d_sc[k].data_ptr(), stream)
+                                         d_sc[k].data_ptr(), stream)
 
 
 def main():
@@ -185,9 +186,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (not used by the driver): SWBENCH_BACKEND=gloo with SWBENCH_SHARE_GPU=1
+    # runs several ranks on one GPU to exercise the multi-rank flow
+    backend = os.environ.get("SWBENCH_BACKEND", "nccl")
+    if os.environ.get("SWBENCH_SHARE_GPU") == "1":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -195,17 +204,38 @@ def main():
     import swbank as S
 
     wl = Workload(args, rank, dev, S, torch)
-    gather = ([torch.empty_like(wl.d_sc) for _ in range(world)]
+    gdev = dev if backend == "nccl" else torch.device("cpu")
+    gather = ([torch.empty_like(wl.d_sc, device=gdev) for _ in range(world)]
               if (world > 1 and rank == 0) else None)
     stream = torch.cuda.current_stream()
+    # Two score buffers: step i scores into bufs[i % 2] while the RCCL gather of step i-1
+    # (async, on RCCL's stream) still reads the other one; a buffer is rewritten only after
+    # the gather that read it has completed (work.wait() orders the compute stream after it).
+    bufs = [wl.d_sc, torch.empty_like(wl.d_sc)]
+    pending = [None, None]
+    nstep = [0]
 
     def step():
-        wl.run(stream.cuda_stream)
-        if world > 1:
-            dist.gather(wl.d_sc, gather_list=gather, dst=0)
+        b = nstep[0] % 2
+        if pending[b] is not None:
+            pending[b].wait()
+            pending[b] = None
+        wl.run(stream.cuda_stream, bufs[b])
+        if world > 1 and backend == "nccl":
+            pending[b] = dist.gather(bufs[b], gather_list=gather, dst=0, async_op=True)
+        elif world > 1:
+            dist.gather(bufs[b].cpu(), gather_list=gather, dst=0)
+        nstep[0] += 1
+
+    def drain():
+        for b in (0, 1):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -214,6 +244,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -222,7 +253,7 @@ def main():
     launches, pack_ms, score_ms = wl.bank.timing()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -302,7 +333,7 @@ def main():
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0 and args.workload == "q100xdata500":
         out["cpu_baseline"], out["parity_sample"] = cpu_baseline(
-            wl.queries[0], wl.batch, wl.d_sc[0], wl.L, args.cpu_seconds)
+            wl.queries[0], wl.batch, bufs[(nstep[0] - 1) % 2][0], wl.L, args.cpu_seconds)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
