@@ -85,10 +85,11 @@ struct sw_bank {
   // f16 tile kernel (DNA LUT, merged gaps): LUT bytes are f16 high bytes; used for a batch
   // whose score bound fits f16's exact integers (|x| <= 2048)
   bool f16 = false;
-  uint32_t nv16 = 0;
+  uint32_t nv16 = 0, PS16 = 0;  // PS16: f16 profile row stride (bytes)
   int32_t f16_neg = 0;     // most negative intermediate: -(o + 2e + |min s|)
   DevBuf<uint32_t> qtab16;
-  struct Seg { int W; size_t off; };  // rows = W*R (last may be shorter), qtab word offset
+  struct Seg { int W; size_t off, off16; };  // rows = W*R (last may be shorter); word offsets
+                                              // in qtab and qtab16
   std::vector<Seg> segs;
   DevBuf<uint2> edge[2];  // bottom rows handed from segment to segment
   // wave kernel (few targets, query <= 1024 rows): lane l owns rows [lK, lK+K)
@@ -314,7 +315,7 @@ static sw_status prepare(sw_bank* b) {
   for (int r0 = 0; r0 < std::max(qlen, 1); r0 += seg_rows) {
     const int rows = std::min(seg_rows, std::max(qlen, 1) - r0);
     const int W = std::max(1, (rows + R - 1) / R);
-    segs.push_back({W, tab.size()});
+    segs.push_back({W, tab.size(), 0});
     if (!prof) {
       const size_t base = tab.size();
       tab.resize(base + (size_t)W * R, 0xFFFFFFFFu);
@@ -342,18 +343,24 @@ static sw_status prepare(sw_bank* b) {
     *out = (uint8_t)(bits >> 8);
     return (bits & 0xFFu) == 0 && (int)(float)h == v;
   };
-  bool f16 = !prof && !gotoh && swk_has_variant(R, RB, col0, 0, 0, 1) != 0;
+  // LUT mode: one byte per entry (the f16 high byte); profile mode: two bytes (any |s| <= 127
+  // is an exact f16), row stride PS16 = 2 x rows, 16 mod 256 like PS
+  bool f16 = swk_has_variant(R, RB, col0, prof, gotoh ? 1 : 0, 1) != 0;
   std::vector<uint32_t> tab16;
   uint8_t hN = 0;
-  f16 = f16 && f16_hi(sN, &hN);
-  for (int i = 0; f16 && i < A * A; ++i) {
-    uint8_t h;
-    f16 = f16_hi(m[i], &h);
+  uint32_t PS16 = 0;
+  if (!prof) {
+    f16 = f16 && f16_hi(sN, &hN);
+    for (int i = 0; f16 && i < A * A; ++i) {
+      uint8_t h;
+      f16 = f16_hi(m[i], &h);
+    }
   }
-  if (f16) {
+  if (f16 && !prof) {
     tab16.assign(tab.size(), 0xE8E8E8E8u);  // padding rows: -2048
-    for (const sw_bank::Seg& sg : segs) {
+    for (sw_bank::Seg& sg : segs) {
       const int r0 = (int)(&sg - segs.data()) * seg_rows;
+      sg.off16 = sg.off;
       for (int i = 0; i < sg.W * R && r0 + i < qlen && i < seg_rows; ++i) {
         uint32_t w = 0;
         for (int c = 0; c < 4; ++c) {
@@ -363,6 +370,21 @@ static sw_status prepare(sw_bank* b) {
         }
         tab16[sg.off + i] = w;
       }
+    }
+  } else if (f16) {
+    PS16 = (uint32_t)((2 * Wseg * R + 15) / 16 * 16);
+    PS16 += (16u + 256u - PS16 % 256u) % 256u;
+    const uint16_t padv = 0xE800u;  // -2048: padding letter and rows past the query
+    for (sw_bank::Seg& sg : segs) {
+      const int r0 = (int)(&sg - segs.data()) * seg_rows;
+      std::vector<uint16_t> qp((size_t)(A + 1) * PS16 / 2, padv);
+      for (int c = 0; c < A; ++c)
+        for (int i = 0; i < sg.W * R && r0 + i < qlen && i < seg_rows; ++i)
+          qp[(size_t)c * PS16 / 2 + i] =
+              __builtin_bit_cast(uint16_t, (_Float16)(float)m[b->query[r0 + i] * A + c]);
+      sg.off16 = tab16.size();
+      tab16.resize(sg.off16 + qp.size() / 2);
+      std::memcpy(tab16.data() + sg.off16, qp.data(), qp.size() * 2);
     }
   }
   // wave-kernel layout of the same query (rows padded to 64K)
@@ -406,6 +428,7 @@ static sw_status prepare(sw_bank* b) {
   HIPOK(b, hipStreamSynchronize(b->stream));
   b->f16 = f16;
   b->nv16 = (uint32_t)hN * 0x01010101u;
+  b->PS16 = PS16;
   b->f16_neg = -(o + 2 * e + (S - smin));
   b->R = R;
   b->RB = RB;
@@ -503,8 +526,10 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
     HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof,
                               b->cfg.gap_model == SW_GAP_GOTOH ? 1 : 0, use_f16 ? 1 : 0, d_res,
                               d_offs, d_lens, n,
-                              (use_f16 ? b->qtab16.p : b->qtab.p) + b->segs[s].off,
-                              use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E, b->PS,
+                              use_f16 ? b->qtab16.p + b->segs[s].off16
+                                      : b->qtab.p + b->segs[s].off,
+                              use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
+                              use_f16 && b->prof ? b->PS16 : b->PS,
                               b->pad, b->segs[s].W, d_scores, ein, eout, ecols, s > 0 ? 1 : 0,
                               packed ? 1 : 0, st));
   }

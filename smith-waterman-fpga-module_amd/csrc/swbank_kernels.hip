@@ -68,6 +68,18 @@ struct ProfLookup {
   }
 };
 
+// f16 profile mode: 2-byte entries (the f16 bits of s); word k of lo/hi holds rows 2k, 2k+1 of
+// the lane's low/high target letter; one v_perm_b32 per row picks the row's two halves.
+template <int R>
+struct ProfLookup16 {
+  uint32_t lo[R / 2], hi[R / 2];
+  __device__ __forceinline__ u16x2 operator()(int r) const {
+    const uint32_t k = (uint32_t)(r & 1) * 2;
+    const uint32_t sel = k | ((k + 1) << 8) | ((k + 4) << 16) | ((k + 5) << 24);
+    return as_u16x2(__builtin_amdgcn_perm(hi[r >> 1], lo[r >> 1], sel));
+  }
+};
+
 // ---- one column of R rows, merged gap matrix (the ScoreBank PE) --------------------------
 // ZDOWN: HDL column-0 rule (G passed down = 0).  RB: rows per scheduling group (a
 // sched_barrier every RB rows bounds how far the scheduler may defer the H/best updates
@@ -128,6 +140,33 @@ __device__ __forceinline__ void column_merged_f16(const LK& lk, u16x2& diag_, u1
   }
   diag_ = as_u16x2(diag);
   upT_ = as_u16x2(upT);
+  best_ = as_u16x2(best);
+}
+
+// Gotoh in f16.  E and F are kept one step ahead ("what the next cell reads") and floored at
+// 0 (a non-positive gap value never reaches a positive H), so H needs one max3 and the
+// H - o - e term is shared by both gap directions: 8.5 VALU per lane per 2 cells (u16: 11).
+//   H = max(D, El, F)   HN = H - o - e   El = max(0, HN, El - e)   F = max(0, HN, F - e)
+template <int R, int RB, class LK>
+__device__ __forceinline__ void column_gotoh_f16(const LK& lk, u16x2& diag_, u16x2& upF_,
+                                                 u16x2 (&Hl)[R], u16x2 (&El)[R], u16x2& best_,
+                                                 f16x2 NOE2, f16x2 NE2) {
+  f16x2 diag = as_f16x2(diag_), F = as_f16x2(upF_), best = as_f16x2(best_);
+  const f16x2 Z = {(_Float16)0, (_Float16)0};
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const f16x2 D = diag + as_f16x2(lk(r));
+    const f16x2 E = as_f16x2(El[r]);
+    const f16x2 H = fmax2(fmax2(D, E), F);
+    const f16x2 HN = H + NOE2;
+    best = fmax2(best, H);
+    diag = as_f16x2(Hl[r]);
+    Hl[r] = as_u16x2(H);
+    El[r] = as_u16x2(fmax2(fmax2(HN, Z), E + NE2));
+    F = fmax2(fmax2(HN, Z), F + NE2);
+    if ((r % RB) == RB - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+  upF_ = as_u16x2(F);
   best_ = as_u16x2(best);
 }
 
@@ -399,7 +438,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const _Float16 fnoe = (_Float16)(-(float)(a.O + a.E)), fne = (_Float16)(-(float)a.E);
   const f16x2 NOE2 = {fnoe, fnoe}, NE2 = {fne, fne};
   if (wave == 0) {
-    bnd[lane] = F16 ? make_uint2(0u, as_u32(as_u16x2(NOE2))) : make_uint2(S | (S << 16), 0u);
+    bnd[lane] = F16 ? make_uint2(0u, GOTOH ? 0u : as_u32(as_u16x2(NOE2)))
+                    : make_uint2(S | (S << 16), 0u);
     if (seg_in)  // the previous segment's bottom row of chunk 0
       dma_edge_chunk(a.edge_in + (size_t)tile * a.ecols * 64, ein, lane);
   }
@@ -424,7 +464,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const uint32_t oes = a.O + a.E + S;
   const u16x2 OES2 = {(unsigned short)oes, (unsigned short)oes};
   const u16x2 H0 = F16 ? (u16x2){0, 0} : S2;          // H of row/column -1
-  const u16x2 X0 = F16 ? as_u16x2(NOE2) : (u16x2){0, 0};  // G/E/T of column -1
+  const u16x2 X0 = (F16 && !GOTOH) ? as_u16x2(NOE2) : (u16x2){0, 0};  // G/E/T of column -1
 
   // H~ and G (merged) / E (Gotoh) / T (f16) of the column to the left
   u16x2 Hl[R], Xl[R];
@@ -481,7 +521,28 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         u16x2 diag = prevUpH;
         prevUpH = upH;
         const uint32_t wlo = jj < 4 ? clo.x : clo.y, whi = jj < 4 ? chi.x : chi.y;
-        if constexpr (PROF) {
+        if constexpr (PROF && F16) {
+          ProfLookup16<R> lk;
+          const uint32_t blo = min((wlo >> (8 * (jj & 3))) & 0xFFu, padc);
+          const uint32_t bhi = min((whi >> (8 * (jj & 3))) & 0xFFu, padc);
+          const uint4* plo = reinterpret_cast<const uint4*>(prof + blo * a.PS + 2 * pbase);
+          const uint4* phi = reinterpret_cast<const uint4*>(prof + bhi * a.PS + 2 * pbase);
+#pragma unroll
+          for (int q = 0; q < R / 8; ++q) {
+            const uint4 x = plo[q], y = phi[q];
+            lk.lo[4 * q] = x.x; lk.lo[4 * q + 1] = x.y; lk.lo[4 * q + 2] = x.z;
+            lk.lo[4 * q + 3] = x.w;
+            lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z;
+            lk.hi[4 * q + 3] = y.w;
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (GOTOH)
+            column_gotoh_f16<R, RB>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+          else if (COL0 && jj == 0 && c == 0)
+            column_merged_f16<R, RB, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+          else
+            column_merged_f16<R, RB, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+        } else if constexpr (PROF) {
           ProfLookup<R> lk;
           const uint32_t blo = min((wlo >> (8 * (jj & 3))) & 0xFFu, padc);
           const uint32_t bhi = min((whi >> (8 * (jj & 3))) & 0xFFu, padc);
@@ -509,6 +570,11 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           const uint32_t sel16 = 0x0Cu | ((uint32_t)(jj & 3) << 8) | (0x0Cu << 16) |
                                  ((uint32_t)(4 + (jj & 3)) << 24);
           const uint32_t selw = __builtin_amdgcn_perm(whi, wlo, sel16) | 0x000C000Cu;
+          if constexpr (GOTOH) {
+            const LutLookup<R> lk{tab, nv, selw};
+            __builtin_amdgcn_sched_barrier(0);
+            column_gotoh_f16<R, RB>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+          } else {
 #if SWK_F16_ASM
           const uint32_t noe = as_u32(as_u16x2(NOE2)), ne = as_u32(as_u16x2(NE2));
           if (COL0 && jj == 0 && c == 0)
@@ -523,6 +589,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           else
             column_merged_f16<R, RB, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
 #endif
+          }
         } else {
           // selector: byte 0 = code of the low target, byte 2 = code of the high target
           const uint32_t sel =
@@ -836,7 +903,9 @@ static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream
   X(16, 4, 0, 1, 0, 0) X(16, 4, 1, 1, 0, 0) X(32, 4, 0, 1, 0, 0) X(32, 4, 1, 1, 0, 0)         \
   X(64, 4, 0, 1, 0, 0) X(64, 4, 1, 1, 0, 0)                                                   \
   X(16, 4, 0, 1, 1, 0) X(32, 4, 0, 1, 1, 0) X(64, 4, 0, 1, 1, 0)                              \
-  X(16, 4, 0, 0, 0, 1) X(16, 4, 1, 0, 0, 1) X(32, 4, 0, 0, 0, 1) X(64, 4, 0, 0, 0, 1)
+  X(16, 4, 0, 0, 0, 1) X(16, 4, 1, 0, 0, 1) X(32, 4, 0, 0, 0, 1) X(64, 4, 0, 0, 0, 1)         \
+  X(16, 4, 0, 0, 1, 1)                                                                        \
+  X(16, 4, 0, 1, 0, 1) X(16, 4, 1, 1, 0, 1) X(16, 4, 0, 1, 1, 1)
 
 extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh, int f16) {
 #define SWK_HAS(RR, BB, C0, PF, GT, FH) \

@@ -309,6 +309,43 @@ def test_gotoh_dna_random_vs_oracle(params, qlen):
     assert (got == want).all()
 
 
+@pytest.mark.parametrize("case", ["dna-gotoh", "prot-merged", "prot-gotoh"])
+def test_f16_gotoh_and_profile_paths(case, kernel_choice):
+    """The f16 Gotoh column and the 2-byte f16 query profile are taken when the score bound
+    allows (and not under SWBANK_F16=0), and agree with the oracle around the bound."""
+    rng = np.random.default_rng(len(case))
+    dna = case.startswith("dna")
+    model = S.GAP_GOTOH if case.endswith("gotoh") else S.GAP_MERGED
+    A = 4 if dna else 20
+    for qlen in (40, 150):
+        q = rng.integers(0, A, qlen, dtype=np.uint8)
+        seqs = [rng.integers(0, A, int(rng.integers(0, 220)), dtype=np.uint8) for _ in range(300)]
+        for k in range(0, 300, 5):
+            seqs[k] = q.copy()
+            seqs[k][::9] = rng.integers(0, A, len(seqs[k][::9]))
+        seqs[1] = q.copy()  # the bound itself: a perfect match
+        with S.ScoreBank(alphabet=S.ALPHABET_DNA if dna else S.ALPHABET_PROTEIN,
+                         gap_model=model) as bank:
+            if dna:
+                bank.set_penalties(5, -4, -10, -1)
+                sub, go, ge = O.dna_matrix(5, -4), -10, -1
+            else:
+                bank.set_matrix(O.BLOSUM62, -11, -1)
+                sub, go, ge = O.BLOSUM62, -11, -1
+            bank.load_query(q)
+            got = bank.score_targets(seqs)
+            kern = bank.last_kernel()
+        res, offs, lens = O.pack_residues(seqs)
+        want = O.score_batch(q, res, offs, lens, sub, go, ge, model)
+        assert (got == want).all(), (kern, np.nonzero(got != want)[0][:5])
+        smax = 5 if dna else 11
+        if kernel_choice == "tile":
+            f16 = min(qlen, max(lens)) * smax + smax <= 2048
+            assert kern.startswith("tile f16" if f16 else "tile u16"), kern
+        elif kernel_choice == "tile-u16":
+            assert kern.startswith("tile u16"), kern
+
+
 @pytest.mark.parametrize("model", [S.GAP_MERGED, S.GAP_GOTOH])
 @pytest.mark.parametrize("gaps", [(-11, -1), (-10, -2), (-2, -1)])
 @pytest.mark.parametrize("qlen", [5, 33, 200, 512])
