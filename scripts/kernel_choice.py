@@ -20,6 +20,8 @@ CASES = [  # (alphabet, model, qlen, L, ntargets)
     ("dna", "merged", 1000, 150, 65536), ("dna", "gotoh", 512, 512, 65536),
     ("protein", "gotoh", 128, 300, 131072), ("protein", "gotoh", 256, 300, 65536),
     ("protein", "merged", 512, 1000, 25000), ("protein", "gotoh", 1024, 1000, 12500),
+    ("protein", "gotoh", 128, 150, 524288), ("protein", "merged", 128, 150, 524288),
+    ("dna", "gotoh", 256, 150, 524288),
 ]
 
 
@@ -52,8 +54,9 @@ def main():
         bank.load_query(q)
         out = {"alphabet": alpha, "model": model, "qlen": qlen, "L": L, "n": n}
         ref = None
-        for kern in ("tile", "wave", "auto"):
-            os.environ["SWBANK_KERNEL"] = kern
+        for kern in ("tile", "tile-u16", "wave", "auto"):
+            os.environ["SWBANK_KERNEL"] = kern.split("-")[0]
+            os.environ["SWBANK_F16"] = "0" if kern == "tile-u16" else "1"
             bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,
                                     d_sc.data_ptr(), stream)
             torch.cuda.synchronize()
@@ -71,6 +74,7 @@ def main():
             out[kern] = round(qlen * L * n * launches / (ms / 1e3) / 1e9, 1)
             out[kern + "_kernel"] = bank.last_kernel()
         os.environ.pop("SWBANK_KERNEL")
+        os.environ.pop("SWBANK_F16")
         bank.close()
         print(json.dumps(out), flush=True)
 

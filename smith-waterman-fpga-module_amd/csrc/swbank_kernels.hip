@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "swbank_internal.h"
 
@@ -170,59 +171,120 @@ __device__ __forceinline__ void column_gotoh_f16(const LK& lk, u16x2& diag_, u16
   best_ = as_u16x2(best);
 }
 
-// Same column, hand-ordered: each row is one asm block whose dependent packed ops are never
-// adjacent (gfx950 needs a wait state between a VOP3P write and a dependent VOP3P read, and
-// LLVM's order of this chain left ~2.5 s_nop per row).  Per row r, with D_r = diag + s_r
-// already computed by row r-1's block:
-//   I = max(Tup, Tl) ; DN = D + NOE ; IN = I + NE ; H = max(D, 0, I) ; T = max(DN, NOE, IN)
-//   [best = max(best, H_prev, H) every second row] ; s' = perm(LUT_{r+1}) ; D' = Hl[r] + s'
+// The f16 columns are normally run as hand-ordered asm (column_f16_asm below): LLVM's order
+// of these chains leaves ~2.5 s_nop per row (gfx950 needs a wait state between a VOP3P write
+// and a dependent VOP3P read); the generated order needs none.  SWK_F16_ASM=0 builds the
+// compiler-scheduled C++ forms above instead (A/B and debugging).
 #ifndef SWK_F16_ASM
 #define SWK_F16_ASM 1
 #endif
 #include "swbank_f16_rows.inc"
-#define SWK_F16_OPS(B)                                                                        \
+#define SWK_F16_HT(B)                                                                         \
   [h0] "+v"(Hl[B]), [h1] "+v"(Hl[B + 1]), [h2] "+v"(Hl[B + 2]), [h3] "+v"(Hl[B + 3]),          \
       [h4] "+v"(Hl[B + 4]), [h5] "+v"(Hl[B + 5]), [h6] "+v"(Hl[B + 6]), [h7] "+v"(Hl[B + 7]),  \
-      [t0] "+v"(Tl[B]), [t1] "+v"(Tl[B + 1]), [t2] "+v"(Tl[B + 2]), [t3] "+v"(Tl[B + 3]),      \
-      [t4] "+v"(Tl[B + 4]), [t5] "+v"(Tl[B + 5]), [t6] "+v"(Tl[B + 6]), [t7] "+v"(Tl[B + 7]),  \
-      [Da] "+v"(Da), [Db] "=&v"(Db), [S1] "=&v"(S1), [X] "=&v"(X), [DN] "=&v"(DN),             \
-      [IN] "=&v"(IN), [best] "+v"(best)
-#define SWK_F16_INS(B)                                                                        \
-  [up] "v"(up), [nv] "v"(nv), [sel] "v"(selw), [noe] "s"(noe), [ne] "s"(ne),                 \
-      [tb0] "s"(tab[B + 1]), [tb1] "s"(tab[B + 2]), [tb2] "s"(tab[B + 3]),                    \
-      [tb3] "s"(tab[B + 4]), [tb4] "s"(tab[B + 5]), [tb5] "s"(tab[B + 6]),                    \
-      [tb6] "s"(tab[B + 7]), [tb7] "s"(tab[(B + 8) < R ? B + 8 : R - 1])
-template <int R, bool ZDOWN>
-__device__ __forceinline__ void column_merged_f16_asm(const uint32_t (&tab)[R], uint32_t nv,
-                                                      uint32_t selw, u16x2& diag_, u16x2& upT_,
-                                                      u16x2 (&Hl)[R], u16x2 (&Tl)[R],
-                                                      u16x2& best_, uint32_t noe, uint32_t ne) {
+      [t0] "+v"(Xl[B]), [t1] "+v"(Xl[B + 1]), [t2] "+v"(Xl[B + 2]), [t3] "+v"(Xl[B + 3]),      \
+      [t4] "+v"(Xl[B + 4]), [t5] "+v"(Xl[B + 5]), [t6] "+v"(Xl[B + 6]), [t7] "+v"(Xl[B + 7]),  \
+      [Da] "+v"(Da), [Db] "=&v"(Db), [S1] "=&v"(S1), [best] "+v"(best)
+#define SWK_F16_OUT_M(B) SWK_F16_HT(B), [X] "=&v"(X), [DN] "=&v"(DN), [IN] "=&v"(IN)
+#define SWK_F16_OUT_G(B) SWK_F16_HT(B), [EN] "=&v"(X), [HN] "=&v"(DN), [FN] "=&v"(IN), [F] "+v"(up)
+#define SWK_F16_IN_L(B)                                                                       \
+  [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up),            \
+      [tb0] "s"(lk.tab[B + 1]), [tb1] "s"(lk.tab[B + 2]), [tb2] "s"(lk.tab[B + 3]),           \
+      [tb3] "s"(lk.tab[B + 4]), [tb4] "s"(lk.tab[B + 5]), [tb5] "s"(lk.tab[B + 6]),           \
+      [tb6] "s"(lk.tab[B + 7]), [tb7] "s"(lk.tab[(B + 8) < R ? B + 8 : R - 1])
+#define SWK_F16_IN_P(B)                                                                       \
+  [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), \
+      [lo0] "v"(lk.lo[B / 2]), [lo1] "v"(lk.lo[B / 2 + 1]), [lo2] "v"(lk.lo[B / 2 + 2]),       \
+      [lo3] "v"(lk.lo[B / 2 + 3]), [lo4] "v"(lk.lo[(B + 8) < R ? B / 2 + 4 : B / 2 + 3]),      \
+      [hi0] "v"(lk.hi[B / 2]), [hi1] "v"(lk.hi[B / 2 + 1]), [hi2] "v"(lk.hi[B / 2 + 2]),       \
+      [hi3] "v"(lk.hi[B / 2 + 3]), [hi4] "v"(lk.hi[(B + 8) < R ? B / 2 + 4 : B / 2 + 3])
+// The gotoh macros have no [up]/[X]/... in their text; unused operands are harmless.
+#define SWK_F16_IN_LG(B)                                                                      \
+  [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne),                          \
+      [tb0] "s"(lk.tab[B + 1]), [tb1] "s"(lk.tab[B + 2]), [tb2] "s"(lk.tab[B + 3]),           \
+      [tb3] "s"(lk.tab[B + 4]), [tb4] "s"(lk.tab[B + 5]), [tb5] "s"(lk.tab[B + 6]),           \
+      [tb6] "s"(lk.tab[B + 7]), [tb7] "s"(lk.tab[(B + 8) < R ? B + 8 : R - 1])
+#define SWK_F16_IN_PG(B)                                                                      \
+  [noe] "s"(noe), [ne] "s"(ne), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u),            \
+      [lo0] "v"(lk.lo[B / 2]), [lo1] "v"(lk.lo[B / 2 + 1]), [lo2] "v"(lk.lo[B / 2 + 2]),       \
+      [lo3] "v"(lk.lo[B / 2 + 3]), [lo4] "v"(lk.lo[(B + 8) < R ? B / 2 + 4 : B / 2 + 3]),      \
+      [hi0] "v"(lk.hi[B / 2]), [hi1] "v"(lk.hi[B / 2 + 1]), [hi2] "v"(lk.hi[B / 2 + 2]),       \
+      [hi3] "v"(lk.hi[B / 2 + 3]), [hi4] "v"(lk.hi[(B + 8) < R ? B / 2 + 4 : B / 2 + 3])
+
+// One f16 column, hand-ordered asm in 8-row blocks (scripts/gen_f16_rows.py).  LK is
+// LutLookup<R> (DNA, row LUT words in SGPRs) or ProfLookup16<R> (2-byte profile words).
+// Merged: Xl = T (= G - e), upX = T passed down.  Gotoh: Xl = E, upX = F of the next row.
+template <int R, bool GOTOH, bool ZDOWN, class LK>
+__device__ __forceinline__ void column_f16_asm(const LK& lk, u16x2& diag_, u16x2& upX_,
+                                               u16x2 (&Hl)[R], u16x2 (&Xl)[R], u16x2& best_,
+                                               uint32_t noe, uint32_t ne) {
   static_assert(R % 8 == 0, "rows come in blocks of 8");
+  constexpr bool PROF = !std::is_same<LK, LutLookup<R>>::value;
   uint32_t Da, Db, S1, X, DN, IN;
-  u16x2 best = best_, up = upT_;
-  asm volatile(
-      "v_perm_b32 %[Da], %[nv], %[t0], %[sel]\n\t"
-      "v_pk_add_f16 %[Da], %[dg], %[Da]"
-      : [Da] "=&v"(Da)
-      : [nv] "v"(nv), [t0] "s"(tab[0]), [sel] "v"(selw), [dg] "v"(diag_));
+  u16x2 best = best_, up = upX_;
+  if constexpr (PROF)
+    asm volatile(
+        "v_perm_b32 %[Da], %[h0], %[l0], %[sA]\n\t"
+        "v_pk_add_f16 %[Da], %[dg], %[Da]"
+        : [Da] "=&v"(Da)
+        : [h0] "v"(lk.hi[0]), [l0] "v"(lk.lo[0]), [sA] "s"(0x05040100u), [dg] "v"(diag_));
+  else
+    asm volatile(
+        "v_perm_b32 %[Da], %[nv], %[t0], %[sel]\n\t"
+        "v_pk_add_f16 %[Da], %[dg], %[Da]"
+        : [Da] "=&v"(Da)
+        : [nv] "v"(lk.nv), [t0] "s"(lk.tab[0]), [sel] "v"(lk.selw), [dg] "v"(diag_));
 #pragma unroll
   for (int b = 0; b < R; b += 8) {
-    if (b + 8 < R) {
-      if constexpr (ZDOWN)
-        asm volatile(SWK_F16_BLOCK_Z1_L0 : SWK_F16_OPS(b) : SWK_F16_INS(b));
-      else
-        asm volatile(SWK_F16_BLOCK_Z0_L0 : SWK_F16_OPS(b) : SWK_F16_INS(b));
+    const bool last = b + 8 >= R;
+    if constexpr (GOTOH) {
+      if constexpr (PROF) {
+        if (last) asm volatile(SWK_F16G_P_L1 : SWK_F16_OUT_G(b) : SWK_F16_IN_PG(b));
+        else      asm volatile(SWK_F16G_P_L0 : SWK_F16_OUT_G(b) : SWK_F16_IN_PG(b));
+      } else {
+        if (last) asm volatile(SWK_F16G_L_L1 : SWK_F16_OUT_G(b) : SWK_F16_IN_LG(b));
+        else      asm volatile(SWK_F16G_L_L0 : SWK_F16_OUT_G(b) : SWK_F16_IN_LG(b));
+      }
     } else {
-      if constexpr (ZDOWN)
-        asm volatile(SWK_F16_BLOCK_Z1_L1 : SWK_F16_OPS(b) : SWK_F16_INS(b));
-      else
-        asm volatile(SWK_F16_BLOCK_Z0_L1 : SWK_F16_OPS(b) : SWK_F16_INS(b));
+      if constexpr (PROF) {
+        if constexpr (ZDOWN) {
+          if (last) asm volatile(SWK_F16M_P_Z1_L1 : SWK_F16_OUT_M(b) : SWK_F16_IN_P(b));
+          else      asm volatile(SWK_F16M_P_Z1_L0 : SWK_F16_OUT_M(b) : SWK_F16_IN_P(b));
+        } else {
+          if (last) asm volatile(SWK_F16M_P_Z0_L1 : SWK_F16_OUT_M(b) : SWK_F16_IN_P(b));
+          else      asm volatile(SWK_F16M_P_Z0_L0 : SWK_F16_OUT_M(b) : SWK_F16_IN_P(b));
+        }
+      } else {
+        if constexpr (ZDOWN) {
+          if (last) asm volatile(SWK_F16M_L_Z1_L1 : SWK_F16_OUT_M(b) : SWK_F16_IN_L(b));
+          else      asm volatile(SWK_F16M_L_Z1_L0 : SWK_F16_OUT_M(b) : SWK_F16_IN_L(b));
+        } else {
+          if (last) asm volatile(SWK_F16M_L_Z0_L1 : SWK_F16_OUT_M(b) : SWK_F16_IN_L(b));
+          else      asm volatile(SWK_F16M_L_Z0_L0 : SWK_F16_OUT_M(b) : SWK_F16_IN_L(b));
+        }
+      }
+      up = ZDOWN ? as_u16x2(noe) : Xl[b + 7];
     }
-    up = ZDOWN ? as_u16x2(noe) : Tl[b + 7];
   }
   (void)Db; (void)S1; (void)X; (void)DN; (void)IN;
-  upT_ = up;
+  upX_ = up;
   best_ = best;
+}
+
+// f16 column: hand-ordered asm (default) or the compiler-scheduled C++ form (SWK_F16_ASM=0).
+template <int R, int RB, bool GOTOH, bool ZDOWN, class LK>
+__device__ __forceinline__ void column_f16(const LK& lk, u16x2& diag, u16x2& upX,
+                                           u16x2 (&Hl)[R], u16x2 (&Xl)[R], u16x2& best,
+                                           f16x2 NOE2, f16x2 NE2) {
+#if SWK_F16_ASM
+  column_f16_asm<R, GOTOH, ZDOWN>(lk, diag, upX, Hl, Xl, best, as_u32(as_u16x2(NOE2)),
+                                  as_u32(as_u16x2(NE2)));
+#else
+  if constexpr (GOTOH)
+    column_gotoh_f16<R, RB>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+  else
+    column_merged_f16<R, RB, ZDOWN>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+#endif
 }
 
 // ---- one column of R rows, Gotoh (separate E/F; ssearch36 semantics) ---------------------
@@ -536,12 +598,10 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
             lk.hi[4 * q + 3] = y.w;
           }
           __builtin_amdgcn_sched_barrier(0);
-          if constexpr (GOTOH)
-            column_gotoh_f16<R, RB>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
-          else if (COL0 && jj == 0 && c == 0)
-            column_merged_f16<R, RB, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+          if (COL0 && jj == 0 && c == 0)
+            column_f16<R, RB, GOTOH, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
           else
-            column_merged_f16<R, RB, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+            column_f16<R, RB, GOTOH, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
         } else if constexpr (PROF) {
           ProfLookup<R> lk;
           const uint32_t blo = min((wlo >> (8 * (jj & 3))) & 0xFFu, padc);
@@ -569,27 +629,12 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           // selector bytes {0x0C, code_lo, 0x0C, code_hi}: the LUT byte is the f16 high byte
           const uint32_t sel16 = 0x0Cu | ((uint32_t)(jj & 3) << 8) | (0x0Cu << 16) |
                                  ((uint32_t)(4 + (jj & 3)) << 24);
-          const uint32_t selw = __builtin_amdgcn_perm(whi, wlo, sel16) | 0x000C000Cu;
-          if constexpr (GOTOH) {
-            const LutLookup<R> lk{tab, nv, selw};
-            __builtin_amdgcn_sched_barrier(0);
-            column_gotoh_f16<R, RB>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
-          } else {
-#if SWK_F16_ASM
-          const uint32_t noe = as_u32(as_u16x2(NOE2)), ne = as_u32(as_u16x2(NE2));
-          if (COL0 && jj == 0 && c == 0)
-            column_merged_f16_asm<R, true>(tab, nv, selw, diag, upX, Hl, Xl, best, noe, ne);
-          else
-            column_merged_f16_asm<R, false>(tab, nv, selw, diag, upX, Hl, Xl, best, noe, ne);
-#else
-          const LutLookup<R> lk{tab, nv, selw};
+          const LutLookup<R> lk{tab, nv, __builtin_amdgcn_perm(whi, wlo, sel16) | 0x000C000Cu};
           __builtin_amdgcn_sched_barrier(0);
           if (COL0 && jj == 0 && c == 0)
-            column_merged_f16<R, RB, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+            column_f16<R, RB, GOTOH, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
           else
-            column_merged_f16<R, RB, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
-#endif
-          }
+            column_f16<R, RB, GOTOH, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
         } else {
           // selector: byte 0 = code of the low target, byte 2 = code of the high target
           const uint32_t sel =
