@@ -29,7 +29,10 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                        const void* edge_in, void* edge_out, uint32_t ecols,
-                                       int accum, int packed, hipStream_t st);
+                                       int accum, int packed, const uint32_t* idx,
+                                       const uint32_t* nidx, hipStream_t st);
+extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
+                                    uint32_t* idx, uint32_t* count, hipStream_t st);
 
 namespace {
 int env_int(const char* name, int dflt) {
@@ -88,6 +91,7 @@ struct sw_bank {
   uint32_t nv16 = 0, PS16 = 0;  // PS16: f16 profile row stride (bytes)
   int32_t f16_neg = 0;     // most negative intermediate: -(o + 2e + |min s|)
   DevBuf<uint32_t> qtab16;
+  DevBuf<uint32_t> fb_idx, fb_cnt;  // pairs an optimistic f16 pass re-scores in u16
   struct Seg { int W; size_t off, off16; };  // rows = W*R (last may be shorter); word offsets
                                               // in qtab and qtab16
   std::vector<Seg> segs;
@@ -189,6 +193,8 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   (void)sw_bank_timing(b, &nl, &pm, &sm);
   b->qtab.release();
   b->qtab16.release();
+  b->fb_idx.release();
+  b->fb_cnt.release();
   b->wtab.release();
   b->edge[0].release();
   b->edge[1].release();
@@ -480,19 +486,27 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   // and the most negative intermediate both within 2048
   const uint64_t top = std::min<uint64_t>(b->query.size(), max_len) * (uint64_t)std::max(0, b->smax) +
                        (uint64_t)std::max(0, b->smax);
-  const bool use_f16 = b->f16 && top <= 2048u && b->f16_neg >= -2048 &&
-                       env_int("SWBANK_F16", 1) != 0;  // SWBANK_F16=0: u16 kernel (tests)
+  // Past that bound the f16 pass is still exact for every pair whose computed score stays
+  // <= 2048 - max(s): a first rounded value needs an exact H > 2048 - max(s) on its
+  // diagonal, and the running max keeps it.  Optimistic mode scores all pairs in f16, then
+  // re-scores the pairs above that threshold in u16 (SWBANK_F16_OPT=0 disables).
+  const bool f16_ok = b->f16 && b->f16_neg >= -2048 && env_int("SWBANK_F16", 1) != 0;
+  const bool exact16 = f16_ok && top <= 2048u;
+  const bool opt16 = f16_ok && !exact16 && env_int("SWBANK_F16_OPT", 1) != 0;
+  const bool use_f16 = exact16 || opt16;
   // Kernel choice by a throughput model calibrated on MI355X (scripts/kernel_choice.py):
   //  tile kernel: base rate x fraction of the 256 CUs holding a tile x f(waves per SIMD),
   //    f = min(1, 0.45 + 0.15 w), x 0.85 when the query runs as several segments;
   //  wave kernel (queries <= 1024 rows): base rate x row fill (query / 64K lanes' rows) x
   //    column fill (L / (L + 63): the 63-step skew of the lane pipeline).
-  // Base GCUPS: tile f16 9000, u16 merged 7400, u16 Gotoh 5800, profile merged 6500,
-  // profile Gotoh 5600; wave merged 6500, Gotoh 5000.  SWBANK_KERNEL=tile|wave forces one.
+  // Base GCUPS: tile f16 merged 9000 (profile 8000), f16 Gotoh 7500 (profile 7100), u16
+  // merged 7400 (profile 6500), u16 Gotoh 5800 (profile 5600); wave merged 6500, Gotoh
+  // 5000.  SWBANK_KERNEL=tile|wave forces one.
   const double tiles = (double)ntiles, W = b->segs[0].W;
   const double cu_frac = std::min(1.0, tiles / 256.0);
   const double wps = std::min(4.0, std::max(1.0, std::ceil(tiles / 256.0)) * W / 4.0);
-  const double tile_base = use_f16 ? 9000 : b->prof ? (gotoh ? 5600 : 6500) : gotoh ? 5800 : 7400;
+  const double tile_base = use_f16 ? (gotoh ? (b->prof ? 7100 : 7500) : (b->prof ? 8000 : 9000))
+                                   : (gotoh ? (b->prof ? 5600 : 5800) : (b->prof ? 6500 : 7400));
   const double tile_est = tile_base * cu_frac * std::min(1.0, 0.45 + 0.15 * wps) *
                           (nseg > 1 ? 0.85 : 1.0);
   double wave_est = 0;
@@ -519,19 +533,33 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   }
   if (!use_wave)
     snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=%zu",
-             use_f16 ? "f16" : "u16", b->prof ? "-profile" : "", b->R, b->segs[0].W, nseg);
-  for (size_t s = 0; !use_wave && s < nseg; ++s) {
-    const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
-    void* eout = s + 1 < nseg ? b->edge[s & 1].p : nullptr;
-    HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof,
-                              b->cfg.gap_model == SW_GAP_GOTOH ? 1 : 0, use_f16 ? 1 : 0, d_res,
-                              d_offs, d_lens, n,
-                              use_f16 ? b->qtab16.p + b->segs[s].off16
-                                      : b->qtab.p + b->segs[s].off,
-                              use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
-                              use_f16 && b->prof ? b->PS16 : b->PS,
-                              b->pad, b->segs[s].W, d_scores, ein, eout, ecols, s > 0 ? 1 : 0,
-                              packed ? 1 : 0, st));
+             opt16 ? "f16+u16-rescore" : use_f16 ? "f16" : "u16", b->prof ? "-profile" : "", b->R,
+             b->segs[0].W, nseg);
+  // pass 0: every pair (f16 or u16); pass 1 (optimistic f16 only): flagged pairs in u16
+  for (int pass = 0; !use_wave && pass < (opt16 ? 2 : 1); ++pass) {
+    const bool f16 = use_f16 && pass == 0;
+    const uint32_t* idx = nullptr;
+    const uint32_t* nidx = nullptr;
+    if (pass == 1) {
+      HIPOK(b, b->fb_idx.reserve(n));
+      HIPOK(b, b->fb_cnt.reserve(1));
+      HIPOK(b, swk_flag_high(d_scores, n, 2048 - std::max(0, b->smax), b->fb_idx.p, b->fb_cnt.p,
+                             st));
+      idx = b->fb_idx.p;
+      nidx = b->fb_cnt.p;
+    }
+    for (size_t s = 0; s < nseg; ++s) {
+      const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
+      void* eout = s + 1 < nseg ? b->edge[s & 1].p : nullptr;
+      HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof, gotoh ? 1 : 0, f16 ? 1 : 0, d_res,
+                                d_offs, d_lens, n,
+                                f16 ? b->qtab16.p + b->segs[s].off16
+                                    : b->qtab.p + b->segs[s].off,
+                                f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
+                                f16 && b->prof ? b->PS16 : b->PS, b->pad, b->segs[s].W,
+                                d_scores, ein, eout, ecols, s > 0 ? 1 : 0, packed ? 1 : 0, idx,
+                                nidx, st));
+    }
   }
   if (b->timing) {
     HIPOK(b, hipEventRecord(ev.c, st));

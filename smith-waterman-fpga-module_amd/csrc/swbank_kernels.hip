@@ -373,20 +373,27 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint3
 
 // Per-tile metadata of one lane (uniform tile id).  packed: `res` is an array of 64-byte CAPI
 // records {u32 ID, u16 length, u8 data[58]} (aligner_Header.h:19-24).
+// idx (optional): position k of the batch is target idx[k] (the u16 re-score of the pairs an
+// optimistic f16 pass flagged).
 __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t* offs,
                                               const uint32_t* lens, size_t n, int tile, int lane,
-                                              bool packed) {
+                                              bool packed, const uint32_t* idx) {
   Lane2 t;
-  const size_t a = (size_t)tile * SWB_TILE + lane, b = a + 64;
+  size_t a = (size_t)tile * SWB_TILE + lane, b = a + 64;
+  const bool va = a < n, vb = b < n;  // positions in the batch
+  if (idx) {
+    a = va ? idx[a] : 0;
+    b = vb ? idx[b] : 0;
+  }
   if (packed) {
-    t.llo = a < n ? *reinterpret_cast<const uint16_t*>(res + a * SWB_RECORD + 4) : 0u;
-    t.lhi = b < n ? *reinterpret_cast<const uint16_t*>(res + b * SWB_RECORD + 4) : 0u;
-    t.plo = res + (a < n ? a : 0) * SWB_RECORD + 6;
-    t.phi = res + (b < n ? b : 0) * SWB_RECORD + 6;
+    t.llo = va ? *reinterpret_cast<const uint16_t*>(res + a * SWB_RECORD + 4) : 0u;
+    t.lhi = vb ? *reinterpret_cast<const uint16_t*>(res + b * SWB_RECORD + 4) : 0u;
+    t.plo = res + (va ? a : 0) * SWB_RECORD + 6;
+    t.phi = res + (vb ? b : 0) * SWB_RECORD + 6;
     return t;
   }
-  t.llo = a < n ? lens[a] : 0u;
-  t.lhi = b < n ? lens[b] : 0u;
+  t.llo = va ? lens[a] : 0u;
+  t.lhi = vb ? lens[b] : 0u;
   // an empty target still needs a readable address for the branch-free slow path
   t.plo = t.llo ? res + offs[a] : reinterpret_cast<const uint8_t*>(lens);
   t.phi = t.lhi ? res + offs[b] : reinterpret_cast<const uint8_t*>(lens);
@@ -427,6 +434,10 @@ struct ScoreArgs {
   uint32_t ecols;
   uint32_t accum;
   uint32_t packed;        // res = 64-byte CAPI records (2-bit codes); offs/lens unused
+  // optional position -> target map: positions [0, *nidx) score targets idx[k] (scores are
+  // written to scores[idx[k]]); used to re-score the pairs an optimistic f16 pass flagged
+  const uint32_t* idx;
+  const uint32_t* nidx;
 };
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -443,10 +454,11 @@ __device__ __forceinline__ void dma_edge_chunk(const uint2* src, uint2* dst, int
 
 // Chunk count of a tile (uniform), from the lengths alone.
 __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens, size_t n,
-                                        int tile, int lane, bool packed) {
+                                        int tile, int lane, bool packed, const uint32_t* idx) {
   const size_t a = (size_t)tile * SWB_TILE + lane, b = a + 64;
   auto len = [&](size_t k) -> uint32_t {
     if (k >= n) return 0u;
+    if (idx) k = idx[k];
     return packed ? *reinterpret_cast<const uint16_t*>(res + k * SWB_RECORD + 4) : lens[k];
   };
   uint32_t L = max(len(a), len(b));
@@ -480,16 +492,16 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   uint2* ring = ein + (seg_in ? 2 * C * 64 : 0);
   uint8_t* prof = reinterpret_cast<uint8_t*>(ring + (size_t)(W > 1 ? W - 1 : 0) * 2 * C * 64);
 
-  const size_t n = a.n;
+  const size_t n = a.idx ? min(a.n, (size_t)__builtin_amdgcn_readfirstlane(*a.nidx)) : a.n;
   const int ntiles = (int)((n + SWB_TILE - 1) / SWB_TILE);
   const int G = (int)gridDim.x;
   int total = 0;  // chunks of all this workgroup's tiles: every wave runs total + W - 1 phases
   const bool packed = a.packed != 0;
   for (int t = blockIdx.x; t < ntiles; t += G)
-    total += tile_nch(a.res, a.lens, n, t, lane, packed);
+    total += tile_nch(a.res, a.lens, n, t, lane, packed, a.idx);
 
   int tile = blockIdx.x;
-  Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed);
+  Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, a.idx);
   int nch, nfull;
   tile_chunks(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
               nfull);
@@ -560,7 +572,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       if (!last) {
         load_raw(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
       } else if (ntile < ntiles) {  // first chunk of the next tile
-        cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed);
+        cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed, a.idx);
         tile_chunks(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
                     n, nch_n, nfull_n);
         load_raw(cur, 0, nfull_n > 0, a.pad, packed, rlo, rhi);
@@ -673,12 +685,14 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
             blo = (int32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)blo);
             bhi = (int32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)bhi);
           }
+          const size_t slo = a.idx && tlo < n ? a.idx[tlo] : tlo;
+          const size_t shi = a.idx && thi < n ? a.idx[thi] : thi;
           if (a.accum) {  // best over the previous query segments
-            if (tlo < n) blo = max(blo, a.scores[tlo]);
-            if (thi < n) bhi = max(bhi, a.scores[thi]);
+            if (tlo < n) blo = max(blo, a.scores[slo]);
+            if (thi < n) bhi = max(bhi, a.scores[shi]);
           }
-          if (tlo < n) a.scores[tlo] = blo;
-          if (thi < n) a.scores[thi] = bhi;
+          if (tlo < n) a.scores[slo] = blo;
+          if (thi < n) a.scores[shi] = bhi;
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -966,11 +980,13 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                        const void* edge_in, void* edge_out, uint32_t ecols,
-                                       int accum, int packed, hipStream_t st) {
+                                       int accum, int packed, const uint32_t* idx,
+                                       const uint32_t* nidx, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                          O,    E,    PS,   pad, scores, static_cast<const uint2*>(edge_in),
-                         static_cast<uint2*>(edge_out), ecols, (uint32_t)accum, (uint32_t)packed};
+                         static_cast<uint2*>(edge_out), ecols, (uint32_t)accum, (uint32_t)packed,
+                         idx, nidx};
   const uint32_t prof_bytes = (pad + 1) * PS;
 #define SWK_CASE(RR, BB, C0, PF, GT, FH)                                                      \
   if (R == RR && RB == BB && col0 == C0 && prof == PF && gotoh == GT && f16 == FH)            \
@@ -979,6 +995,25 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
   SWK_VARIANTS(SWK_CASE)
 #undef SWK_CASE
   return hipErrorInvalidValue;
+}
+
+namespace swk {
+// Pairs an optimistic f16 pass may have rounded: score > thresh (= 2048 - max s) -> idx list.
+__global__ void __launch_bounds__(256) flag_kernel(const int32_t* scores, size_t n,
+                                                   int32_t thresh, uint32_t* idx,
+                                                   uint32_t* count) {
+  const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < n && scores[k] > thresh) idx[atomicAdd(count, 1u)] = (uint32_t)k;
+}
+}  // namespace swk
+
+extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
+                                    uint32_t* idx, uint32_t* count, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), st);
+  if (e != hipSuccess || n == 0) return e;
+  hipLaunchKernelGGL(swk::flag_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     scores, n, thresh, idx, count);
+  return hipGetLastError();
 }
 
 #define SWK_WAVE_VARIANTS(X)                                                              \
@@ -993,7 +1028,7 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, cons
                                       int packed, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
-                         nullptr, nullptr, 0u, 0u, (uint32_t)packed};
+                         nullptr, nullptr, 0u, 0u, (uint32_t)packed, nullptr, nullptr};
   const uint32_t prof_bytes = (pad + 1) * PS;
 #define SWK_WCASE(KK, C0, PF, GT)                                                  \
   if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                          \

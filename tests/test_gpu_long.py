@@ -96,3 +96,43 @@ def test_generated_golden_swapped_orientation():
             for t, want in zip(c["targets"][:12], c["scores"][:12]):
                 bank.load_query(S.encode(t))
                 assert bank.score_targets([S.encode(c["query"])]).tolist() == [want]
+
+
+@pytest.mark.parametrize("alphabet", ["dna", "protein"])
+@pytest.mark.parametrize("model", [S.GAP_MERGED, S.GAP_GOTOH])
+def test_optimistic_f16_rescore(alphabet, model, kernel_choice):
+    """Past the exact f16 bound the tile kernel scores every pair in f16 and re-scores, in
+    u16, only the pairs whose f16 score exceeds 2048 - max(s) (the only ones a rounded value
+    can have touched).  Half the targets here are near-copies scoring far above 2048, half
+    are random; long queries run as several segments in both passes."""
+    rng = np.random.default_rng(11 + model + (alphabet == "dna"))
+    A = 4 if alphabet == "dna" else 20
+    qlen = 1200 if alphabet == "dna" else 700
+    q = rng.integers(0, A, qlen, dtype=np.uint8)
+    seqs = []
+    for k in range(260):
+        if k % 2:
+            seqs.append(rng.integers(0, A, int(rng.integers(0, 900)), dtype=np.uint8))
+        else:
+            a = int(rng.integers(0, qlen // 3))
+            t = q[a:a + int(rng.integers(300, 900))].copy()
+            t[::13] = rng.integers(0, A, len(t[::13]))
+            seqs.append(t)
+    with S.ScoreBank(alphabet=S.ALPHABET_DNA if alphabet == "dna" else S.ALPHABET_PROTEIN,
+                     gap_model=model) as bank:
+        if alphabet == "dna":
+            bank.set_penalties(5, -4, -10, -1)
+            sub, go, ge = O.dna_matrix(5, -4), -10, -1
+        else:
+            bank.set_matrix(O.BLOSUM62, -11, -1)
+            sub, go, ge = O.BLOSUM62, -11, -1
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+        kern = bank.last_kernel()
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, sub, go, ge, model)
+    assert want.max() > 2048 and (want < 2000).sum() > 100
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (kern, [(int(i), int(got[i]), int(want[i])) for i in bad[:8]])
+    if kernel_choice == "tile":
+        assert kern.startswith("tile f16+u16-rescore"), kern
