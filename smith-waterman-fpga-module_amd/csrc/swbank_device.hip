@@ -18,7 +18,8 @@
 #include "swbank_internal.h"
 
 extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh, int f16);
-extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, const uint8_t* res,
+extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int f16,
+                                      const uint8_t* res,
                                       const uint64_t* offs, const uint32_t* lens, size_t n,
                                       const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
@@ -100,6 +101,8 @@ struct sw_bank {
   int wK = 0;              // 0: query too long for the wave kernel
   uint32_t wPS = 0;
   DevBuf<uint32_t> wtab;   // LUT: 64K row words | PROF: (A+1) x 64K profile bytes
+  DevBuf<uint32_t> wtab16; // the same in f16 (LUT: high bytes | PROF: 2-byte entries)
+  uint32_t wPS16 = 0;
 
   // workspaces
   DevBuf<uint8_t> res;
@@ -196,6 +199,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->fb_idx.release();
   b->fb_cnt.release();
   b->wtab.release();
+  b->wtab16.release();
   b->edge[0].release();
   b->edge[1].release();
   b->res.release();
@@ -415,7 +419,38 @@ static sw_status prepare(sw_bank* b) {
       std::memcpy(wt.data(), qp.data(), qp.size());
     }
   }
+  std::vector<uint32_t> wt16;
+  uint32_t wPS16 = 0;
+  if (wK && f16) {
+    const int rows = 64 * wK;
+    if (!prof) {
+      wt16.assign((size_t)rows, 0xE8E8E8E8u);  // rows past the query: -2048
+      for (int i = 0; i < qlen; ++i) {
+        uint32_t w = 0;
+        for (int c = 0; c < 4; ++c) {
+          uint8_t h;
+          f16_hi(m[b->query[i] * A + c], &h);
+          w |= (uint32_t)h << (8 * c);
+        }
+        wt16[i] = w;
+      }
+    } else {
+      wPS16 = (uint32_t)rows * 2;
+      std::vector<uint16_t> qp((size_t)(A + 1) * rows, 0xE800u);
+      for (int c = 0; c < A; ++c)
+        for (int i = 0; i < qlen; ++i)
+          qp[(size_t)c * rows + i] = __builtin_bit_cast(uint16_t, (_Float16)(float)m[b->query[i] * A + c]);
+      wt16.resize(qp.size() / 2);
+      std::memcpy(wt16.data(), qp.data(), qp.size() * 2);
+    }
+  }
   HIPOK(b, hipSetDevice(b->device));
+  if (!wt16.empty()) {
+    HIPOK(b, b->wtab16.reserve(wt16.size()));
+    HIPOK(b, hipMemcpyAsync(b->wtab16.p, wt16.data(), wt16.size() * 4, hipMemcpyHostToDevice,
+                            b->stream));
+  }
+  b->wPS16 = wPS16;
   if (wK) {
     HIPOK(b, b->wtab.reserve(wt.size()));
     HIPOK(b, hipMemcpyAsync(b->wtab.p, wt.data(), wt.size() * 4, hipMemcpyHostToDevice,
@@ -519,24 +554,27 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   bool use_wave = b->wK > 0 && wave_est > tile_est;
   if (kforce && std::strcmp(kforce, "tile") == 0) use_wave = false;
   if (kforce && std::strcmp(kforce, "wave") == 0 && b->wK > 0) use_wave = true;
+  const char* arith = opt16 ? "f16+u16-rescore" : use_f16 ? "f16" : "u16";
   if (use_wave) {
-    snprintf(b->last_kernel, sizeof(b->last_kernel), "wave %s K=%d",
-             b->prof ? "u16-profile" : "u16", b->wK);
-    HIPOK(b, swk_launch_wave(b->wK, b->col0, b->prof, gotoh ? 1 : 0,
-                             d_res, d_offs, d_lens, n, b->wtab.p, b->nv, b->S, b->O, b->E,
-                             b->wPS, b->pad, d_scores, packed ? 1 : 0, st));
+    snprintf(b->last_kernel, sizeof(b->last_kernel), "wave %s%s K=%d", arith,
+             b->prof ? "-profile" : "", b->wK);
+    HIPOK(b, swk_launch_wave(b->wK, b->col0, b->prof, gotoh ? 1 : 0, use_f16 ? 1 : 0, d_res,
+                             d_offs, d_lens, n, use_f16 ? b->wtab16.p : b->wtab.p,
+                             use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
+                             use_f16 && b->prof ? b->wPS16 : b->wPS, b->pad, d_scores,
+                             packed ? 1 : 0, st));
+  } else {
+    snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=%zu", arith,
+             b->prof ? "-profile" : "", b->R, b->segs[0].W, nseg);
   }
-  if (!use_wave && nseg > 1) {
+  if (nseg > 1 && (!use_wave || opt16)) {
     const size_t words = std::max<size_t>(1, ntiles * ecols * 64);
     HIPOK(b, b->edge[0].reserve(words));
     HIPOK(b, b->edge[1].reserve(words));
   }
-  if (!use_wave)
-    snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=%zu",
-             opt16 ? "f16+u16-rescore" : use_f16 ? "f16" : "u16", b->prof ? "-profile" : "", b->R,
-             b->segs[0].W, nseg);
-  // pass 0: every pair (f16 or u16); pass 1 (optimistic f16 only): flagged pairs in u16
-  for (int pass = 0; !use_wave && pass < (opt16 ? 2 : 1); ++pass) {
+  // pass 0: every pair with the tile kernel (unless the wave kernel ran); pass 1 (optimistic
+  // f16 only): the pairs scoring above 2048 - max(s), re-scored in u16 by the tile kernel
+  for (int pass = use_wave ? 1 : 0; pass < (opt16 ? 2 : 1); ++pass) {
     const bool f16 = use_f16 && pass == 0;
     const uint32_t* idx = nullptr;
     const uint32_t* nidx = nullptr;

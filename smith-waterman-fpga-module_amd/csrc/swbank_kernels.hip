@@ -772,6 +772,15 @@ struct ProfLookupK {
   }
 };
 template <int K>
+struct ProfLookupK16 {  // f16 profile, 2-byte entries: word k = rows 2k, 2k+1 of a letter
+  uint32_t lo[K / 2], hi[K / 2];
+  __device__ __forceinline__ u16x2 operator()(int r) const {
+    const uint32_t k = (uint32_t)(r & 1) * 2;
+    const uint32_t sel = k | ((k + 1) << 8) | ((k + 4) << 16) | ((k + 5) << 24);
+    return as_u16x2(__builtin_amdgcn_perm(hi[r >> 1], lo[r >> 1], sel));
+  }
+};
+template <int K>
 struct LaneLutLookup {  // per-lane row LUTs (the lane's own query rows) in VGPRs
   const uint32_t (&lut)[K];
   uint32_t nv, selw;
@@ -801,12 +810,37 @@ __device__ __forceinline__ void column_merged_mask(const LK& lk, u16x2& diag, u1
   }
 }
 
+// f16 merged column with a per-lane column-0 mask (zdown: T passed down = -o-e)
+template <int R, int RB, class LK>
+__device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag_, u16x2& upT_,
+                                                       u16x2 (&Hl)[R], u16x2 (&Tl)[R],
+                                                       u16x2& best_, f16x2 NOE2, f16x2 NE2,
+                                                       bool zdown) {
+  f16x2 diag = as_f16x2(diag_), upT = as_f16x2(upT_), best = as_f16x2(best_);
+  const f16x2 Z = {(_Float16)0, (_Float16)0};
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const f16x2 D = diag + as_f16x2(lk(r));
+    const f16x2 I = fmax2(upT, as_f16x2(Tl[r]));
+    const f16x2 H = fmax2(fmax2(D, Z), I);
+    const f16x2 T = fmax2(fmax2(D + NOE2, NOE2), I + NE2);
+    best = fmax2(best, H);
+    diag = as_f16x2(Hl[r]);
+    Hl[r] = as_u16x2(H);
+    Tl[r] = as_u16x2(T);
+    upT = zdown ? NOE2 : T;
+    if ((r % RB) == RB - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+  upT_ = as_u16x2(upT);
+  best_ = as_u16x2(best);
+}
+
 __device__ __forceinline__ uint32_t dpp_shr1(uint32_t lane0_value, uint32_t v) {
   return __builtin_amdgcn_update_dpp(lane0_value, v, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
 }
 
 // qtab (wave layout): LUT: 64*K row words | PROF: (pad+1) x PS bytes, PS = 64*K.
-template <int K, bool COL0, bool PROF, bool GOTOH>
+template <int K, bool COL0, bool PROF, bool GOTOH, bool F16>
 __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
@@ -838,7 +872,14 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
   const u16x2 E2 = {(unsigned short)a.E, (unsigned short)a.E};
   const uint32_t oes = a.O + a.E + S;
   const u16x2 OES2 = {(unsigned short)oes, (unsigned short)oes};
-  const uint32_t padsel = pad | (pad << 16) | 0x0C000C00u;
+  // selector word: u16 {code_lo, 0x0C, code_hi, 0x0C}; f16 {0x0C, code_lo, 0x0C, code_hi}
+  // (the f16 LUT byte is the high byte; 2-byte f16 profiles use the code byte only)
+  const uint32_t padsel = F16 && !PROF ? ((pad << 8) | (pad << 24) | 0x000C000Cu)
+                                       : (pad | (pad << 16) | 0x0C000C00u);
+  const _Float16 fnoe = (_Float16)(-(float)(a.O + a.E)), fne = (_Float16)(-(float)a.E);
+  const f16x2 NOE2 = {fnoe, fnoe}, NE2 = {fne, fne};
+  const u16x2 H0 = F16 ? (u16x2){0, 0} : S2;                          // H of row/col -1
+  const u16x2 X0 = (F16 && !GOTOH) ? as_u16x2(NOE2) : (u16x2){0, 0};  // T/G/E/F of row/col -1
 
   uint32_t lut[PROF ? 1 : K];
   if constexpr (!PROF) {
@@ -846,17 +887,18 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
     for (int k = 0; k < K; ++k) lut[k] = a.qtab[lane * K + k];
   }
   const uint32_t nv = a.nv;
-  const uint8_t* prow = prof + lane * K;  // this lane's rows in every profile letter row
+  const uint8_t* prow = prof + lane * K;       // this lane's rows in every profile letter row
+  const uint8_t* prow2 = prof + lane * K * 2;  // f16 profile: 2 bytes per row
 
   u16x2 Hl[K], Xl[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    Hl[k] = S2;
-    Xl[k] = (u16x2){0, 0};
+    Hl[k] = H0;
+    Xl[k] = X0;
   }
   u16x2 best = {0, 0};
-  u16x2 prevUpH = S2;
-  uint32_t botH = as_u32(S2), botX = 0u, let = padsel, buf = padsel;
+  u16x2 prevUpH = H0;
+  uint32_t botH = as_u32(H0), botX = as_u32(X0), let = padsel, buf = padsel;
 
   const int nsteps = Lmax + 63;
   for (int t = 0; t < nsteps; ++t) {
@@ -870,16 +912,54 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
         if (c < LA) x = pA[c];
         if (c < LB) y = pB[c];
       }
-      buf = min(x, pad) | (min(y, pad) << 16) | 0x0C000C00u;
+      buf = F16 && !PROF ? ((min(x, pad) << 8) | (min(y, pad) << 24) | 0x000C000Cu)
+                         : (min(x, pad) | (min(y, pad) << 16) | 0x0C000C00u);
     }
     const uint32_t inj = __builtin_amdgcn_readlane(buf, t & 63);
-    const u16x2 upH = as_u16x2(dpp_shr1(as_u32(S2), botH));
-    u16x2 upX = as_u16x2(dpp_shr1(0u, botX));
+    const u16x2 upH = as_u16x2(dpp_shr1(as_u32(H0), botH));
+    u16x2 upX = as_u16x2(dpp_shr1(as_u32(X0), botX));
     let = dpp_shr1(inj, let);
     u16x2 diag = prevUpH;
     prevUpH = upH;
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (PROF) {
+    if constexpr (F16) {
+      const bool z = COL0 && t == lane;
+      if constexpr (PROF) {
+        ProfLookupK16<K> lk;
+        const uint32_t blo = let & 0xFFu, bhi = (let >> 16) & 0xFFu;
+        const uint8_t* plo = prow2 + blo * a.PS;
+        const uint8_t* phi = prow2 + bhi * a.PS;
+        if constexpr (K == 4) {
+          const uint2 x = *reinterpret_cast<const uint2*>(plo);
+          const uint2 y = *reinterpret_cast<const uint2*>(phi);
+          lk.lo[0] = x.x; lk.lo[1] = x.y; lk.hi[0] = y.x; lk.hi[1] = y.y;
+        } else {
+#pragma unroll
+          for (int q = 0; q < K / 8; ++q) {
+            const uint4 x = reinterpret_cast<const uint4*>(plo)[q];
+            const uint4 y = reinterpret_cast<const uint4*>(phi)[q];
+            lk.lo[4 * q] = x.x; lk.lo[4 * q + 1] = x.y; lk.lo[4 * q + 2] = x.z;
+            lk.lo[4 * q + 3] = x.w;
+            lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z;
+            lk.hi[4 * q + 3] = y.w;
+          }
+        }
+        if constexpr (GOTOH)
+          column_gotoh_f16<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+        else if constexpr (COL0)
+          column_merged_f16_mask<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, z);
+        else
+          column_merged_f16<K, 4, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+      } else {
+        const LaneLutLookup<K> lk{lut, nv, let};
+        if constexpr (GOTOH)
+          column_gotoh_f16<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+        else if constexpr (COL0)
+          column_merged_f16_mask<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, z);
+        else
+          column_merged_f16<K, 4, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+      }
+    } else if constexpr (PROF) {
       ProfLookupK<K> lk;
       const uint32_t blo = let & 0xFFu, bhi = (let >> 16) & 0xFFu;
       if constexpr (K == 4) {
@@ -920,8 +1000,12 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
     botH = as_u32(Hl[K - 1]);
     botX = as_u32(upX);
   }
-  // max over the wave's rows, per target
+  // max over the wave's rows, per target (f16: non-negative integers -> int)
   uint32_t bx = best.x, by = best.y;
+  if constexpr (F16) {
+    bx = (uint32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)bx);
+    by = (uint32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)by);
+  }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     bx = max(bx, (uint32_t)__shfl_xor((int)bx, off));
@@ -933,12 +1017,12 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
   }
 }
 
-template <int K, bool COL0, bool PROF, bool GOTOH>
+template <int K, bool COL0, bool PROF, bool GOTOH, bool F16>
 static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream_t st) {
   const size_t pairs = (a.n + 1) / 2;
   const size_t blocks = (pairs + 3) / 4;
   const size_t lds = PROF ? prof_bytes : 0;
-  auto fn = &score_wave<K, COL0, PROF, GOTOH>;
+  auto fn = &score_wave<K, COL0, PROF, GOTOH, F16>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -1016,12 +1100,14 @@ extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thr
   return hipGetLastError();
 }
 
+// (K, COL0, PROF, GOTOH) x {u16, f16}
 #define SWK_WAVE_VARIANTS(X)                                                              \
   X(4, 0, 0, 0) X(4, 1, 0, 0) X(4, 0, 0, 1) X(4, 0, 1, 0) X(4, 1, 1, 0) X(4, 0, 1, 1)     \
   X(8, 0, 0, 0) X(8, 1, 0, 0) X(8, 0, 0, 1) X(8, 0, 1, 0) X(8, 1, 1, 0) X(8, 0, 1, 1)     \
   X(16, 0, 0, 0) X(16, 1, 0, 0) X(16, 0, 0, 1) X(16, 0, 1, 0) X(16, 1, 1, 0) X(16, 0, 1, 1)
 
-extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, const uint8_t* res,
+extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int f16,
+                                      const uint8_t* res,
                                       const uint64_t* offs, const uint32_t* lens, size_t n,
                                       const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
@@ -1030,9 +1116,10 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, cons
   const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
                          nullptr, nullptr, 0u, 0u, (uint32_t)packed, nullptr, nullptr};
   const uint32_t prof_bytes = (pad + 1) * PS;
-#define SWK_WCASE(KK, C0, PF, GT)                                                  \
-  if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                          \
-    return swk::launch_wave<KK, (C0 != 0), (PF != 0), (GT != 0)>(a, prof_bytes, st);
+#define SWK_WCASE(KK, C0, PF, GT)                                                         \
+  if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                                 \
+    return f16 ? swk::launch_wave<KK, (C0 != 0), (PF != 0), (GT != 0), true>(a, prof_bytes, st) \
+               : swk::launch_wave<KK, (C0 != 0), (PF != 0), (GT != 0), false>(a, prof_bytes, st);
   SWK_WAVE_VARIANTS(SWK_WCASE)
 #undef SWK_WCASE
   return hipErrorInvalidValue;

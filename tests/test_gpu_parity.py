@@ -15,16 +15,16 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["tile", "tile-u16", "wave"])
+@pytest.fixture(autouse=True, params=["tile", "tile-u16", "wave", "wave-u16"])
 def kernel_choice(request, monkeypatch):
     """Run every parity test through each score kernel: the tile kernel (waves = row blocks,
-    lanes = targets) with its f16 arithmetic where the batch's score bound allows it
-    ("tile") and forced to u16 ("tile-u16"), and the wave kernel (lanes = rows, DPP
-    hand-off).  The wave kernel takes queries up to 1024 rows; longer ones fall back to
-    the tile kernel."""
+    lanes = targets) and the wave kernel (lanes = rows, DPP hand-off), each with its f16
+    arithmetic where eligible ("tile", "wave": exact below the f16 bound, optimistic with a
+    u16 re-score above it) and forced to u16 ("-u16").  The wave kernel takes queries up to
+    1024 rows; longer ones fall back to the tile kernel."""
     kern = request.param.split("-")[0]
     monkeypatch.setenv("SWBANK_KERNEL", kern)
-    monkeypatch.setenv("SWBANK_F16", "0" if request.param == "tile-u16" else "1")
+    monkeypatch.setenv("SWBANK_F16", "0" if request.param.endswith("-u16") else "1")
     return request.param
 
 
