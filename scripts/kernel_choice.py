@@ -54,9 +54,9 @@ def main():
         bank.load_query(q)
         out = {"alphabet": alpha, "model": model, "qlen": qlen, "L": L, "n": n}
         ref = None
-        for kern in ("tile", "tile-u16", "wave", "auto"):
+        for kern in ("tile", "tile-u16", "wave", "wave-u16", "auto"):
             os.environ["SWBANK_KERNEL"] = kern.split("-")[0]
-            os.environ["SWBANK_F16"] = "0" if kern == "tile-u16" else "1"
+            os.environ["SWBANK_F16"] = "0" if kern.endswith("-u16") else "1"
             bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,
                                     d_sc.data_ptr(), stream)
             torch.cuda.synchronize()
