@@ -10,7 +10,7 @@ Penalties 5/-4/-12/-4 (data/smith-waterman.py:6-10), merged gap model (the Score
 Other workloads (``--workload``), same JSON line:
   reads150x1k    configs[3]: per GPU ``--reads`` synthetic 150-bp reads x a fixed slice of
                  ``--slice`` 1-kbp targets (every read x every target of the slice); each
-                 1-kbp target is the bank query (4 segments of 256 rows), the reads the batch.
+                 1-kbp target is the bank query (2 segments of 512 rows), the reads the batch.
   protein512x1k  configs[4]: a 512-aa query x ``--ptargets`` 1-kaa targets per GPU,
                  BLOSUM62, gap -11/-1, Gotoh (ssearch36 semantics), uniform 20-letter residues.
 
@@ -133,7 +133,7 @@ class Workload:
             self.name = f"reads150x{n}x1k{args.slice}"
             self.desc = (f"{n} synthetic 150-bp reads per GPU x a slice of {args.slice} "
                          f"synthetic 1-kbp targets (BASELINE configs[3]); target = bank query "
-                         f"(4 x 256-row segments), reads = batch")
+                         f"(2 x 512-row segments), reads = batch")
             self.params = {"penalties": list(PEN), "gap_model": "merged (ScoreBank PE)"}
         else:
             n, L = args.ptargets, 1000

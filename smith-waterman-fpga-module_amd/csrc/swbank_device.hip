@@ -295,13 +295,14 @@ static sw_status prepare(sw_bank* b) {
   // Rows per wave: 32 for the merged DNA LUT kernels; 16 for tiny queries and for the
   // Gotoh / profile / column-0 variants, whose 32-row columns do not fit 128 VGPRs (the
   // occupancy-4 budget) without spilling.  Queries longer than one workgroup (16 waves) run
-  // as segments of SWBANK_SEG rows (default 256), each segment's bottom row handed to the
-  // next through HBM.  SWBANK_R / SWBANK_RB / SWBANK_SEG override (tuning only).
+  // as segments of SWBANK_SEG rows (default: a full 16-wave workgroup, 16·R rows), each
+  // segment's bottom row handed to the next through HBM.  SWBANK_R / SWBANK_RB / SWBANK_SEG
+  // override (tuning only).
   int R = (qlen <= 16 || gotoh || prof || col0) ? 16 : 32, RB = 4;
   R = env_int("SWBANK_R", R);
   RB = env_int("SWBANK_RB", RB);
   const int max_rows = (R >= 64 ? 8 : 16) * R;
-  int seg_rows = qlen > max_rows ? env_int("SWBANK_SEG", std::min(256, max_rows))
+  int seg_rows = qlen > max_rows ? env_int("SWBANK_SEG", max_rows)
                                  : std::max(qlen, 1);
   if (seg_rows % R != 0 && seg_rows < qlen)
     return fail(b, SW_ERR_ARG, "segment rows %d not a multiple of R=%d", seg_rows, R);
