@@ -536,8 +536,8 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   //  wave kernel (queries <= 1024 rows): base rate x row fill (query / 64K lanes' rows) x
   //    column fill (L / (L + 63): the 63-step skew of the lane pipeline).
   // Base GCUPS: tile f16 merged 9000 (profile 8000), f16 Gotoh 7500 (profile 7100), u16
-  // merged 7400 (profile 6500), u16 Gotoh 5800 (profile 5600); wave f16 merged 7200, f16
-  // Gotoh 5800, u16 merged 6500, u16 Gotoh 5000.  SWBANK_KERNEL=tile|wave forces one.
+  // merged 7400 (profile 6500), u16 Gotoh 5800 (profile 5600); wave f16 merged 7600, f16
+  // Gotoh 6600, u16 merged 6500, u16 Gotoh 5000.  SWBANK_KERNEL=tile|wave forces one.
   const double tiles = (double)ntiles, W = b->segs[0].W;
   const double cu_frac = std::min(1.0, tiles / 256.0);
   const double wps = std::min(4.0, std::max(1.0, std::ceil(tiles / 256.0)) * W / 4.0);
@@ -549,7 +549,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   if (b->wK > 0) {
     const double rowfill = (double)b->query.size() / (64.0 * b->wK);
     const double colfill = max_len / (max_len + 63.0);
-    wave_est = (use_f16 ? (gotoh ? 5800 : 7200) : (gotoh ? 5000 : 6500)) * rowfill * colfill;
+    wave_est = (use_f16 ? (gotoh ? 6600 : 7600) : (gotoh ? 5000 : 6500)) * rowfill * colfill;
   }
   const char* kforce = std::getenv("SWBANK_KERNEL");
   bool use_wave = b->wK > 0 && wave_est > tile_est;

@@ -835,6 +835,96 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
   best_ = as_u16x2(best);
 }
 
+// Wave-kernel f16 column (K rows per lane, no column-0 rule), hand-ordered asm: the same
+// generated row blocks as the tile kernel with the lane's own LUT words / profile words in
+// VGPRs.  K = 4: one 4-row block; K = 8, 16: 8-row blocks.
+#define SWK_CLAMP(x, n) ((x) < (n) ? (x) : (n) - 1)
+#define SWK_W_HT(B)                                                                           \
+  [h0] "+v"(Hl[B]), [h1] "+v"(Hl[SWK_CLAMP(B + 1, K)]), [h2] "+v"(Hl[SWK_CLAMP(B + 2, K)]),    \
+      [h3] "+v"(Hl[SWK_CLAMP(B + 3, K)]), [h4] "+v"(Hl[SWK_CLAMP(B + 4, K)]),                  \
+      [h5] "+v"(Hl[SWK_CLAMP(B + 5, K)]), [h6] "+v"(Hl[SWK_CLAMP(B + 6, K)]),                  \
+      [h7] "+v"(Hl[SWK_CLAMP(B + 7, K)]), [t0] "+v"(Xl[B]), [t1] "+v"(Xl[SWK_CLAMP(B + 1, K)]), \
+      [t2] "+v"(Xl[SWK_CLAMP(B + 2, K)]), [t3] "+v"(Xl[SWK_CLAMP(B + 3, K)]),                  \
+      [t4] "+v"(Xl[SWK_CLAMP(B + 4, K)]), [t5] "+v"(Xl[SWK_CLAMP(B + 5, K)]),                  \
+      [t6] "+v"(Xl[SWK_CLAMP(B + 6, K)]), [t7] "+v"(Xl[SWK_CLAMP(B + 7, K)]), [Da] "+v"(Da),   \
+      [Db] "=&v"(Db), [S1] "=&v"(S1), [best] "+v"(best)
+#define SWK_W_OUT_M(B) SWK_W_HT(B), [X] "=&v"(X), [DN] "=&v"(DN), [IN] "=&v"(IN)
+// K = 4: four distinct rows only (an output operand bound twice would copy back stale values)
+#define SWK_W4_HT                                                                             \
+  [h0] "+v"(Hl[0]), [h1] "+v"(Hl[1]), [h2] "+v"(Hl[2]), [h3] "+v"(Hl[3]), [t0] "+v"(Xl[0]),    \
+      [t1] "+v"(Xl[1]), [t2] "+v"(Xl[2]), [t3] "+v"(Xl[3]), [Da] "+v"(Da), [Db] "=&v"(Db),     \
+      [S1] "=&v"(S1), [best] "+v"(best)
+#define SWK_W4_OUT_M SWK_W4_HT, [X] "=&v"(X), [DN] "=&v"(DN), [IN] "=&v"(IN)
+#define SWK_W4_OUT_G SWK_W4_HT, [EN] "=&v"(X), [HN] "=&v"(DN), [FN] "=&v"(IN), [F] "+v"(up)
+#define SWK_W_OUT_G(B) SWK_W_HT(B), [EN] "=&v"(X), [HN] "=&v"(DN), [FN] "=&v"(IN), [F] "+v"(up)
+#define SWK_W_TB(B)                                                                           \
+  [tb0] "v"(lk.lut[SWK_CLAMP(B + 1, K)]), [tb1] "v"(lk.lut[SWK_CLAMP(B + 2, K)]),              \
+      [tb2] "v"(lk.lut[SWK_CLAMP(B + 3, K)]), [tb3] "v"(lk.lut[SWK_CLAMP(B + 4, K)]),          \
+      [tb4] "v"(lk.lut[SWK_CLAMP(B + 5, K)]), [tb5] "v"(lk.lut[SWK_CLAMP(B + 6, K)]),          \
+      [tb6] "v"(lk.lut[SWK_CLAMP(B + 7, K)]), [tb7] "v"(lk.lut[SWK_CLAMP(B + 8, K)])
+#define SWK_W_LH(B)                                                                           \
+  [lo0] "v"(lk.lo[B / 2]), [lo1] "v"(lk.lo[SWK_CLAMP(B / 2 + 1, K / 2)]),                      \
+      [lo2] "v"(lk.lo[SWK_CLAMP(B / 2 + 2, K / 2)]), [lo3] "v"(lk.lo[SWK_CLAMP(B / 2 + 3, K / 2)]), \
+      [lo4] "v"(lk.lo[SWK_CLAMP(B / 2 + 4, K / 2)]), [hi0] "v"(lk.hi[B / 2]),                  \
+      [hi1] "v"(lk.hi[SWK_CLAMP(B / 2 + 1, K / 2)]), [hi2] "v"(lk.hi[SWK_CLAMP(B / 2 + 2, K / 2)]), \
+      [hi3] "v"(lk.hi[SWK_CLAMP(B / 2 + 3, K / 2)]), [hi4] "v"(lk.hi[SWK_CLAMP(B / 2 + 4, K / 2)])
+#define SWK_W_IN_LM(B) [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up), SWK_W_TB(B)
+#define SWK_W_IN_LG(B) [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), SWK_W_TB(B)
+#define SWK_W_IN_PM(B)                                                                        \
+  [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), \
+      SWK_W_LH(B)
+#define SWK_W_IN_PG(B) [noe] "s"(noe), [ne] "s"(ne), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), SWK_W_LH(B)
+
+template <int K, bool GOTOH, class LK>
+__device__ __forceinline__ void column_f16_lane_asm(const LK& lk, u16x2& diag_, u16x2& upX_,
+                                                    u16x2 (&Hl)[K], u16x2 (&Xl)[K],
+                                                    u16x2& best_, uint32_t noe, uint32_t ne) {
+  constexpr bool PROF = !std::is_same<LK, LaneLutLookup<K>>::value;
+  uint32_t Da, Db, S1, X, DN, IN;
+  u16x2 best = best_, up = upX_;
+  if constexpr (PROF)
+    asm volatile(
+        "v_perm_b32 %[Da], %[h0], %[l0], %[sA]\n\t"
+        "v_pk_add_f16 %[Da], %[dg], %[Da]"
+        : [Da] "=&v"(Da)
+        : [h0] "v"(lk.hi[0]), [l0] "v"(lk.lo[0]), [sA] "s"(0x05040100u), [dg] "v"(diag_));
+  else
+    asm volatile(
+        "v_perm_b32 %[Da], %[nv], %[t0], %[sel]\n\t"
+        "v_pk_add_f16 %[Da], %[dg], %[Da]"
+        : [Da] "=&v"(Da)
+        : [nv] "v"(lk.nv), [t0] "v"(lk.lut[0]), [sel] "v"(lk.selw), [dg] "v"(diag_));
+  if constexpr (K == 4) {
+    if constexpr (GOTOH && PROF) asm volatile(SWK_F16G_P_L1_R4 : SWK_W4_OUT_G : SWK_W_IN_PG(0));
+    else if constexpr (GOTOH)    asm volatile(SWK_F16G_L_L1_R4 : SWK_W4_OUT_G : SWK_W_IN_LG(0));
+    else if constexpr (PROF)     asm volatile(SWK_F16M_P_Z0_L1_R4 : SWK_W4_OUT_M : SWK_W_IN_PM(0));
+    else                         asm volatile(SWK_F16M_L_Z0_L1_R4 : SWK_W4_OUT_M : SWK_W_IN_LM(0));
+    if constexpr (!GOTOH) up = Xl[3];
+  } else {
+#pragma unroll
+    for (int b = 0; b < K; b += 8) {
+      const bool last = b + 8 >= K;
+      if constexpr (GOTOH && PROF) {
+        if (last) asm volatile(SWK_F16G_P_L1 : SWK_W_OUT_G(b) : SWK_W_IN_PG(b));
+        else      asm volatile(SWK_F16G_P_L0 : SWK_W_OUT_G(b) : SWK_W_IN_PG(b));
+      } else if constexpr (GOTOH) {
+        if (last) asm volatile(SWK_F16G_L_L1 : SWK_W_OUT_G(b) : SWK_W_IN_LG(b));
+        else      asm volatile(SWK_F16G_L_L0 : SWK_W_OUT_G(b) : SWK_W_IN_LG(b));
+      } else if constexpr (PROF) {
+        if (last) asm volatile(SWK_F16M_P_Z0_L1 : SWK_W_OUT_M(b) : SWK_W_IN_PM(b));
+        else      asm volatile(SWK_F16M_P_Z0_L0 : SWK_W_OUT_M(b) : SWK_W_IN_PM(b));
+      } else {
+        if (last) asm volatile(SWK_F16M_L_Z0_L1 : SWK_W_OUT_M(b) : SWK_W_IN_LM(b));
+        else      asm volatile(SWK_F16M_L_Z0_L0 : SWK_W_OUT_M(b) : SWK_W_IN_LM(b));
+      }
+      if constexpr (!GOTOH) up = Xl[SWK_CLAMP(b + 7, K)];
+    }
+  }
+  (void)Db; (void)S1; (void)X; (void)DN; (void)IN;
+  upX_ = up;
+  best_ = best;
+}
+
 __device__ __forceinline__ uint32_t dpp_shr1(uint32_t lane0_value, uint32_t v) {
   return __builtin_amdgcn_update_dpp(lane0_value, v, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
 }
@@ -880,6 +970,7 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
   const f16x2 NOE2 = {fnoe, fnoe}, NE2 = {fne, fne};
   const u16x2 H0 = F16 ? (u16x2){0, 0} : S2;                          // H of row/col -1
   const u16x2 X0 = (F16 && !GOTOH) ? as_u16x2(NOE2) : (u16x2){0, 0};  // T/G/E/F of row/col -1
+  const uint32_t noe = as_u32(as_u16x2(NOE2)), ne = as_u32(as_u16x2(NE2));
 
   uint32_t lut[PROF ? 1 : K];
   if constexpr (!PROF) {
@@ -944,20 +1035,16 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
             lk.hi[4 * q + 3] = y.w;
           }
         }
-        if constexpr (GOTOH)
-          column_gotoh_f16<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
-        else if constexpr (COL0)
+        if constexpr (COL0)
           column_merged_f16_mask<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, z);
         else
-          column_merged_f16<K, 4, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+          column_f16_lane_asm<K, GOTOH>(lk, diag, upX, Hl, Xl, best, noe, ne);
       } else {
         const LaneLutLookup<K> lk{lut, nv, let};
-        if constexpr (GOTOH)
-          column_gotoh_f16<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
-        else if constexpr (COL0)
+        if constexpr (COL0)
           column_merged_f16_mask<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, z);
         else
-          column_merged_f16<K, 4, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+          column_f16_lane_asm<K, GOTOH>(lk, diag, upX, Hl, Xl, best, noe, ne);
       }
     } else if constexpr (PROF) {
       ProfLookupK<K> lk;
