@@ -31,7 +31,7 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                        const void* edge_in, void* edge_out, uint32_t ecols,
                                        int accum, int packed, const uint32_t* idx,
-                                       const uint32_t* nidx, hipStream_t st);
+                                       const uint32_t* nidx, uint32_t idx_base, hipStream_t st);
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
                                     uint32_t* idx, uint32_t* count, hipStream_t st);
 
@@ -528,7 +528,8 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   // re-scores the pairs above that threshold in u16 (SWBANK_F16_OPT=0 disables).
   const bool f16_ok = b->f16 && b->f16_neg >= -2048 && env_int("SWBANK_F16", 1) != 0;
   const bool exact16 = f16_ok && top <= 2048u;
-  const bool opt16 = f16_ok && !exact16 && env_int("SWBANK_F16_OPT", 1) != 0;
+  const bool opt16 = f16_ok && !exact16 && env_int("SWBANK_F16_OPT", 1) != 0 &&
+                     n <= 0xFFFFFFFFull;  // the re-score list holds 32-bit target numbers
   const bool use_f16 = exact16 || opt16;
   // Kernel choice by a throughput model calibrated on MI355X (scripts/kernel_choice.py):
   //  tile kernel: base rate x fraction of the 256 CUs holding a tile x f(waves per SIMD),
@@ -568,36 +569,61 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
     snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=%zu", arith,
              b->prof ? "-profile" : "", b->R, b->segs[0].W, nseg);
   }
-  if (nseg > 1 && (!use_wave || opt16)) {
-    const size_t words = std::max<size_t>(1, ntiles * ecols * 64);
-    HIPOK(b, b->edge[0].reserve(words));
-    HIPOK(b, b->edge[1].reserve(words));
+  // Segmented queries hand each segment's bottom row to the next through HBM: ntiles x ecols
+  // x 512 B per edge buffer.  Past SWBANK_EDGE_MB (default 2048) the batch runs as
+  // consecutive position ranges, each with its own edge rows.
+  size_t span = n;
+  if (nseg > 1) {
+    const size_t budget = (size_t)std::max(1, env_int("SWBANK_EDGE_MB", 2048)) << 20;
+    const size_t per_tile = (size_t)ecols * 64 * sizeof(uint2);
+    span = std::max<size_t>(1, budget / std::max<size_t>(per_tile, 1)) * SWB_TILE;
+    span = std::min(span, n);
+    if (!use_wave || opt16) {
+      const size_t words = std::max<size_t>(1, (span + SWB_TILE - 1) / SWB_TILE * ecols * 64);
+      HIPOK(b, b->edge[0].reserve(words));
+      HIPOK(b, b->edge[1].reserve(words));
+    }
   }
   // pass 0: every pair with the tile kernel (unless the wave kernel ran); pass 1 (optimistic
   // f16 only): the pairs scoring above 2048 - max(s), re-scored in u16 by the tile kernel
   for (int pass = use_wave ? 1 : 0; pass < (opt16 ? 2 : 1); ++pass) {
     const bool f16 = use_f16 && pass == 0;
-    const uint32_t* idx = nullptr;
-    const uint32_t* nidx = nullptr;
     if (pass == 1) {
       HIPOK(b, b->fb_idx.reserve(n));
       HIPOK(b, b->fb_cnt.reserve(1));
       HIPOK(b, swk_flag_high(d_scores, n, 2048 - std::max(0, b->smax), b->fb_idx.p, b->fb_cnt.p,
                              st));
-      idx = b->fb_idx.p;
-      nidx = b->fb_cnt.p;
     }
-    for (size_t s = 0; s < nseg; ++s) {
-      const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
-      void* eout = s + 1 < nseg ? b->edge[s & 1].p : nullptr;
-      HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof, gotoh ? 1 : 0, f16 ? 1 : 0, d_res,
-                                d_offs, d_lens, n,
-                                f16 ? b->qtab16.p + b->segs[s].off16
-                                    : b->qtab.p + b->segs[s].off,
-                                f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
-                                f16 && b->prof ? b->PS16 : b->PS, b->pad, b->segs[s].W,
-                                d_scores, ein, eout, ecols, s > 0 ? 1 : 0, packed ? 1 : 0, idx,
-                                nidx, st));
+    for (size_t p0 = 0; p0 < n; p0 += span) {
+      const size_t np = std::min(span, n - p0);
+      // pass 0 offsets the batch arrays; pass 1 keeps them whole (idx holds target numbers)
+      const uint8_t* res = d_res;
+      const uint64_t* offs = d_offs;
+      const uint32_t* lens = d_lens;
+      int32_t* scores = d_scores;
+      const uint32_t* idx = nullptr;
+      if (pass == 0 && packed) {
+        res = d_res + p0 * SWB_RECORD;
+        scores = d_scores + p0;
+      } else if (pass == 0) {
+        offs = d_offs + p0;
+        lens = d_lens + p0;
+        scores = d_scores + p0;
+      } else {
+        idx = b->fb_idx.p + p0;
+      }
+      for (size_t s = 0; s < nseg; ++s) {
+        const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
+        void* eout = s + 1 < nseg ? b->edge[s & 1].p : nullptr;
+        HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof, gotoh ? 1 : 0, f16 ? 1 : 0, res,
+                                  offs, lens, np,
+                                  f16 ? b->qtab16.p + b->segs[s].off16
+                                      : b->qtab.p + b->segs[s].off,
+                                  f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
+                                  f16 && b->prof ? b->PS16 : b->PS, b->pad, b->segs[s].W,
+                                  scores, ein, eout, ecols, s > 0 ? 1 : 0, packed ? 1 : 0, idx,
+                                  idx ? b->fb_cnt.p : nullptr, (uint32_t)p0, st));
+      }
     }
   }
   if (b->timing) {

@@ -437,7 +437,8 @@ struct ScoreArgs {
   // optional position -> target map: positions [0, *nidx) score targets idx[k] (scores are
   // written to scores[idx[k]]); used to re-score the pairs an optimistic f16 pass flagged
   const uint32_t* idx;
-  const uint32_t* nidx;
+  const uint32_t* nidx;   // with idx: positions [0, min(n, *nidx - idx_base)) are valid
+  uint32_t idx_base;
 };
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -492,7 +493,11 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   uint2* ring = ein + (seg_in ? 2 * C * 64 : 0);
   uint8_t* prof = reinterpret_cast<uint8_t*>(ring + (size_t)(W > 1 ? W - 1 : 0) * 2 * C * 64);
 
-  const size_t n = a.idx ? min(a.n, (size_t)__builtin_amdgcn_readfirstlane(*a.nidx)) : a.n;
+  size_t n = a.n;
+  if (a.idx) {
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(*a.nidx);
+    n = cnt > a.idx_base ? min(a.n, (size_t)(cnt - a.idx_base)) : 0;
+  }
   const int ntiles = (int)((n + SWB_TILE - 1) / SWB_TILE);
   const int G = (int)gridDim.x;
   int total = 0;  // chunks of all this workgroup's tiles: every wave runs total + W - 1 phases
@@ -1152,12 +1157,12 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                        const void* edge_in, void* edge_out, uint32_t ecols,
                                        int accum, int packed, const uint32_t* idx,
-                                       const uint32_t* nidx, hipStream_t st) {
+                                       const uint32_t* nidx, uint32_t idx_base, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                          O,    E,    PS,   pad, scores, static_cast<const uint2*>(edge_in),
                          static_cast<uint2*>(edge_out), ecols, (uint32_t)accum, (uint32_t)packed,
-                         idx, nidx};
+                         idx, nidx, idx_base};
   const uint32_t prof_bytes = (pad + 1) * PS;
 #define SWK_CASE(RR, BB, C0, PF, GT, FH)                                                      \
   if (R == RR && RB == BB && col0 == C0 && prof == PF && gotoh == GT && f16 == FH)            \
@@ -1201,7 +1206,7 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
                                       int packed, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
-                         nullptr, nullptr, 0u, 0u, (uint32_t)packed, nullptr, nullptr};
+                         nullptr, nullptr, 0u, 0u, (uint32_t)packed, nullptr, nullptr, 0u};
   const uint32_t prof_bytes = (pad + 1) * PS;
 #define SWK_WCASE(KK, C0, PF, GT)                                                         \
   if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                                 \

@@ -136,3 +136,27 @@ def test_optimistic_f16_rescore(alphabet, model, kernel_choice):
     assert bad.size == 0, (kern, [(int(i), int(got[i]), int(want[i])) for i in bad[:8]])
     if kernel_choice == "tile":
         assert kern.startswith("tile f16+u16-rescore"), kern
+
+
+def test_segmented_batch_in_position_ranges(monkeypatch):
+    """A small SWBANK_EDGE_MB splits a segmented batch into position ranges (each with its own
+    HBM edge rows), in both the f16 pass and the optimistic u16 re-score."""
+    monkeypatch.setenv("SWBANK_EDGE_MB", "1")
+    rng = np.random.default_rng(5)
+    q = rng.integers(0, 4, 1100, dtype=np.uint8)
+    seqs = []
+    for k in range(600):
+        if k % 3 == 0:
+            a = int(rng.integers(0, 400))
+            seqs.append(q[a:a + int(rng.integers(400, 700))].copy())
+        else:
+            seqs.append(rng.integers(0, 4, int(rng.integers(0, 700)), dtype=np.uint8))
+    with S.ScoreBank() as bank:
+        bank.set_penalties(5, -4, -10, -1)
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -10, -1)
+    assert want.max() > 2048
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:8]]
