@@ -140,6 +140,11 @@ sw_status sw_score_records_device(sw_bank *bank, const void *d_records, size_t n
  * score; *best_id = ids ? ids[index] : index. */
 sw_status sw_best_hit(sw_bank *bank, const int32_t *scores, const uint64_t *ids, size_t n,
                       uint64_t *best_id, int32_t *best_score);
+/* The same on device buffers, asynchronous on `stream`: d_out[0] = best id
+ * (d_ids ? d_ids[index] : index), d_out[1] = best score (int32 sign-extended to 64 bits).
+ * n <= 2^32. */
+sw_status sw_best_hit_device(sw_bank *bank, const int32_t *d_scores, const uint64_t *d_ids,
+                             size_t n, uint64_t *d_out, void *stream);
 
 /* ---- profiling (≙ the CAPI AFU's cycle counters, capi_sample_aligner/hdl-verliog/afu.v
  *      _DEBUGGING_ "calculation #N completed, runtime: C cycles") ------------------------- */

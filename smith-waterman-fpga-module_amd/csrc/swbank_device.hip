@@ -32,6 +32,8 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        const void* edge_in, void* edge_out, uint32_t ecols,
                                        int accum, int packed, const uint32_t* idx,
                                        const uint32_t* nidx, uint32_t idx_base, hipStream_t st);
+extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
+                                   unsigned long long* key, uint64_t* out, hipStream_t st);
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
                                     uint32_t* idx, uint32_t* count, hipStream_t st);
 
@@ -93,6 +95,7 @@ struct sw_bank {
   int32_t f16_neg = 0;     // most negative intermediate: -(o + 2e + |min s|)
   DevBuf<uint32_t> qtab16;
   DevBuf<uint32_t> fb_idx, fb_cnt;  // pairs an optimistic f16 pass re-scores in u16
+  DevBuf<unsigned long long> best_key;  // sw_best_hit_device scratch
   struct Seg { int W; size_t off, off16; };  // rows = W*R (last may be shorter); word offsets
                                               // in qtab and qtab16
   std::vector<Seg> segs;
@@ -198,6 +201,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->qtab16.release();
   b->fb_idx.release();
   b->fb_cnt.release();
+  b->best_key.release();
   b->wtab.release();
   b->wtab16.release();
   b->edge[0].release();
@@ -806,6 +810,18 @@ extern "C" sw_status sw_bank_timing(sw_bank* b, uint64_t* launches, double* pack
   if (pack_ms) *pack_ms = p;
   if (score_ms) *score_ms = s;
   return st;
+}
+
+extern "C" sw_status sw_best_hit_device(sw_bank* b, const int32_t* d_scores, const uint64_t* d_ids,
+                                        size_t n, uint64_t* d_out, void* stream) {
+  if (!b) return SW_ERR_ARG;
+  if (!d_scores || !d_out || n == 0 || n > 0xFFFFFFFFull)
+    return fail(b, SW_ERR_ARG, "sw_best_hit_device: empty, null or > 2^32 scores");
+  HIPOK(b, hipSetDevice(b->device));
+  HIPOK(b, b->best_key.reserve(1));
+  HIPOK(b, swk_best_hit(d_scores, d_ids, n, b->best_key.p, d_out,
+                        stream ? reinterpret_cast<hipStream_t>(stream) : b->stream));
+  return SW_OK;
 }
 
 extern "C" sw_status sw_best_hit(sw_bank* b, const int32_t* scores, const uint64_t* ids, size_t n,

@@ -1183,6 +1183,48 @@ __global__ void __launch_bounds__(256) flag_kernel(const int32_t* scores, size_t
 }
 }  // namespace swk
 
+namespace swk {
+// Bank best hit on the device (≙ ScoreBank_v2 max/vld_max): key = biased score << 32 |
+// (2^32 - 1 - index), so one 64-bit max picks the highest score and, among equals, the
+// lowest index.  Block-level max in LDS, one atomicMax per block.
+__global__ void __launch_bounds__(256) best_kernel(const int32_t* scores, size_t n,
+                                                   unsigned long long* key) {
+  __shared__ unsigned long long red[256];
+  unsigned long long m = 0;
+  for (size_t k = (size_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (size_t)gridDim.x * 256) {
+    const unsigned long long v = ((unsigned long long)((uint32_t)scores[k] ^ 0x80000000u) << 32) |
+                                 (0xFFFFFFFFull - (uint32_t)k);
+    m = v > m ? v : m;
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w && red[threadIdx.x + w] > red[threadIdx.x])
+      red[threadIdx.x] = red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicMax(key, red[0]);
+}
+__global__ void best_finalize(const unsigned long long* key, const uint64_t* ids, uint64_t* out) {
+  const unsigned long long v = *key;
+  const uint64_t idx = 0xFFFFFFFFull - (v & 0xFFFFFFFFull);
+  out[0] = ids ? ids[idx] : idx;
+  out[1] = (uint64_t)(int64_t)(int32_t)((uint32_t)(v >> 32) ^ 0x80000000u);
+}
+}  // namespace swk
+
+// out[0] = best id, out[1] = best score (sign-extended); key: 8 bytes of device scratch.
+extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
+                                   unsigned long long* key, uint64_t* out, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(key, 0, sizeof(*key), st);
+  if (e != hipSuccess) return e;
+  const size_t blocks = std::min<size_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(swk::best_kernel, dim3((unsigned)std::max<size_t>(blocks, 1)), dim3(256), 0,
+                     st, scores, n, key);
+  hipLaunchKernelGGL(swk::best_finalize, dim3(1), dim3(1), 0, st, key, ids, out);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
                                     uint32_t* idx, uint32_t* count, hipStream_t st) {
   hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), st);

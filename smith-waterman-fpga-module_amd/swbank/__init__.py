@@ -40,6 +40,7 @@ EXPORTS = (
     "sw_score_batch_device", "sw_best_hit", "sw_encode_ascii", "sw_pack_2bit",
     "sw_unpack_2bit", "sw_fill_matrix", "sw_bank_set_timing", "sw_bank_timing",
     "sw_last_kernel", "sw_load_query_record", "sw_score_records", "sw_score_records_device",
+    "sw_best_hit_device",
 )
 RECORD_BYTES, RECORD_MAX_BASES = 64, 232
 
@@ -103,6 +104,7 @@ def lib() -> ctypes.CDLL:
         "sw_load_query_record": (i32, [P, P]),
         "sw_score_records": (i32, [P, P, sz, P]),
         "sw_score_records_device": (i32, [P, P, sz, P, P]),
+        "sw_best_hit_device": (i32, [P, P, P, sz, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -299,6 +301,12 @@ class ScoreBank:
         self._check(lib().sw_best_hit(self._h, _p(s), _p(ida) if ida is not None else None,
                                       len(s), ctypes.byref(bid), ctypes.byref(bsc)))
         return int(bid.value), int(bsc.value)
+
+    def best_hit_device(self, d_scores: int, n: int, d_out: int, d_ids: int = 0,
+                        stream: int = 0):
+        """Device best hit: d_out (2 x uint64) <- (best id, best score); async on `stream`."""
+        self._check(lib().sw_best_hit_device(self._h, d_scores, d_ids or None, n, d_out,
+                                             stream or None))
 
     # profiling
     def set_timing(self, enable: bool = True):

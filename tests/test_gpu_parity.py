@@ -440,3 +440,30 @@ def test_capi_records_path(bank, kernel_choice):
     bad[0, 4:6] = np.frombuffer(np.uint16(233).tobytes(), np.uint8)
     with pytest.raises(S.SwbankError):
         bank.score_records(bad)
+
+
+def test_best_hit_device(bank):
+    """Row f1 on the device: highest score, lowest index among ties, optional 64-bit IDs."""
+    import torch
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(3)
+    for n in (1, 7, 256, 1000, 300001):
+        sc = rng.integers(-5, 2000, n).astype(np.int32)
+        if n > 10:
+            sc[n // 3] = sc[2 * n // 3] = sc.max() + 1  # a tie: the lower index wins
+        ids = rng.integers(0, 2**63, n, dtype=np.uint64)
+        d_sc = torch.from_numpy(sc).to(dev)
+        d_ids = torch.from_numpy(ids.view(np.int64)).to(dev)
+        d_out = torch.zeros(2, dtype=torch.int64, device=dev)
+        stream = torch.cuda.current_stream().cuda_stream
+        bank.best_hit_device(d_sc.data_ptr(), n, d_out.data_ptr(), stream=stream)
+        torch.cuda.synchronize()
+        bi = int(np.argmax(sc))
+        assert d_out.cpu().numpy().tolist() == [bi, int(sc[bi])]
+        assert bank.best_hit(sc) == (bi, int(sc[bi]))
+        bank.best_hit_device(d_sc.data_ptr(), n, d_out.data_ptr(), d_ids=d_ids.data_ptr(),
+                             stream=stream)
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy().view(np.uint64)
+        assert int(out[0]) == int(ids[bi]) and int(out[1]) == int(sc[bi])
