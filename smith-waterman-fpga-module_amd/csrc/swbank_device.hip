@@ -291,7 +291,17 @@ static sw_status prepare(sw_bank* b) {
   const int sN = m[4];
   for (int i = 0; lut && i < A; ++i) lut = m[i * A + 4] == sN;
   lut = lut && sN <= 0;
-  const int prof = (env_int("SWBANK_PROFILE", 0) || !lut) ? 1 : 0;
+  // The f16 LUT holds one byte per entry (the f16 high byte): only scores whose f16 low byte
+  // is 0 (|s| <= 8, or coarser even values) qualify.  Other DNA matrices run in profile mode
+  // (2-byte f16 entries) when f16 applies at all: faster than the u16 LUT kernel.
+  bool lut_f16 = true;
+  for (int i = 0; i < A * A; ++i) {
+    const uint16_t bits = __builtin_bit_cast(uint16_t, (_Float16)(float)m[i]);
+    lut_f16 = lut_f16 && (bits & 0xFFu) == 0;
+  }
+  const bool f16_range = -(o + 2 * e + (std::max(0, smax) - smin)) >= -2048;
+  const int prof =
+      (env_int("SWBANK_PROFILE", 0) || !lut || (!lut_f16 && f16_range)) ? 1 : 0;
 
   const int qlen = (int)b->query.size();
   // the HDL column-0 rule differs from the plain recurrence only if a match pays for a gap

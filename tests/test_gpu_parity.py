@@ -130,10 +130,10 @@ def test_edge_shapes(bank):
 @pytest.mark.parametrize("qlen", [200, 407, 408, 409, 410, 512])
 @pytest.mark.parametrize("match", [5, 8, 9, 16])
 def test_f16_bound_edges(bank, qlen, match, kernel_choice):
-    """Scores at and past the f16 kernel's exact range: the host takes the f16 tile kernel
-    only while min(|q|, max|t|) * max(s) + max(s) <= 2048 and every substitution score is an
-    f16 with a zero low byte (match 9 is not: u16 kernel); perfect and near-perfect matches
-    put the optimum right at the bound."""
+    """Scores at and past the f16 kernel's exact range (exact f16 while min(|q|, max|t|) *
+    max(s) + max(s) <= 2048, optimistic f16 + u16 re-score past it); match 9 has a non-zero
+    f16 low byte, so it runs on the 2-byte profile; perfect and near-perfect matches put the
+    optimum right at the bound."""
     rng = np.random.default_rng(qlen * 7 + match)
     q = rng.integers(0, 4, qlen, dtype=np.uint8)
     near = q.copy()
@@ -150,9 +150,10 @@ def test_f16_bound_edges(bank, qlen, match, kernel_choice):
     assert got[0] == match * qlen
     if kernel_choice == "tile":
         # exact f16 within the bound; past it optimistic f16 with a u16 re-score of the pairs
-        # above 2048 - max(s); a score with a non-zero f16 low byte (9) cannot use the LUT
-        want_k = ("tile u16 " if match == 9 else "tile f16 " if qlen * match + match <= 2048
-                  else "tile f16+u16-rescore ")
+        # above 2048 - max(s); a score with a non-zero f16 low byte (9) cannot use the
+        # one-byte LUT and runs on the 2-byte f16 profile instead
+        want_k = ("tile f16" + ("" if qlen * match + match <= 2048 else "+u16-rescore") +
+                  ("-profile " if match == 9 else " "))
         assert bank.last_kernel().startswith(want_k), bank.last_kernel()
     elif kernel_choice == "tile-u16":
         assert bank.last_kernel().startswith("tile u16")
