@@ -178,6 +178,9 @@ __device__ __forceinline__ void column_gotoh_f16(const LK& lk, u16x2& diag_, u16
 #ifndef SWK_F16_ASM
 #define SWK_F16_ASM 1
 #endif
+#ifndef SWK_F16_COLBLOCK
+#define SWK_F16_COLBLOCK 1
+#endif
 #include "swbank_f16_rows.inc"
 #define SWK_F16_HT(B)                                                                         \
   [h0] "+v"(Hl[B]), [h1] "+v"(Hl[B + 1]), [h2] "+v"(Hl[B + 2]), [h3] "+v"(Hl[B + 3]),          \
@@ -222,6 +225,22 @@ __device__ __forceinline__ void column_f16_asm(const LK& lk, u16x2& diag_, u16x2
   constexpr bool PROF = !std::is_same<LK, LutLookup<R>>::value;
   uint32_t Da, Db, S1, X, DN, IN;
   u16x2 best = best_, up = upX_;
+#if SWK_F16_COLBLOCK
+  if constexpr (R == 32 && !GOTOH && !PROF && !ZDOWN) {
+    // the headline variant: the whole column (prologue + 32 rows) as one asm block
+    asm volatile(
+        "v_perm_b32 %[Da], %[nv], %[tz], %[sel]\n\t"
+        "v_pk_add_f16 %[Da], %[dg], %[Da]\n\t" SWK_F16M_L_Z0_COL32
+        : SWK_F16_COL32_HT, [Da] "=&v"(Da), [Db] "=&v"(Db), [S1] "=&v"(S1), [X] "=&v"(X),
+          [DN] "=&v"(DN), [IN] "=&v"(IN), [best] "+v"(best)
+        : [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up),
+          [tz] "s"(lk.tab[0]), [dg] "v"(diag_), SWK_F16_COL32_TB);
+    (void)Db; (void)S1; (void)X; (void)DN; (void)IN;
+    upX_ = Xl[R - 1];
+    best_ = best;
+    return;
+  }
+#endif
   if constexpr (PROF)
     asm volatile(
         "v_perm_b32 %[Da], %[h0], %[l0], %[sA]\n\t"
