@@ -63,6 +63,27 @@ struct DevBuf {
     cap = 0;
   }
 };
+
+// Pinned host staging for the query tables (so their uploads are truly asynchronous).
+struct PinBuf {
+  uint8_t* p = nullptr;
+  size_t cap = 0;  // bytes
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(n, 4096);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
 }  // namespace
 
 struct sw_bank {
@@ -114,6 +135,13 @@ struct sw_bank {
   DevBuf<int32_t> scores;
 
   char last_kernel[96] = {0};
+
+  // Query tables are rewritten in place by prepare() while earlier launches may still read
+  // them on the caller's stream: the upload (on the bank stream) waits for ev_used (recorded
+  // after every launch), and every launch waits for ev_ready (recorded after the upload).
+  // Nothing blocks the host except reusing the pinned staging of a copy still in flight.
+  hipEvent_t ev_ready = nullptr, ev_used = nullptr;
+  PinBuf stage;
 
   // profiling
   bool timing = false;
@@ -199,6 +227,9 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   (void)sw_bank_timing(b, &nl, &pm, &sm);
   b->qtab.release();
   b->qtab16.release();
+  b->stage.release();
+  if (b->ev_ready) (void)hipEventDestroy(b->ev_ready);
+  if (b->ev_used) (void)hipEventDestroy(b->ev_used);
   b->fb_idx.release();
   b->fb_cnt.release();
   b->best_key.release();
@@ -460,28 +491,35 @@ static sw_status prepare(sw_bank* b) {
     }
   }
   HIPOK(b, hipSetDevice(b->device));
-  if (!wt16.empty()) {
-    HIPOK(b, b->wtab16.reserve(wt16.size()));
-    HIPOK(b, hipMemcpyAsync(b->wtab16.p, wt16.data(), wt16.size() * 4, hipMemcpyHostToDevice,
-                            b->stream));
+  if (!b->ev_ready) {
+    HIPOK(b, hipEventCreateWithFlags(&b->ev_ready, hipEventDisableTiming));
+    HIPOK(b, hipEventCreateWithFlags(&b->ev_used, hipEventDisableTiming));
+    HIPOK(b, hipEventRecord(b->ev_ready, b->stream));
+    HIPOK(b, hipEventRecord(b->ev_used, b->stream));
   }
+  // the previous upload must have left the staging buffer before it is refilled
+  HIPOK(b, hipEventSynchronize(b->ev_ready));
+  const size_t nbytes = (wt16.size() + wt.size() + tab.size() + tab16.size()) * 4;
+  HIPOK(b, b->stage.reserve(nbytes));
+  // earlier launches (any stream) must be done reading the tables this upload overwrites
+  HIPOK(b, hipStreamWaitEvent(b->stream, b->ev_used, 0));
+  size_t at = 0;
+  auto upload = [&](DevBuf<uint32_t>& dst, const std::vector<uint32_t>& src) -> hipError_t {
+    hipError_t e = dst.reserve(src.size());
+    if (e != hipSuccess || src.empty()) return e;
+    std::memcpy(b->stage.p + at, src.data(), src.size() * 4);
+    e = hipMemcpyAsync(dst.p, b->stage.p + at, src.size() * 4, hipMemcpyHostToDevice, b->stream);
+    at += src.size() * 4;
+    return e;
+  };
+  if (!wt16.empty()) HIPOK(b, upload(b->wtab16, wt16));
   b->wPS16 = wPS16;
-  if (wK) {
-    HIPOK(b, b->wtab.reserve(wt.size()));
-    HIPOK(b, hipMemcpyAsync(b->wtab.p, wt.data(), wt.size() * 4, hipMemcpyHostToDevice,
-                            b->stream));
-  }
+  if (wK) HIPOK(b, upload(b->wtab, wt));
   b->wK = wK;
   b->wPS = wPS;
-  HIPOK(b, b->qtab.reserve(tab.size()));
-  HIPOK(b, hipMemcpyAsync(b->qtab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice,
-                          b->stream));
-  if (f16) {
-    HIPOK(b, b->qtab16.reserve(tab16.size()));
-    HIPOK(b, hipMemcpyAsync(b->qtab16.p, tab16.data(), tab16.size() * 4, hipMemcpyHostToDevice,
-                            b->stream));
-  }
-  HIPOK(b, hipStreamSynchronize(b->stream));
+  HIPOK(b, upload(b->qtab, tab));
+  if (f16) HIPOK(b, upload(b->qtab16, tab16));
+  HIPOK(b, hipEventRecord(b->ev_ready, b->stream));
   b->f16 = f16;
   b->nv16 = (uint32_t)hN * 0x01010101u;
   b->PS16 = PS16;
@@ -527,6 +565,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   // no separate feeder kernel: the score kernel streams the codes itself, so the "pack"
   // interval (a..b) is empty and kept only for ABI stability
   if (b->timing) HIPOK(b, hipEventRecord(ev.b, st));
+  HIPOK(b, hipStreamWaitEvent(st, b->ev_ready, 0));  // the query tables are uploaded
   const size_t nseg = b->segs.size();
   const uint32_t ecols = (max_len + 7) / 8 * 8;
   const size_t ntiles = (n + SWB_TILE - 1) / SWB_TILE;
@@ -640,6 +679,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
       }
     }
   }
+  HIPOK(b, hipEventRecord(b->ev_used, st));  // the next table upload waits for this
   if (b->timing) {
     HIPOK(b, hipEventRecord(ev.c, st));
     b->events.push_back(ev);

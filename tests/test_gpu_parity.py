@@ -468,3 +468,40 @@ def test_best_hit_device(bank):
         torch.cuda.synchronize()
         out = d_out.cpu().numpy().view(np.uint64)
         assert int(out[0]) == int(ids[bi]) and int(out[1]) == int(sc[bi])
+
+
+def test_back_to_back_queries_on_a_user_stream():
+    """ld_sequence between asynchronous device batches on the caller's own stream: the new
+    query's tables are uploaded only after the previous launch has read the old ones, and the
+    next launch waits for the upload (no host synchronisation in between)."""
+    import torch
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(21)
+    n, L = 20000, 200
+    tg = rng.integers(0, 4, (n, L), dtype=np.uint8)
+    queries = [rng.integers(0, 4, int(rng.integers(100, 700)), dtype=np.uint8) for _ in range(6)]
+    for k in range(0, n, 97):  # homologs of the queries
+        qq = queries[k % 6]
+        a = int(rng.integers(0, max(1, len(qq) - L)))
+        tg[k, :len(qq[a:a + L])] = qq[a:a + L]
+    d_res = torch.from_numpy(tg.reshape(-1)).to(dev)
+    d_offs = torch.arange(n, dtype=torch.int64, device=dev) * L
+    d_lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+    d_sc = torch.zeros((len(queries), n), dtype=torch.int32, device=dev)
+    user = torch.cuda.Stream()
+    with S.ScoreBank() as bank:
+        bank.set_penalties(5, -4, -12, -4)
+        for rep in range(2):
+            for k, qq in enumerate(queries):
+                bank.load_query(qq)
+                bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(),
+                                        n, L, d_sc[k].data_ptr(), user.cuda_stream)
+        user.synchronize()
+    got = d_sc.cpu().numpy()
+    idx = np.arange(0, n, 7)
+    offs = (idx * L).astype(np.uint64)
+    for k, qq in enumerate(queries):
+        want = O.score_batch(qq, tg.reshape(-1), offs, np.full(len(idx), L, np.uint32),
+                             O.dna_matrix(), -12, -4)
+        assert (got[k][idx] == want).all(), k
