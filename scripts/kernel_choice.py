@@ -22,6 +22,7 @@ CASES = [  # (alphabet, model, qlen, L, ntargets)
     ("protein", "merged", 512, 1000, 25000), ("protein", "gotoh", 1024, 1000, 12500),
     ("protein", "gotoh", 128, 150, 524288), ("protein", "merged", 128, 150, 524288),
     ("dna", "gotoh", 256, 150, 524288),
+    ("dna", "merged", 4000, 1000, 2000), ("protein", "gotoh", 3000, 500, 5000),
 ]
 
 

@@ -19,7 +19,8 @@
 
 extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh, int f16);
 extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int f16,
-                                      const uint8_t* res,
+                                      const void* edge_in, void* edge_out, uint32_t ecols,
+                                      int accum, const uint8_t* res,
                                       const uint64_t* offs, const uint32_t* lens, size_t n,
                                       const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
@@ -122,7 +123,9 @@ struct sw_bank {
   std::vector<Seg> segs;
   DevBuf<uint2> edge[2];  // bottom rows handed from segment to segment
   // wave kernel (few targets, query <= 1024 rows): lane l owns rows [lK, lK+K)
-  int wK = 0;              // 0: query too long for the wave kernel
+  int wK = 0;              // rows per lane: 4, 8 or 16 (16 with several segments)
+  int wsegs = 1;           // 1024-row segments of the wave kernel
+  size_t wseg_words = 0, wseg_words16 = 0;  // table words per segment (u16, f16)
   uint32_t wPS = 0;
   DevBuf<uint32_t> wtab;   // LUT: 64K row words | PROF: (A+1) x 64K profile bytes
   DevBuf<uint32_t> wtab16; // the same in f16 (LUT: high bytes | PROF: 2-byte entries)
@@ -443,51 +446,55 @@ static sw_status prepare(sw_bank* b) {
       std::memcpy(tab16.data() + sg.off16, qp.data(), qp.size() * 2);
     }
   }
-  // wave-kernel layout of the same query (rows padded to 64K)
-  std::vector<uint32_t> wt;
-  int wK = qlen <= 256 ? 4 : qlen <= 512 ? 8 : qlen <= 1024 ? 16 : 0;
-  uint32_t wPS = 0;
-  if (wK) {
-    const int rows = 64 * wK;
+  // wave-kernel layout of the same query: rows padded to 64K; queries past 1024 rows run as
+  // 1024-row segments (K = 16), one table per segment, concatenated
+  std::vector<uint32_t> wt, wt16;
+  const int wK = qlen <= 256 ? 4 : qlen <= 512 ? 8 : 16;
+  const int wrows = 64 * wK;
+  const int wsegs = std::max(1, (qlen + wrows - 1) / wrows);
+  const uint32_t wPS = prof ? (uint32_t)wrows : 0, wPS16 = prof ? (uint32_t)wrows * 2 : 0;
+  for (int sg = 0; sg < wsegs; ++sg) {
+    const int r0 = sg * wrows, nr = std::min(wrows, std::max(0, qlen - r0));
     if (!prof) {
-      wt.assign((size_t)rows, 0xFFFFFFFFu);
-      for (int i = 0; i < qlen; ++i) {
+      const size_t base = wt.size();
+      wt.resize(base + wrows, 0xFFFFFFFFu);
+      for (int i = 0; i < nr; ++i) {
         uint32_t w = 0;
-        for (int c = 0; c < 4; ++c) w |= (uint32_t)(uint8_t)(S - m[b->query[i] * A + c]) << (8 * c);
-        wt[i] = w;
+        for (int c = 0; c < 4; ++c)
+          w |= (uint32_t)(uint8_t)(S - m[b->query[r0 + i] * A + c]) << (8 * c);
+        wt[base + i] = w;
+      }
+      if (f16) {
+        const size_t b16 = wt16.size();
+        wt16.resize(b16 + wrows, 0xE8E8E8E8u);  // rows past the query: -2048
+        for (int i = 0; i < nr; ++i) {
+          uint32_t w = 0;
+          for (int c = 0; c < 4; ++c) {
+            uint8_t h;
+            f16_hi(m[b->query[r0 + i] * A + c], &h);
+            w |= (uint32_t)h << (8 * c);
+          }
+          wt16[b16 + i] = w;
+        }
       }
     } else {
-      wPS = (uint32_t)rows;
       std::vector<uint8_t> qp((size_t)(A + 1) * wPS, 0xFF);
       for (int c = 0; c < A; ++c)
-        for (int i = 0; i < qlen; ++i) qp[(size_t)c * wPS + i] = (uint8_t)(S - m[b->query[i] * A + c]);
-      wt.resize(qp.size() / 4);
-      std::memcpy(wt.data(), qp.data(), qp.size());
-    }
-  }
-  std::vector<uint32_t> wt16;
-  uint32_t wPS16 = 0;
-  if (wK && f16) {
-    const int rows = 64 * wK;
-    if (!prof) {
-      wt16.assign((size_t)rows, 0xE8E8E8E8u);  // rows past the query: -2048
-      for (int i = 0; i < qlen; ++i) {
-        uint32_t w = 0;
-        for (int c = 0; c < 4; ++c) {
-          uint8_t h;
-          f16_hi(m[b->query[i] * A + c], &h);
-          w |= (uint32_t)h << (8 * c);
-        }
-        wt16[i] = w;
+        for (int i = 0; i < nr; ++i)
+          qp[(size_t)c * wPS + i] = (uint8_t)(S - m[b->query[r0 + i] * A + c]);
+      const size_t base = wt.size();
+      wt.resize(base + qp.size() / 4);
+      std::memcpy(wt.data() + base, qp.data(), qp.size());
+      if (f16) {
+        std::vector<uint16_t> q16((size_t)(A + 1) * wrows, 0xE800u);
+        for (int c = 0; c < A; ++c)
+          for (int i = 0; i < nr; ++i)
+            q16[(size_t)c * wrows + i] =
+                __builtin_bit_cast(uint16_t, (_Float16)(float)m[b->query[r0 + i] * A + c]);
+        const size_t b16 = wt16.size();
+        wt16.resize(b16 + q16.size() / 2);
+        std::memcpy(wt16.data() + b16, q16.data(), q16.size() * 2);
       }
-    } else {
-      wPS16 = (uint32_t)rows * 2;
-      std::vector<uint16_t> qp((size_t)(A + 1) * rows, 0xE800u);
-      for (int c = 0; c < A; ++c)
-        for (int i = 0; i < qlen; ++i)
-          qp[(size_t)c * rows + i] = __builtin_bit_cast(uint16_t, (_Float16)(float)m[b->query[i] * A + c]);
-      wt16.resize(qp.size() / 2);
-      std::memcpy(wt16.data(), qp.data(), qp.size() * 2);
     }
   }
   HIPOK(b, hipSetDevice(b->device));
@@ -513,10 +520,13 @@ static sw_status prepare(sw_bank* b) {
     return e;
   };
   if (!wt16.empty()) HIPOK(b, upload(b->wtab16, wt16));
+  HIPOK(b, upload(b->wtab, wt));
   b->wPS16 = wPS16;
-  if (wK) HIPOK(b, upload(b->wtab, wt));
   b->wK = wK;
   b->wPS = wPS;
+  b->wsegs = wsegs;
+  b->wseg_words = wt.size() / wsegs;
+  b->wseg_words16 = wt16.empty() ? 0 : wt16.size() / wsegs;
   HIPOK(b, upload(b->qtab, tab));
   if (f16) HIPOK(b, upload(b->qtab16, tab16));
   HIPOK(b, hipEventRecord(b->ev_ready, b->stream));
@@ -601,9 +611,10 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                           (nseg > 1 ? 0.85 : 1.0);
   double wave_est = 0;
   if (b->wK > 0) {
-    const double rowfill = (double)b->query.size() / (64.0 * b->wK);
+    const double rowfill = (double)b->query.size() / (64.0 * b->wK * b->wsegs);
     const double colfill = max_len / (max_len + 63.0);
-    wave_est = (use_f16 ? (gotoh ? 6600 : 7600) : (gotoh ? 5000 : 6500)) * rowfill * colfill;
+    wave_est = (use_f16 ? (gotoh ? 6600 : 7600) : (gotoh ? 5000 : 6500)) * rowfill * colfill *
+               (b->wsegs > 1 ? 0.9 : 1.0);
   }
   const char* kforce = std::getenv("SWBANK_KERNEL");
   bool use_wave = b->wK > 0 && wave_est > tile_est;
@@ -611,13 +622,33 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   if (kforce && std::strcmp(kforce, "wave") == 0 && b->wK > 0) use_wave = true;
   const char* arith = opt16 ? "f16+u16-rescore" : use_f16 ? "f16" : "u16";
   if (use_wave) {
-    snprintf(b->last_kernel, sizeof(b->last_kernel), "wave %s%s K=%d", arith,
-             b->prof ? "-profile" : "", b->wK);
-    HIPOK(b, swk_launch_wave(b->wK, b->col0, b->prof, gotoh ? 1 : 0, use_f16 ? 1 : 0, d_res,
-                             d_offs, d_lens, n, use_f16 ? b->wtab16.p : b->wtab.p,
-                             use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
-                             use_f16 && b->prof ? b->wPS16 : b->wPS, b->pad, d_scores,
-                             packed ? 1 : 0, st));
+    snprintf(b->last_kernel, sizeof(b->last_kernel), "wave %s%s K=%d segs=%d", arith,
+             b->prof ? "-profile" : "", b->wK, b->wsegs);
+    // segments hand the bottom row on through HBM: pairs x ecols x 8 B per edge buffer,
+    // in position ranges under SWBANK_EDGE_MB like the tile kernel
+    size_t wspan = n;
+    if (b->wsegs > 1) {
+      const size_t budget = (size_t)std::max(1, env_int("SWBANK_EDGE_MB", 2048)) << 20;
+      wspan = std::min(n, std::max<size_t>(1, budget / ((size_t)ecols * sizeof(uint2))) * 2);
+      const size_t words = std::max<size_t>(1, (wspan + 1) / 2 * ecols);
+      HIPOK(b, b->edge[0].reserve(words));
+      HIPOK(b, b->edge[1].reserve(words));
+    }
+    for (size_t p0 = 0; p0 < n; p0 += wspan) {
+      const size_t np = std::min(wspan, n - p0);
+      for (int sg = 0; sg < b->wsegs; ++sg) {
+        const void* ein = sg > 0 ? b->edge[(sg - 1) & 1].p : nullptr;
+        void* eout = sg + 1 < b->wsegs ? b->edge[sg & 1].p : nullptr;
+        HIPOK(b, swk_launch_wave(
+                     b->wK, b->col0, b->prof, gotoh ? 1 : 0, use_f16 ? 1 : 0, ein, eout, ecols,
+                     sg > 0 ? 1 : 0, packed ? d_res + p0 * SWB_RECORD : d_res,
+                     packed ? d_offs : d_offs + p0, packed ? d_lens : d_lens + p0, np,
+                     use_f16 ? b->wtab16.p + sg * b->wseg_words16 : b->wtab.p + sg * b->wseg_words,
+                     use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
+                     use_f16 && b->prof ? b->wPS16 : b->wPS, b->pad, d_scores + p0,
+                     packed ? 1 : 0, st));
+      }
+    }
   } else {
     snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=%zu", arith,
              b->prof ? "-profile" : "", b->R, b->segs[0].W, nseg);

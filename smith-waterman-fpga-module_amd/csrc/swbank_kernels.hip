@@ -1014,6 +1014,13 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
   u16x2 best = {0, 0};
   u16x2 prevUpH = H0;
   uint32_t botH = as_u32(H0), botX = as_u32(X0), let = padsel, buf = padsel;
+  // query segments (queries longer than 64K rows): lane 0 reads row -1 of this segment (the
+  // previous segment's bottom row) from edge_in, lane 63 writes this segment's bottom row;
+  // layout [pair][column] {H, G/T/F} of both targets
+  const bool seg_in = a.edge_in != nullptr, seg_out = a.edge_out != nullptr;
+  const uint2* ein = seg_in ? a.edge_in + pair * a.ecols : nullptr;
+  uint2* eout = seg_out ? a.edge_out + pair * a.ecols : nullptr;
+  uint2 ebuf = make_uint2(as_u32(H0), as_u32(X0));
 
   const int nsteps = Lmax + 63;
   for (int t = 0; t < nsteps; ++t) {
@@ -1029,10 +1036,16 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
       }
       buf = F16 && !PROF ? ((min(x, pad) << 8) | (min(y, pad) << 24) | 0x000C000Cu)
                          : (min(x, pad) | (min(y, pad) << 16) | 0x0C000C00u);
+      if (seg_in) ebuf = c < (uint32_t)Lmax ? ein[c] : make_uint2(as_u32(H0), as_u32(X0));
     }
     const uint32_t inj = __builtin_amdgcn_readlane(buf, t & 63);
-    const u16x2 upH = as_u16x2(dpp_shr1(as_u32(H0), botH));
-    u16x2 upX = as_u16x2(dpp_shr1(as_u32(X0), botX));
+    uint32_t bH = as_u32(H0), bX = as_u32(X0);
+    if (seg_in) {
+      bH = __builtin_amdgcn_readlane(ebuf.x, t & 63);
+      bX = __builtin_amdgcn_readlane(ebuf.y, t & 63);
+    }
+    const u16x2 upH = as_u16x2(dpp_shr1(bH, botH));
+    u16x2 upX = as_u16x2(dpp_shr1(bX, botX));
     let = dpp_shr1(inj, let);
     u16x2 diag = prevUpH;
     prevUpH = upH;
@@ -1110,6 +1123,7 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
     asm volatile("" : "+v"(best));
     botH = as_u32(Hl[K - 1]);
     botX = as_u32(upX);
+    if (seg_out && lane == 63 && t >= 63 && t - 63 < Lmax) eout[t - 63] = make_uint2(botH, botX);
   }
   // max over the wave's rows, per target (f16: non-negative integers -> int)
   uint32_t bx = best.x, by = best.y;
@@ -1123,8 +1137,13 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
     by = max(by, (uint32_t)__shfl_xor((int)by, off));
   }
   if (lane == 0) {
-    a.scores[tA] = (int32_t)bx;
-    if (tB < n) a.scores[tB] = (int32_t)by;
+    int32_t sa = (int32_t)bx, sb = (int32_t)by;
+    if (a.accum) {  // best over the previous query segments
+      sa = max(sa, a.scores[tA]);
+      if (tB < n) sb = max(sb, a.scores[tB]);
+    }
+    a.scores[tA] = sa;
+    if (tB < n) a.scores[tB] = sb;
   }
 }
 
@@ -1260,14 +1279,16 @@ extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thr
   X(16, 0, 0, 0) X(16, 1, 0, 0) X(16, 0, 0, 1) X(16, 0, 1, 0) X(16, 1, 1, 0) X(16, 0, 1, 1)
 
 extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int f16,
-                                      const uint8_t* res,
+                                      const void* edge_in, void* edge_out, uint32_t ecols,
+                                      int accum, const uint8_t* res,
                                       const uint64_t* offs, const uint32_t* lens, size_t n,
                                       const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
                                       int packed, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
-                         nullptr, nullptr, 0u, 0u, (uint32_t)packed, nullptr, nullptr, 0u};
+                         static_cast<const uint2*>(edge_in), static_cast<uint2*>(edge_out), ecols,
+                         (uint32_t)accum, (uint32_t)packed, nullptr, nullptr, 0u};
   const uint32_t prof_bytes = (pad + 1) * PS;
 #define SWK_WCASE(KK, C0, PF, GT)                                                         \
   if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                                 \

@@ -136,6 +136,9 @@ def test_optimistic_f16_rescore(alphabet, model, kernel_choice):
     assert bad.size == 0, (kern, [(int(i), int(got[i]), int(want[i])) for i in bad[:8]])
     if kernel_choice == "tile":
         assert kern.startswith("tile f16+u16-rescore"), kern
+    elif kernel_choice == "wave":  # past 1024 rows the wave kernel runs 1024-row segments
+        assert kern.startswith("wave f16+u16-rescore"), kern
+        assert kern.endswith(f"segs={(qlen + 1023) // 1024}"), kern
 
 
 def test_segmented_batch_in_position_ranges(monkeypatch):
