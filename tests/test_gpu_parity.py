@@ -20,8 +20,8 @@ def kernel_choice(request, monkeypatch):
     """Run every parity test through each score kernel: the tile kernel (waves = row blocks,
     lanes = targets) and the wave kernel (lanes = rows, DPP hand-off), each with its f16
     arithmetic where eligible ("tile", "wave": exact below the f16 bound, optimistic with a
-    u16 re-score above it) and forced to u16 ("-u16").  The wave kernel takes queries up to
-    1024 rows; longer ones fall back to the tile kernel."""
+    u16 re-score above it) and forced to u16 ("-u16").  Past 1024 rows the wave kernel runs
+    the query as 1024-row segments."""
     kern = request.param.split("-")[0]
     monkeypatch.setenv("SWBANK_KERNEL", kern)
     monkeypatch.setenv("SWBANK_F16", "0" if request.param.endswith("-u16") else "1")
