@@ -226,15 +226,19 @@ __device__ __forceinline__ void column_f16_asm(const LK& lk, u16x2& diag_, u16x2
   uint32_t Da, Db, S1, X, DN, IN;
   u16x2 best = best_, up = upX_;
 #if SWK_F16_COLBLOCK
-  if constexpr (R == 32 && !GOTOH && !PROF && !ZDOWN) {
-    // the headline variant: the whole column (prologue + 32 rows) as one asm block
-    asm volatile(
-        "v_perm_b32 %[Da], %[nv], %[tz], %[sel]\n\t"
-        "v_pk_add_f16 %[Da], %[dg], %[Da]\n\t" SWK_F16M_L_Z0_COL32
-        : SWK_F16_COL32_HT, [Da] "=&v"(Da), [Db] "=&v"(Db), [S1] "=&v"(S1), [X] "=&v"(X),
-          [DN] "=&v"(DN), [IN] "=&v"(IN), [best] "+v"(best)
-        : [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up),
-          [tz] "s"(lk.tab[0]), [dg] "v"(diag_), SWK_F16_COL32_TB);
+  if constexpr ((R == 32 || R == 16) && !GOTOH && !PROF && !ZDOWN) {
+    // DNA LUT merged (the headline): the whole column (prologue + R rows) as one asm block
+#define SWK_F16_COLASM(RR)                                                                    \
+    asm volatile(                                                                             \
+        "v_perm_b32 %[Da], %[nv], %[tz], %[sel]\n\t"                                          \
+        "v_pk_add_f16 %[Da], %[dg], %[Da]\n\t" SWK_F16M_L_Z0_COL##RR                          \
+        : SWK_F16_COL##RR##_HT, [Da] "=&v"(Da), [Db] "=&v"(Db), [S1] "=&v"(S1), [X] "=&v"(X), \
+          [DN] "=&v"(DN), [IN] "=&v"(IN), [best] "+v"(best)                                  \
+        : [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up),     \
+          [tz] "s"(lk.tab[0]), [dg] "v"(diag_), SWK_F16_COL##RR##_TB)
+    if constexpr (R == 32) SWK_F16_COLASM(32);
+    else SWK_F16_COLASM(16);
+#undef SWK_F16_COLASM
     (void)Db; (void)S1; (void)X; (void)DN; (void)IN;
     upX_ = Xl[R - 1];
     best_ = best;
