@@ -620,6 +620,8 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   bool use_wave = b->wK > 0 && wave_est > tile_est;
   if (kforce && std::strcmp(kforce, "tile") == 0) use_wave = false;
   if (kforce && std::strcmp(kforce, "wave") == 0 && b->wK > 0) use_wave = true;
+  // the f16 wave kernel carries profile offsets in 16-bit halves (24 letters + pad fit)
+  if (use_f16 && b->prof && (size_t)(b->alpha + 1) * b->wPS16 > 65536) use_wave = false;
   const char* arith = opt16 ? "f16+u16-rescore" : use_f16 ? "f16" : "u16";
   if (use_wave) {
     snprintf(b->last_kernel, sizeof(b->last_kernel), "wave %s%s K=%d segs=%d", arith,

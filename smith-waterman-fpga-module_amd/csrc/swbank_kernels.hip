@@ -956,10 +956,13 @@ __device__ __forceinline__ void column_f16_lane_asm(const LK& lk, u16x2& diag_, 
 __device__ __forceinline__ uint32_t dpp_shr1(uint32_t lane0_value, uint32_t v) {
   return __builtin_amdgcn_update_dpp(lane0_value, v, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
 }
+__device__ __forceinline__ uint32_t dpp_shr1_zero(uint32_t v) {  // lane 0 reads 0
+  return __builtin_amdgcn_mov_dpp(v, 0x138 /* wave_shr:1 */, 0xF, 0xF, true);
+}
 
 // qtab (wave layout): LUT: 64*K row words | PROF: (pad+1) x PS bytes, PS = 64*K.
 template <int K, bool COL0, bool PROF, bool GOTOH, bool F16>
-__global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
+__global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
   const int lane = threadIdx.x & 63;
@@ -970,7 +973,8 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
       reinterpret_cast<uint4*>(prof)[i] = src[i];
     __syncthreads();
   }
-  const size_t pair = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t pair = (size_t)blockIdx.x * (blockDim.x >> 6) +
+                      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const size_t tA = 2 * pair, tB = tA + 1;
   const size_t n = a.n;
   if (tA >= n) return;  // whole wave
@@ -992,8 +996,17 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
   const u16x2 OES2 = {(unsigned short)oes, (unsigned short)oes};
   // selector word: u16 {code_lo, 0x0C, code_hi, 0x0C}; f16 {0x0C, code_lo, 0x0C, code_hi}
   // (the f16 LUT byte is the high byte; 2-byte f16 profiles use the code byte only)
-  const uint32_t padsel = F16 && !PROF ? ((pad << 8) | (pad << 24) | 0x000C000Cu)
-                                       : (pad | (pad << 16) | 0x0C000C00u);
+  // f16 profile: the code word carries the LDS byte offsets of both letters' profile rows
+  // plus the lane's own row offset (2K bytes per lane, added per DPP hop), so the lane's two
+  // addresses are one mask / shift each; the host keeps (pad + 1) x PS <= 64 KiB
+  const uint32_t PSb = a.PS;
+  const uint32_t hop = (2u * K) | (2u * K) << 16;
+  const auto code_word = [&](uint32_t x, uint32_t y) -> uint32_t {
+    if constexpr (F16 && PROF) return x * PSb | (y * PSb) << 16;
+    else if constexpr (F16) return (x << 8) | (y << 24) | 0x000C000Cu;
+    else return x | (y << 16) | 0x0C000C00u;
+  };
+  const uint32_t padsel = code_word(pad, pad);
   const _Float16 fnoe = (_Float16)(-(float)(a.O + a.E)), fne = (_Float16)(-(float)a.E);
   const f16x2 NOE2 = {fnoe, fnoe}, NE2 = {fne, fne};
   const u16x2 H0 = F16 ? (u16x2){0, 0} : S2;                          // H of row/col -1
@@ -1007,7 +1020,6 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
   }
   const uint32_t nv = a.nv;
   const uint8_t* prow = prof + lane * K;       // this lane's rows in every profile letter row
-  const uint8_t* prow2 = prof + lane * K * 2;  // f16 profile: 2 bytes per row
 
   u16x2 Hl[K], Xl[K];
 #pragma unroll
@@ -1017,7 +1029,8 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
   }
   u16x2 best = {0, 0};
   u16x2 prevUpH = H0;
-  uint32_t botH = as_u32(H0), botX = as_u32(X0), let = padsel, buf = padsel;
+  uint32_t botH = as_u32(H0), botX = as_u32(X0), buf = padsel;
+  uint32_t let = F16 && PROF ? padsel + lane * hop : padsel;
   // query segments (queries longer than 64K rows): lane 0 reads row -1 of this segment (the
   // previous segment's bottom row) from edge_in, lane 63 writes this segment's bottom row;
   // layout [pair][column] {H, G/T/F} of both targets
@@ -1026,9 +1039,12 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
   uint2* eout = seg_out ? a.edge_out + pair * a.ecols : nullptr;
   uint2 ebuf = make_uint2(as_u32(H0), as_u32(X0));
 
+  // two steps per iteration (the loop-carried values alternate registers instead of being
+  // copied back); an odd count gets one extra all-padding step, which changes no score
   const int nsteps = Lmax + 63;
-  for (int t = 0; t < nsteps; ++t) {
-    if ((t & 63) == 0) {  // next 64 columns of both targets, one code pair per lane
+  const auto step = [&](const int t, const bool even, auto segc) __attribute__((always_inline)) {
+    constexpr bool SEG = decltype(segc)::value;  // query segment: row -1 from edge_in
+    if (even && (t & 63) == 0) {  // next 64 columns of both targets, one code pair per lane
       const uint32_t c = (uint32_t)t + lane;
       uint32_t x = pad, y = pad;
       if (packed) {
@@ -1038,19 +1054,26 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
         if (c < LA) x = pA[c];
         if (c < LB) y = pB[c];
       }
-      buf = F16 && !PROF ? ((min(x, pad) << 8) | (min(y, pad) << 24) | 0x000C000Cu)
-                         : (min(x, pad) | (min(y, pad) << 16) | 0x0C000C00u);
-      if (seg_in) ebuf = c < (uint32_t)Lmax ? ein[c] : make_uint2(as_u32(H0), as_u32(X0));
+      buf = code_word(min(x, pad), min(y, pad));
+      if (SEG) ebuf = c < (uint32_t)Lmax ? ein[c] : make_uint2(as_u32(H0), as_u32(X0));
     }
     const uint32_t inj = __builtin_amdgcn_readlane(buf, t & 63);
-    uint32_t bH = as_u32(H0), bX = as_u32(X0);
-    if (seg_in) {
-      bH = __builtin_amdgcn_readlane(ebuf.x, t & 63);
-      bX = __builtin_amdgcn_readlane(ebuf.y, t & 63);
+    u16x2 upH, upX;
+    if constexpr (SEG) {
+      upH = as_u16x2(dpp_shr1(__builtin_amdgcn_readlane(ebuf.x, t & 63), botH));
+      upX = as_u16x2(dpp_shr1(__builtin_amdgcn_readlane(ebuf.y, t & 63), botX));
+    } else {  // row -1 boundary; a zero boundary comes from DPP's bound_ctrl (no lane-0 move)
+      upH = as_u16x2(as_u32(H0) == 0 ? dpp_shr1_zero(botH) : dpp_shr1(as_u32(H0), botH));
+      upX = as_u16x2(as_u32(X0) == 0 ? dpp_shr1_zero(botX) : dpp_shr1(as_u32(X0), botX));
     }
-    const u16x2 upH = as_u16x2(dpp_shr1(bH, botH));
-    u16x2 upX = as_u16x2(dpp_shr1(bX, botX));
-    let = dpp_shr1(inj, let);
+    if constexpr (F16 && PROF) {  // shift down one lane and add the lane's row offset
+      uint32_t nl = inj;
+      asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
+                   : "+v"(nl) : "v"(let), "v"(hop));
+      let = nl;
+    } else {
+      let = dpp_shr1(inj, let);
+    }
     u16x2 diag = prevUpH;
     prevUpH = upH;
     __builtin_amdgcn_sched_barrier(0);
@@ -1058,18 +1081,17 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
       const bool z = COL0 && t == lane;
       if constexpr (PROF) {
         ProfLookupK16<K> lk;
-        const uint32_t blo = let & 0xFFu, bhi = (let >> 16) & 0xFFu;
-        const uint8_t* plo = prow2 + blo * a.PS;
-        const uint8_t* phi = prow2 + bhi * a.PS;
+        const uint8_t* lds = reinterpret_cast<const uint8_t*>(smem);
+        const uint32_t olo = let & 0xFFFFu, ohi = let >> 16;
         if constexpr (K == 4) {
-          const uint2 x = *reinterpret_cast<const uint2*>(plo);
-          const uint2 y = *reinterpret_cast<const uint2*>(phi);
+          const uint2 x = *reinterpret_cast<const uint2*>(lds + olo);
+          const uint2 y = *reinterpret_cast<const uint2*>(lds + ohi);
           lk.lo[0] = x.x; lk.lo[1] = x.y; lk.hi[0] = y.x; lk.hi[1] = y.y;
         } else {
 #pragma unroll
           for (int q = 0; q < K / 8; ++q) {
-            const uint4 x = reinterpret_cast<const uint4*>(plo)[q];
-            const uint4 y = reinterpret_cast<const uint4*>(phi)[q];
+            const uint4 x = reinterpret_cast<const uint4*>(lds + olo)[q];
+            const uint4 y = reinterpret_cast<const uint4*>(lds + ohi)[q];
             lk.lo[4 * q] = x.x; lk.lo[4 * q + 1] = x.y; lk.lo[4 * q + 2] = x.z;
             lk.lo[4 * q + 3] = x.w;
             lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z;
@@ -1128,6 +1150,17 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
     botH = as_u32(Hl[K - 1]);
     botX = as_u32(upX);
     if (seg_out && lane == 63 && t >= 63 && t - 63 < Lmax) eout[t - 63] = make_uint2(botH, botX);
+  };
+  if (seg_in) {
+    for (int t = 0; t < nsteps; t += 2) {
+      step(t, true, std::true_type{});
+      step(t + 1, false, std::true_type{});
+    }
+  } else {
+    for (int t = 0; t < nsteps; t += 2) {
+      step(t, true, std::false_type{});
+      step(t + 1, false, std::false_type{});
+    }
   }
   // max over the wave's rows, per target (f16: non-negative integers -> int)
   uint32_t bx = best.x, by = best.y;
@@ -1154,7 +1187,11 @@ __global__ void __launch_bounds__(256) score_wave(const ScoreArgs a) {
 template <int K, bool COL0, bool PROF, bool GOTOH, bool F16>
 static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream_t st) {
   const size_t pairs = (a.n + 1) / 2;
-  const size_t blocks = (pairs + 3) / 4;
+  // 4 waves (pairs) per block, sharing one LDS copy of the profile; SWBANK_WAVE_BLOCK=1..8
+  // for tuning (measured on 12.5k protein targets: 4 and 5 best, 8 -11 %, 2 -25 %)
+  const char* wenv = std::getenv("SWBANK_WAVE_BLOCK");
+  const unsigned wpb = wenv && *wenv ? (unsigned)std::min(std::max(std::atoi(wenv), 1), 8) : 4u;
+  const size_t blocks = (pairs + wpb - 1) / wpb;
   const size_t lds = PROF ? prof_bytes : 0;
   auto fn = &score_wave<K, COL0, PROF, GOTOH, F16>;
   static bool attr_set = false;
@@ -1165,7 +1202,7 @@ static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream
     attr_set = true;
   }
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(256), (unsigned)lds, st, a);
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(64 * wpb), (unsigned)lds, st, a);
   return hipGetLastError();
 }
 
