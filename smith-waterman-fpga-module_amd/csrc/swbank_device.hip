@@ -600,8 +600,9 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   //  wave kernel (queries <= 1024 rows): base rate x row fill (query / 64K lanes' rows) x
   //    column fill (L / (L + 63): the 63-step skew of the lane pipeline).
   // Base GCUPS: tile f16 merged 9000 (profile 8000), f16 Gotoh 7500 (profile 7100), u16
-  // merged 7400 (profile 6500), u16 Gotoh 5800 (profile 5600); wave f16 merged 7600, f16
-  // Gotoh 6600, u16 merged 6500, u16 Gotoh 5000.  SWBANK_KERNEL=tile|wave forces one.
+  // merged 7400 (profile 6500), u16 Gotoh 5800 (profile 5600); wave f16 merged 8600
+  // (profile 7700), f16 Gotoh 7800 (profile 6800), u16 merged 7600 (profile 6600), u16 Gotoh
+  // 6100 (profile 5200).  SWBANK_KERNEL=tile|wave forces one.
   const double tiles = (double)ntiles, W = b->segs[0].W;
   const double cu_frac = std::min(1.0, tiles / 256.0);
   const double wps = std::min(4.0, std::max(1.0, std::ceil(tiles / 256.0)) * W / 4.0);
@@ -613,7 +614,9 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   if (b->wK > 0) {
     const double rowfill = (double)b->query.size() / (64.0 * b->wK * b->wsegs);
     const double colfill = max_len / (max_len + 63.0);
-    wave_est = (use_f16 ? (gotoh ? 6600 : 7600) : (gotoh ? 5000 : 6500)) * rowfill * colfill *
+    const double wave_base = use_f16 ? (gotoh ? (b->prof ? 6800 : 7800) : (b->prof ? 7700 : 8600))
+                                     : (gotoh ? (b->prof ? 5200 : 6100) : (b->prof ? 6600 : 7600));
+    wave_est = wave_base * rowfill * colfill *
                (b->wsegs > 1 ? 0.9 : 1.0);
   }
   const char* kforce = std::getenv("SWBANK_KERNEL");
