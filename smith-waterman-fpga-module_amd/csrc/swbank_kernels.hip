@@ -627,8 +627,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           ProfLookup16<R> lk;
           const uint32_t blo = min((wlo >> (8 * (jj & 3))) & 0xFFu, padc);
           const uint32_t bhi = min((whi >> (8 * (jj & 3))) & 0xFFu, padc);
-          const uint4* plo = reinterpret_cast<const uint4*>(prof + blo * a.PS + 2 * pbase);
-          const uint4* phi = reinterpret_cast<const uint4*>(prof + bhi * a.PS + 2 * pbase);
+          // 24-bit multiplies (full rate; a 32-bit v_mul_lo is quarter rate)
+          const uint4* plo = reinterpret_cast<const uint4*>(prof + __umul24(blo, a.PS) + 2 * pbase);
+          const uint4* phi = reinterpret_cast<const uint4*>(prof + __umul24(bhi, a.PS) + 2 * pbase);
 #pragma unroll
           for (int q = 0; q < R / 8; ++q) {
             const uint4 x = plo[q], y = phi[q];
@@ -646,8 +647,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           ProfLookup<R> lk;
           const uint32_t blo = min((wlo >> (8 * (jj & 3))) & 0xFFu, padc);
           const uint32_t bhi = min((whi >> (8 * (jj & 3))) & 0xFFu, padc);
-          const uint4* plo = reinterpret_cast<const uint4*>(prof + blo * a.PS + pbase);
-          const uint4* phi = reinterpret_cast<const uint4*>(prof + bhi * a.PS + pbase);
+          const uint4* plo = reinterpret_cast<const uint4*>(prof + __umul24(blo, a.PS) + pbase);
+          const uint4* phi = reinterpret_cast<const uint4*>(prof + __umul24(bhi, a.PS) + pbase);
 #pragma unroll
           for (int q = 0; q < R / 16; ++q) {
             const uint4 x = plo[q], y = phi[q];
@@ -1113,15 +1114,15 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
       ProfLookupK<K> lk;
       const uint32_t blo = let & 0xFFu, bhi = (let >> 16) & 0xFFu;
       if constexpr (K == 4) {
-        lk.lo[0] = *reinterpret_cast<const uint32_t*>(prow + blo * a.PS);
-        lk.hi[0] = *reinterpret_cast<const uint32_t*>(prow + bhi * a.PS);
+        lk.lo[0] = *reinterpret_cast<const uint32_t*>(prow + __umul24(blo, a.PS));
+        lk.hi[0] = *reinterpret_cast<const uint32_t*>(prow + __umul24(bhi, a.PS));
       } else if constexpr (K == 8) {
-        const uint2 x = *reinterpret_cast<const uint2*>(prow + blo * a.PS);
-        const uint2 y = *reinterpret_cast<const uint2*>(prow + bhi * a.PS);
+        const uint2 x = *reinterpret_cast<const uint2*>(prow + __umul24(blo, a.PS));
+        const uint2 y = *reinterpret_cast<const uint2*>(prow + __umul24(bhi, a.PS));
         lk.lo[0] = x.x; lk.lo[1] = x.y; lk.hi[0] = y.x; lk.hi[1] = y.y;
       } else {
-        const uint4 x = *reinterpret_cast<const uint4*>(prow + blo * a.PS);
-        const uint4 y = *reinterpret_cast<const uint4*>(prow + bhi * a.PS);
+        const uint4 x = *reinterpret_cast<const uint4*>(prow + __umul24(blo, a.PS));
+        const uint4 y = *reinterpret_cast<const uint4*>(prow + __umul24(bhi, a.PS));
         lk.lo[0] = x.x; lk.lo[1] = x.y; lk.lo[2] = x.z; lk.lo[3] = x.w;
         lk.hi[0] = y.x; lk.hi[1] = y.y; lk.hi[2] = y.z; lk.hi[3] = y.w;
       }
