@@ -11,7 +11,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 #include "swbank.h"
@@ -85,6 +91,68 @@ struct PinBuf {
     cap = 0;
   }
 };
+
+// Host worker threads for the host-buffer feeder (gather / scatter of a chunk): run(f) calls
+// f(part) for part = 0..size()-1, part 0 on the calling thread, and returns when all are done.
+class HostPool {
+ public:
+  explicit HostPool(unsigned n) : n_(std::max(1u, n)) {
+    for (unsigned i = 1; i < n_; ++i) th_.emplace_back([this, i] { loop(i); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  unsigned size() const { return n_; }
+  void run(const std::function<void(unsigned)>& f) {
+    if (n_ == 1) {
+      f(0);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &f;
+      pending_ = n_ - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> l(m_);
+    done_.wait(l, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(unsigned i) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(unsigned)>* job;
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        job = job_;
+      }
+      (*job)(i);
+      std::lock_guard<std::mutex> g(m_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  unsigned n_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(unsigned)>* job_ = nullptr;
+  unsigned pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
 }  // namespace
 
 struct sw_bank {
@@ -130,6 +198,16 @@ struct sw_bank {
   DevBuf<uint32_t> wtab;   // LUT: 64K row words | PROF: (A+1) x 64K profile bytes
   DevBuf<uint32_t> wtab16; // the same in f16 (LUT: high bytes | PROF: 2-byte entries)
   uint32_t wPS16 = 0;
+
+  // host-buffer feeder (sw_score_batch / sw_score_records): NSLOT pinned staging slots and
+  // device slots, chunk i gathered on the host while chunk i-1 crosses PCIe on copy_stream
+  // and chunk i-2 is scored on `stream`
+  static constexpr int NSLOT = 3;
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t h2d_done[NSLOT] = {}, kern_done[NSLOT] = {};
+  PinBuf hslot[NSLOT], hscores;
+  DevBuf<uint8_t> dslot[NSLOT];
+  std::unique_ptr<HostPool> pool;
 
   // workspaces
   DevBuf<uint8_t> res;
@@ -240,6 +318,16 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->wtab16.release();
   b->edge[0].release();
   b->edge[1].release();
+  if (b->copy_stream) (void)hipStreamSynchronize(b->copy_stream);
+  for (int i = 0; i < sw_bank::NSLOT; ++i) {
+    b->hslot[i].release();
+    b->dslot[i].release();
+    if (b->h2d_done[i]) (void)hipEventDestroy(b->h2d_done[i]);
+    if (b->kern_done[i]) (void)hipEventDestroy(b->kern_done[i]);
+  }
+  b->hscores.release();
+  b->pool.reset();
+  if (b->copy_stream) (void)hipStreamDestroy(b->copy_stream);
   b->res.release();
   b->offs.release();
   b->lens.release();
@@ -562,9 +650,12 @@ static sw_status range_check(sw_bank* b, uint32_t max_len) {
 }
 
 // packed: d_res holds n 64-byte CAPI records (2-bit codes); d_offs/d_lens are unused.
+// perm/perm_n (optional, tile kernel): pass 0 visits the targets in the order perm[0..n)
+// (target numbers; *perm_n = n on the device), e.g. longest first; the wave kernel ignores it.
 static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                         const uint32_t* d_lens, size_t n, uint32_t max_len, int32_t* d_scores,
-                        hipStream_t st, bool packed = false) {
+                        hipStream_t st, bool packed = false, const uint32_t* perm = nullptr,
+                        const uint32_t* perm_n = nullptr) {
   sw_bank::Ev ev{};
   if (b->timing) {
     HIPOK(b, hipEventCreate(&ev.a));
@@ -691,7 +782,11 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
       const uint32_t* lens = d_lens;
       int32_t* scores = d_scores;
       const uint32_t* idx = nullptr;
-      if (pass == 0 && packed) {
+      const uint32_t* nidx = nullptr;
+      if (pass == 0 && perm) {  // whole arrays, visited through the permutation
+        idx = perm + p0;
+        nidx = perm_n;
+      } else if (pass == 0 && packed) {
         res = d_res + p0 * SWB_RECORD;
         scores = d_scores + p0;
       } else if (pass == 0) {
@@ -700,6 +795,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
         scores = d_scores + p0;
       } else {
         idx = b->fb_idx.p + p0;
+        nidx = b->fb_cnt.p;
       }
       for (size_t s = 0; s < nseg; ++s) {
         const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
@@ -711,7 +807,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                                   f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
                                   f16 && b->prof ? b->PS16 : b->PS, b->pad, b->segs[s].W,
                                   scores, ein, eout, ecols, s > 0 ? 1 : 0, packed ? 1 : 0, idx,
-                                  idx ? b->fb_cnt.p : nullptr, (uint32_t)p0, st));
+                                  nidx, (uint32_t)p0, st));
       }
     }
   }
@@ -738,56 +834,282 @@ extern "C" sw_status sw_score_batch_device(sw_bank* b, const uint8_t* d_res,
                 stream ? reinterpret_cast<hipStream_t>(stream) : b->stream);
 }
 
+// ---- host-buffer batches: a pipelined feeder ----------------------------------------------
+// The reference host hands the accelerator host buffers (main_test.c:297-370 builds the WED
+// and sequence_t arrays in host memory).  A host batch is put in longest-first feed order,
+// cut into chunks and fed through NSLOT pinned staging slots: host threads gather chunk i
+// (code validation fused into the copy) while chunk i-1 crosses PCIe on the copy stream and
+// chunk i-2 is scored on the bank stream.
+namespace {
+unsigned host_threads() {
+  const int t = env_int("SWBANK_HOST_THREADS", 0);
+  if (t > 0) return (unsigned)std::min(t, 64);
+  return std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+}
+
+// f(lo, hi) over [0, n) split into the pool's parts (inline below 2048 items)
+template <class F>
+void parallel_for(HostPool& pool, size_t n, F&& f) {
+  const unsigned T = pool.size();
+  if (T <= 1 || n < 2048) {
+    f((size_t)0, n);
+    return;
+  }
+  const size_t step = (n + T - 1) / T;
+  pool.run([&](unsigned p) {
+    const size_t lo = std::min(n, p * step), hi = std::min(n, lo + step);
+    if (lo < hi) f(lo, hi);
+  });
+}
+
+// Longest-first visiting order of a chunk (the PrioEncoder feed order, ScoreBank_v2.v:142-148:
+// each 128-target tile then holds similar lengths): false when the lengths are already
+// non-increasing (no permutation needed), else perm[] = a stable counting sort over the
+// length range (parallel over the pool's parts when the range is small), or a stable
+// comparison sort when the range is wide.
+bool chunk_perm(HostPool& pool, const uint32_t* len, size_t n, uint32_t* perm) {
+  const unsigned T = n >= 8192 ? pool.size() : 1;
+  const size_t step = (n + T - 1) / T;
+  std::vector<uint32_t> plo(T, UINT32_MAX), phi(T, 0);
+  std::vector<char> pinc(T, 1);
+  const auto scan = [&](unsigned p) {
+    const size_t a = std::min(n, p * step), e = std::min(n, a + step);
+    uint32_t lo = UINT32_MAX, hi = 0, prev = a > 0 ? len[a - 1] : UINT32_MAX;
+    bool inc = true;
+    for (size_t k = a; k < e; ++k) {
+      const uint32_t l = len[k];
+      lo = std::min(lo, l);
+      hi = std::max(hi, l);
+      inc &= l <= prev;
+      prev = l;
+    }
+    plo[p] = lo;
+    phi[p] = hi;
+    pinc[p] = inc;
+  };
+  if (T > 1) pool.run(scan); else scan(0);
+  const uint32_t lo = *std::min_element(plo.begin(), plo.end());
+  const uint32_t hi = *std::max_element(phi.begin(), phi.end());
+  if (std::all_of(pinc.begin(), pinc.end(), [](char c) { return c != 0; })) return false;
+  const size_t range = (size_t)hi - lo + 1;
+  if (range <= 65536 && range <= 4 * n + 4096) {
+    // per-part histograms of bucket hi - l (longest first), then each part scatters at the
+    // prefix over (bucket, part): stable
+    std::vector<uint32_t> h((size_t)T * range, 0);
+    const auto count = [&](unsigned p) {
+      uint32_t* hp = h.data() + (size_t)p * range;
+      const size_t a = std::min(n, p * step), e = std::min(n, a + step);
+      for (size_t k = a; k < e; ++k) ++hp[hi - len[k]];
+    };
+    if (T > 1) pool.run(count); else count(0);
+    uint32_t acc = 0;
+    for (size_t bkt = 0; bkt < range; ++bkt)
+      for (unsigned p = 0; p < T; ++p) {
+        const uint32_t c = h[(size_t)p * range + bkt];
+        h[(size_t)p * range + bkt] = acc;
+        acc += c;
+      }
+    const auto place = [&](unsigned p) {
+      uint32_t* hp = h.data() + (size_t)p * range;
+      const size_t a = std::min(n, p * step), e = std::min(n, a + step);
+      for (size_t k = a; k < e; ++k) perm[hp[hi - len[k]]++] = (uint32_t)k;
+    };
+    if (T > 1) pool.run(place); else place(0);
+  } else {
+    std::iota(perm, perm + n, 0u);
+    std::stable_sort(perm, perm + n, [&](uint32_t a, uint32_t c) { return len[a] > len[c]; });
+  }
+  return true;
+}
+
+// chunk target: a quarter of the batch (so gather, copy and score overlap), 16-256 MiB
+size_t chunk_target(size_t total) {
+  const int mb = env_int("SWBANK_CHUNK_MB", 0);
+  if (mb > 0) return (size_t)mb << 20;
+  return std::min<size_t>((size_t)256 << 20, std::max<size_t>((size_t)16 << 20, total / 4));
+}
+}  // namespace
+
+static sw_status feeder_init(sw_bank* b) {
+  if (!b->pool) b->pool.reset(new (std::nothrow) HostPool(host_threads()));
+  if (!b->pool) return fail(b, SW_ERR_NOMEM, "host worker pool");
+  if (b->copy_stream) return SW_OK;
+  HIPOK(b, hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
+  for (int i = 0; i < sw_bank::NSLOT; ++i) {
+    HIPOK(b, hipEventCreateWithFlags(&b->h2d_done[i], hipEventDisableTiming));
+    HIPOK(b, hipEventCreateWithFlags(&b->kern_done[i], hipEventDisableTiming));
+  }
+  return SW_OK;
+}
+
+// One chunk = input positions [c0, c1), staged as `bytes` bytes in slot c % NSLOT.
+struct Chunk {
+  size_t c0, c1, bytes;
+};
+
+// Runs the feeder: gather(slot, chunk) fills the host slot (false: bad input, message set),
+// the slot goes to the device on the copy stream, score(dslot, chunk, d_scores) launches the
+// kernel on the bank stream; the scores come back to the pinned hscores in input order.
+template <class GatherF, class ScoreF>
+static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, GatherF gather,
+                      ScoreF score) {
+  sw_status st = feeder_init(b);
+  if (st != SW_OK) return st;
+  size_t slot_bytes = 0;
+  for (const Chunk& c : chunks) slot_bytes = std::max(slot_bytes, c.bytes);
+  for (int i = 0; i < std::min<int>(sw_bank::NSLOT, (int)chunks.size()); ++i) {
+    HIPOK(b, b->hslot[i].reserve(slot_bytes));
+    HIPOK(b, b->dslot[i].reserve(slot_bytes));
+  }
+  HIPOK(b, b->scores.reserve(n));
+  HIPOK(b, b->hscores.reserve(n * 4));
+  for (size_t i = 0; i < chunks.size(); ++i) {
+    const int s = (int)(i % sw_bank::NSLOT);
+    const Chunk& c = chunks[i];
+    if (i >= (size_t)sw_bank::NSLOT) HIPOK(b, hipEventSynchronize(b->h2d_done[s]));
+    if (!gather(b->hslot[s].p, c)) {
+      (void)hipStreamSynchronize(b->stream);
+      (void)hipStreamSynchronize(b->copy_stream);
+      return SW_ERR_ARG;
+    }
+    if (i >= (size_t)sw_bank::NSLOT)
+      HIPOK(b, hipStreamWaitEvent(b->copy_stream, b->kern_done[s], 0));
+    HIPOK(b, hipMemcpyAsync(b->dslot[s].p, b->hslot[s].p, c.bytes, hipMemcpyHostToDevice,
+                            b->copy_stream));
+    HIPOK(b, hipEventRecord(b->h2d_done[s], b->copy_stream));
+    HIPOK(b, hipStreamWaitEvent(b->stream, b->h2d_done[s], 0));
+    if ((st = score(b->dslot[s].p, c, b->scores.p + c.c0)) != SW_OK) {
+      (void)hipStreamSynchronize(b->stream);
+      (void)hipStreamSynchronize(b->copy_stream);
+      return st;
+    }
+    HIPOK(b, hipEventRecord(b->kern_done[s], b->stream));
+  }
+  HIPOK(b, hipMemcpyAsync(b->hscores.p, b->scores.p, n * 4, hipMemcpyDeviceToHost, b->stream));
+  HIPOK(b, hipStreamSynchronize(b->stream));
+  return SW_OK;
+}
+
+static inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// Chunk slot tail shared by both host paths: lens u32 x cnt | perm u32 x cnt | count u32.
+struct SlotTail {
+  size_t lens_at, perm_at, cnt_at;
+};
+static SlotTail slot_tail(size_t tail_at, size_t cnt) {
+  return {tail_at, tail_at + cnt * 4, tail_at + cnt * 8};
+}
+
 extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const uint64_t* offsets,
                                     const uint32_t* lens, size_t n, int32_t* scores_out) {
   if (!b) return SW_ERR_ARG;
   if (n == 0) return SW_OK;
   if (!offsets || !lens || !scores_out) return fail(b, SW_ERR_ARG, "null host buffer");
+  if (n > 0xFFFFFFFFull)
+    return fail(b, SW_ERR_ARG, "host batches hold < 2^32 targets (sw_score_batch_device does not)");
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
+  if ((st = feeder_init(b)) != SW_OK) return st;
 
-  // Feeder order: longest targets first so each 128-target tile has similar lengths
-  // (the RTL's PrioEncoder routes to the first free module, ScoreBank_v2.v:142-148).
-  std::vector<uint32_t> order(n);
-  std::iota(order.begin(), order.end(), 0u);
-  std::stable_sort(order.begin(), order.end(),
-                   [&](uint32_t a, uint32_t c) { return lens[a] > lens[c]; });
-  uint32_t max_len = n ? lens[order[0]] : 0;
+  // chunks in input order, cut at ~chunk_target() code bytes
+  uint32_t max_len = 0;
+  size_t total = 0;
+  for (size_t k = 0; k < n; ++k) {
+    max_len = std::max(max_len, lens[k]);
+    total += lens[k];
+  }
   if (max_len && !residues) return fail(b, SW_ERR_ARG, "null residues");
   if ((st = range_check(b, max_len)) != SW_OK) return st;
-
-  size_t total = 0;
-  for (size_t k = 0; k < n; ++k) total += lens[k];
-  std::vector<uint8_t> hres(std::max<size_t>(total, 1));
-  std::vector<uint64_t> hoffs(n);
-  std::vector<uint32_t> hlens(n);
-  size_t pos = 0;
-  for (size_t k = 0; k < n; ++k) {
-    const uint32_t src = order[k];
-    const uint8_t* p = residues + offsets[src];
-    for (uint32_t j = 0; j < lens[src]; ++j)
-      if (p[j] >= (uint32_t)b->alpha)
-        return fail(b, SW_ERR_ARG, "target %u code %u outside alphabet", src, p[j]);
-    std::memcpy(hres.data() + pos, p, lens[src]);
-    hoffs[k] = pos;
-    hlens[k] = lens[src];
-    pos += lens[src];
+  const size_t target = chunk_target(total);
+  std::vector<Chunk> chunks;
+  std::vector<uint32_t> chunk_max;
+  for (size_t k = 0, c0 = 0, acc = 0, ml = 0; k < n; ++k) {
+    acc += lens[k];
+    ml = std::max<size_t>(ml, lens[k]);
+    if (acc >= target || k + 1 == n) {
+      const size_t cnt = k + 1 - c0;
+      // slot: codes (16-B aligned) | offsets u64 | lens | perm | count
+      chunks.push_back({c0, k + 1, align16(align16(acc) + cnt * 16 + 4)});
+      chunk_max.push_back((uint32_t)ml);
+      c0 = k + 1;
+      acc = 0;
+      ml = 0;
+    }
   }
-
+  HostPool& pool = *b->pool;
+  const unsigned T = pool.size();
+  const uint32_t alpha = (uint32_t)b->alpha;
   HIPOK(b, hipSetDevice(b->device));
-  HIPOK(b, b->res.reserve(hres.size()));
-  HIPOK(b, b->offs.reserve(n));
-  HIPOK(b, b->lens.reserve(n));
-  HIPOK(b, b->scores.reserve(n));
-  HIPOK(b, hipMemcpyAsync(b->res.p, hres.data(), hres.size(), hipMemcpyHostToDevice, b->stream));
-  HIPOK(b, hipMemcpyAsync(b->offs.p, hoffs.data(), n * 8, hipMemcpyHostToDevice, b->stream));
-  HIPOK(b, hipMemcpyAsync(b->lens.p, hlens.data(), n * 4, hipMemcpyHostToDevice, b->stream));
-  st = launch(b, b->res.p, b->offs.p, b->lens.p, n, max_len, b->scores.p, b->stream);
-  if (st != SW_OK) return st;
-  std::vector<int32_t> sorted(n);
-  HIPOK(b, hipMemcpyAsync(sorted.data(), b->scores.p, n * 4, hipMemcpyDeviceToHost, b->stream));
-  HIPOK(b, hipStreamSynchronize(b->stream));
-  for (size_t k = 0; k < n; ++k) scores_out[order[k]] = sorted[k];
+  const auto offs_at = [&](const Chunk& c) { return c.bytes - align16((c.c1 - c.c0) * 16 + 4); };
+  std::vector<char> has_perm(chunks.size(), 0);
+  std::vector<size_t> part(T + 1);
+  std::atomic<size_t> bad{SIZE_MAX};
+  size_t gi = 0, si = 0;
+  const auto gather = [&](uint8_t* slot, const Chunk& c) -> bool {
+    const size_t cnt = c.c1 - c.c0, oa = offs_at(c);
+    const SlotTail tl = slot_tail(oa + cnt * 8, cnt);
+    uint64_t* so = reinterpret_cast<uint64_t*>(slot + oa);
+    uint32_t* sl = reinterpret_cast<uint32_t*>(slot + tl.lens_at);
+    // two passes over the pool's parts: code bytes per part, then copy at the prefix
+    const size_t step = (cnt + T - 1) / T;
+    std::fill(part.begin(), part.end(), 0);
+    pool.run([&](unsigned p) {
+      size_t acc = 0;
+      for (size_t k = c.c0 + std::min(cnt, p * step); k < c.c0 + std::min(cnt, (p + 1) * step); ++k)
+        acc += lens[k];
+      part[p + 1] = acc;
+    });
+    for (unsigned p = 0; p < T; ++p) part[p + 1] += part[p];
+    pool.run([&](unsigned p) {
+      size_t at = part[p];
+      for (size_t i = std::min(cnt, p * step); i < std::min(cnt, (p + 1) * step); ++i) {
+        const size_t k = c.c0 + i;
+        const uint32_t l = lens[k];
+        const uint8_t* src = residues + offsets[k];
+        uint8_t* d = slot + at;
+        uint8_t m = 0;
+        for (uint32_t j = 0; j < l; ++j) {  // copy + alphabet check, vectorised
+          const uint8_t v = src[j];
+          d[j] = v;
+          m = v > m ? v : m;
+        }
+        if (l && m >= alpha) {
+          size_t cur = bad.load();
+          while (k < cur && !bad.compare_exchange_weak(cur, k)) {
+          }
+        }
+        so[i] = at;
+        sl[i] = l;
+        at += l;
+      }
+    });
+    if (bad.load() != SIZE_MAX) {
+      const size_t k = bad.load();
+      uint8_t m = 0;
+      for (uint32_t j = 0; j < lens[k]; ++j) m = std::max(m, residues[offsets[k] + j]);
+      fail(b, SW_ERR_ARG, "target %zu code %u outside alphabet", k, (unsigned)m);
+      return false;
+    }
+    has_perm[gi++] = chunk_perm(pool, sl, cnt, reinterpret_cast<uint32_t*>(slot + tl.perm_at));
+    *reinterpret_cast<uint32_t*>(slot + tl.cnt_at) = (uint32_t)cnt;
+    return true;
+  };
+  const auto score = [&](uint8_t* dslot, const Chunk& c, int32_t* d_scores) -> sw_status {
+    const size_t cnt = c.c1 - c.c0, oa = offs_at(c);
+    const SlotTail tl = slot_tail(oa + cnt * 8, cnt);
+    const bool pm = has_perm[si];
+    const uint32_t ml = chunk_max[si++];
+    return launch(b, dslot, reinterpret_cast<const uint64_t*>(dslot + oa),
+                  reinterpret_cast<const uint32_t*>(dslot + tl.lens_at), cnt, ml, d_scores,
+                  b->stream, false,
+                  pm ? reinterpret_cast<const uint32_t*>(dslot + tl.perm_at) : nullptr,
+                  pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr);
+  };
+  if ((st = feed(b, n, chunks, gather, score)) != SW_OK) return st;
+  const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
+  parallel_for(pool, n, [&](size_t lo, size_t hi) {
+    std::memcpy(scores_out + lo, hs + lo, (hi - lo) * 4);
+  });
   return SW_OK;
 }
 
@@ -832,35 +1154,83 @@ extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
   if (n == 0) return SW_OK;
   if (!records || !scores_out) return fail(b, SW_ERR_ARG, "null host buffer");
   if (b->alpha != SW_DNA_ALPHA) return fail(b, SW_ERR_UNSUPPORTED, "records carry DNA only");
+  if (n > 0xFFFFFFFFull)
+    return fail(b, SW_ERR_ARG, "host batches hold < 2^32 records (sw_score_records_device does not)");
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
+  if ((st = feeder_init(b)) != SW_OK) return st;
   const uint8_t* recs = static_cast<const uint8_t*>(records);
-  std::vector<uint32_t> order(n);
-  std::iota(order.begin(), order.end(), 0u);
-  for (size_t k = 0; k < n; ++k)
-    if (record_len(recs + k * SWB_RECORD) > SWB_RECORD_MAX)
-      return fail(b, SW_ERR_ARG, "record %zu length %u > %u", k, record_len(recs + k * SWB_RECORD),
-                  SWB_RECORD_MAX);
-  // longest first, as sw_score_batch (PrioEncoder order)
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t c) {
-    return record_len(recs + (size_t)a * SWB_RECORD) > record_len(recs + (size_t)c * SWB_RECORD);
-  });
-  const uint32_t max_len = record_len(recs + (size_t)order[0] * SWB_RECORD);
-  if ((st = range_check(b, max_len)) != SW_OK) return st;
-  std::vector<uint8_t> sorted(n * SWB_RECORD);
-  for (size_t k = 0; k < n; ++k)
-    std::memcpy(sorted.data() + k * SWB_RECORD, recs + (size_t)order[k] * SWB_RECORD, SWB_RECORD);
+  const auto rlen = [&](size_t k) { return record_len(recs + k * SWB_RECORD); };
+  // lengths are checked while gathering; the range check takes the record capacity unless
+  // that is too long for the 16-bit lanes, then the batch's true maximum
+  if (range_check(b, SWB_RECORD_MAX) != SW_OK) {
+    uint32_t max_len = 0;
+    for (size_t k = 0; k < n; ++k) max_len = std::max(max_len, std::min(rlen(k), SWB_RECORD_MAX));
+    if ((st = range_check(b, max_len)) != SW_OK) return st;
+  }
+  // chunks in input order: records | lens | perm | count (longest-first order per chunk)
+  const size_t per = std::max<size_t>(1, chunk_target(n * SWB_RECORD) / SWB_RECORD);
+  std::vector<Chunk> chunks;
+  for (size_t c0 = 0; c0 < n; c0 += per) {
+    const size_t c1 = std::min(n, c0 + per);
+    chunks.push_back({c0, c1, align16((c1 - c0) * (SWB_RECORD + 8) + 4)});
+  }
+  HostPool& pool = *b->pool;
   HIPOK(b, hipSetDevice(b->device));
-  HIPOK(b, b->res.reserve(sorted.size()));
-  HIPOK(b, b->scores.reserve(n));
-  HIPOK(b, hipMemcpyAsync(b->res.p, sorted.data(), sorted.size(), hipMemcpyHostToDevice,
-                          b->stream));
-  st = launch(b, b->res.p, nullptr, nullptr, n, max_len, b->scores.p, b->stream, true);
-  if (st != SW_OK) return st;
-  std::vector<int32_t> out(n);
-  HIPOK(b, hipMemcpyAsync(out.data(), b->scores.p, n * 4, hipMemcpyDeviceToHost, b->stream));
-  HIPOK(b, hipStreamSynchronize(b->stream));
-  for (size_t k = 0; k < n; ++k) scores_out[order[k]] = out[k];
+  std::vector<char> has_perm(chunks.size(), 0);
+  std::vector<uint32_t> chunk_max(chunks.size(), 0);
+  std::atomic<size_t> bad{SIZE_MAX};
+  std::atomic<uint32_t> cmax{0};
+  size_t gi = 0, si = 0;
+  const auto gather = [&](uint8_t* slot, const Chunk& c) -> bool {
+    const size_t cnt = c.c1 - c.c0;
+    const SlotTail tl = slot_tail(cnt * SWB_RECORD, cnt);
+    uint32_t* sl = reinterpret_cast<uint32_t*>(slot + tl.lens_at);
+    cmax = 0;
+    parallel_for(pool, cnt, [&](size_t lo, size_t hi) {
+      std::memcpy(slot + lo * SWB_RECORD, recs + (c.c0 + lo) * SWB_RECORD, (hi - lo) * SWB_RECORD);
+      uint32_t m = 0;
+      for (size_t i = lo; i < hi; ++i) {
+        const uint32_t l = record_len(slot + i * SWB_RECORD);
+        sl[i] = l;
+        m = std::max(m, l);
+      }
+      uint32_t cur = cmax.load();
+      while (m > cur && !cmax.compare_exchange_weak(cur, m)) {
+      }
+      if (m > SWB_RECORD_MAX) {
+        for (size_t i = lo; i < hi; ++i) {
+          size_t cb = bad.load();
+          while (sl[i] > SWB_RECORD_MAX && c.c0 + i < cb &&
+                 !bad.compare_exchange_weak(cb, c.c0 + i)) {
+          }
+        }
+      }
+    });
+    if (bad.load() != SIZE_MAX) {
+      const size_t k = bad.load();
+      fail(b, SW_ERR_ARG, "record %zu length %u > %u", k, rlen(k), SWB_RECORD_MAX);
+      return false;
+    }
+    has_perm[gi] = chunk_perm(pool, sl, cnt, reinterpret_cast<uint32_t*>(slot + tl.perm_at));
+    chunk_max[gi++] = cmax.load();
+    *reinterpret_cast<uint32_t*>(slot + tl.cnt_at) = (uint32_t)cnt;
+    return true;
+  };
+  const auto score = [&](uint8_t* dslot, const Chunk& c, int32_t* d_scores) -> sw_status {
+    const size_t cnt = c.c1 - c.c0;
+    const SlotTail tl = slot_tail(cnt * SWB_RECORD, cnt);
+    const bool pm = has_perm[si];
+    const uint32_t ml = chunk_max[si++];
+    return launch(b, dslot, nullptr, nullptr, cnt, ml, d_scores, b->stream, true,
+                  pm ? reinterpret_cast<const uint32_t*>(dslot + tl.perm_at) : nullptr,
+                  pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr);
+  };
+  if ((st = feed(b, n, chunks, gather, score)) != SW_OK) return st;
+  const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
+  parallel_for(pool, n, [&](size_t lo, size_t hi) {
+    std::memcpy(scores_out + lo, hs + lo, (hi - lo) * 4);
+  });
   return SW_OK;
 }
 

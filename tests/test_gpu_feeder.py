@@ -1,0 +1,118 @@
+"""GPU: the host-buffer feeder of sw_score_batch / sw_score_records (chunks in input order,
+pinned staging slots, copy stream, a longest-first permutation per chunk).
+
+Forced to many small chunks (SWBANK_CHUNK_MB=1) with ragged lengths, so several chunks are in
+flight at once and each carries its own permutation; the scores must equal the device-API
+path's (one launch over the whole batch, caller's order) and the oracle's."""
+import numpy as np
+import pytest
+
+import swbank as S
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+REF = (5, -4, -12, -4)
+
+
+def _ragged(rng, n, lo, hi, A=4):
+    lens = rng.integers(lo, hi + 1, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    res = rng.integers(0, A, int(lens.sum()), dtype=np.uint8)
+    return res, offs, lens
+
+
+def _device_scores(bank, res, offs, lens):
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    d_sc = torch.zeros(len(lens), dtype=torch.int32, device=dev)
+    s = torch.cuda.Stream()
+    bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), len(lens),
+                            int(lens.max()), d_sc.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    return d_sc.cpu().numpy()
+
+
+@pytest.mark.parametrize("chunk_mb", ["1", "3"])
+def test_feeder_many_chunks_ragged(monkeypatch, chunk_mb):
+    monkeypatch.setenv("SWBANK_CHUNK_MB", chunk_mb)
+    rng = np.random.default_rng(11)
+    res, offs, lens = _ragged(rng, 60000, 0, 220)  # ~6.6 MB of codes: 2-7 chunks
+    q = rng.integers(0, 4, 100, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        got = bank.score_batch(res, offs, lens)
+        dev = _device_scores(bank, res, offs, lens)
+    assert np.array_equal(got, dev)
+    sel = rng.choice(len(lens), 3000, replace=False)
+    sub = [res[int(offs[k]):int(offs[k]) + int(lens[k])] for k in sel]
+    want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(*REF[:2]), *REF[2:])
+    assert np.array_equal(got[sel], want)
+
+
+def test_feeder_scattered_offsets(monkeypatch):
+    """offsets in any order and with gaps (the caller's layout, not the feeder's)"""
+    monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
+    rng = np.random.default_rng(12)
+    res, offs, lens = _ragged(rng, 30000, 1, 150)
+    n = len(lens)
+    perm = rng.permutation(n)                 # target j of the new batch = old target perm[j]
+    lens2 = lens[perm]
+    gap = np.full(int(lens.sum()) + 7 * n, 3, np.uint8)
+    offs2 = np.zeros(n, np.uint64)
+    cursor = 0
+    for j in rng.permutation(n):              # laid out in memory in yet another order
+        offs2[j] = cursor
+        k = int(perm[j])
+        gap[cursor:cursor + int(lens2[j])] = res[int(offs[k]):int(offs[k]) + int(lens[k])]
+        cursor += int(lens2[j]) + 7
+    q = rng.integers(0, 4, 64, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        base = bank.score_batch(res, offs, lens)
+        got = bank.score_batch(gap, offs2, lens2)
+    assert np.array_equal(got, base[perm])
+
+
+def test_feeder_bad_code_in_late_chunk(monkeypatch):
+    monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
+    rng = np.random.default_rng(13)
+    res, offs, lens = _ragged(rng, 30000, 50, 150)
+    bad = 27000
+    res[int(offs[bad]) + 3] = 9
+    q = rng.integers(0, 4, 64, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        with pytest.raises(S.SwbankError) as ei:
+            bank.score_batch(res, offs, lens)
+        assert ei.value.status == S.ERR_ARG and f"target {bad} code 9" in str(ei.value)
+        res[int(offs[bad]) + 3] = 1  # the bank stays usable after the error
+        got = bank.score_batch(res, offs, lens)
+        assert np.array_equal(got, _device_scores(bank, res, offs, lens))
+
+
+def test_feeder_records_many_chunks(monkeypatch):
+    monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
+    rng = np.random.default_rng(14)
+    n = 50000  # 3.2 MB of records: 4 chunks
+    L = rng.integers(1, S.RECORD_MAX_BASES + 1, n)
+    seqs = [rng.integers(0, 4, int(l), dtype=np.uint8) for l in L]
+    recs = S.make_records(seqs)
+    q = rng.integers(0, 4, 120, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        got = bank.score_records(recs)
+        want = bank.score_targets(seqs)
+        assert np.array_equal(got, want)
+        recs[40000, 4:6] = np.frombuffer(np.uint16(S.RECORD_MAX_BASES + 1).tobytes(), np.uint8)
+        with pytest.raises(S.SwbankError) as ei:
+            bank.score_records(recs)
+        assert ei.value.status == S.ERR_ARG and "record 40000" in str(ei.value)
