@@ -109,7 +109,9 @@ sw_status sw_load_query(sw_bank *bank, uint64_t id, const uint8_t *codes, uint32
 
 /* ---- target stream -> scores ----------------------------------------------------------- */
 /* Host buffers, blocking.  Target k = residues[offsets[k] .. offsets[k]+lens[k]) (codes).
- * scores_out[k] = max local-alignment score of (query, target k). */
+ * scores_out[k] = max local-alignment score of (query, target k).  The bank feeds the batch in
+ * chunks through pinned staging on its own worker threads and a copy stream (gather, PCIe and
+ * scoring overlap), so host buffers need no pinning or layout; n < 2^32. */
 sw_status sw_score_batch(sw_bank *bank, const uint8_t *residues, const uint64_t *offsets,
                          const uint32_t *lens, size_t n, int32_t *scores_out);
 
