@@ -615,6 +615,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       uint2* rout = wave < W - 1 ? ring + ((size_t)(wave * 2 + slot) * C) * 64 + lane
                                  : sink + lane;
       uint2 rv = rin[0];
+      ProfLookup16<PROF && F16 ? R : 2> lkq;  // f16 profile: the next column's words
+      (void)lkq;
 #pragma unroll
       for (int jj = 0; jj < C; ++jj) {
         const u16x2 upH = as_u16x2(rv.x);
@@ -624,20 +626,27 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         prevUpH = upH;
         const uint32_t wlo = jj < 4 ? clo.x : clo.y, whi = jj < 4 ? chi.x : chi.y;
         if constexpr (PROF && F16) {
-          ProfLookup16<R> lk;
-          const uint32_t blo = min((wlo >> (8 * (jj & 3))) & 0xFFu, padc);
-          const uint32_t bhi = min((whi >> (8 * (jj & 3))) & 0xFFu, padc);
-          // 24-bit multiplies (full rate; a 32-bit v_mul_lo is quarter rate)
-          const uint4* plo = reinterpret_cast<const uint4*>(prof + __umul24(blo, a.PS) + 2 * pbase);
-          const uint4* phi = reinterpret_cast<const uint4*>(prof + __umul24(bhi, a.PS) + 2 * pbase);
+          // profile words one column ahead (the LDS latency hides behind a column)
+          const auto load16 = [&](int j, ProfLookup16<R>& out) {
+            const uint32_t wl = j < 4 ? clo.x : clo.y, wh = j < 4 ? chi.x : chi.y;
+            const uint32_t blo = min((wl >> (8 * (j & 3))) & 0xFFu, padc);
+            const uint32_t bhi = min((wh >> (8 * (j & 3))) & 0xFFu, padc);
+            // 24-bit multiplies (full rate; a 32-bit v_mul_lo is quarter rate)
+            const uint4* plo = reinterpret_cast<const uint4*>(prof + __umul24(blo, a.PS) + 2 * pbase);
+            const uint4* phi = reinterpret_cast<const uint4*>(prof + __umul24(bhi, a.PS) + 2 * pbase);
 #pragma unroll
-          for (int q = 0; q < R / 8; ++q) {
-            const uint4 x = plo[q], y = phi[q];
-            lk.lo[4 * q] = x.x; lk.lo[4 * q + 1] = x.y; lk.lo[4 * q + 2] = x.z;
-            lk.lo[4 * q + 3] = x.w;
-            lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z;
-            lk.hi[4 * q + 3] = y.w;
-          }
+            for (int q = 0; q < R / 8; ++q) {
+              const uint4 x = plo[q], y = phi[q];
+              out.lo[4 * q] = x.x; out.lo[4 * q + 1] = x.y; out.lo[4 * q + 2] = x.z;
+              out.lo[4 * q + 3] = x.w;
+              out.hi[4 * q] = y.x; out.hi[4 * q + 1] = y.y; out.hi[4 * q + 2] = y.z;
+              out.hi[4 * q + 3] = y.w;
+            }
+          };
+          ProfLookup16<R> lk;
+          if (jj == 0) load16(0, lk);
+          else lk = lkq;
+          if (jj + 1 < C) load16(jj + 1, lkq);
           __builtin_amdgcn_sched_barrier(0);
           if (COL0 && jj == 0 && c == 0)
             column_f16<R, RB, GOTOH, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
