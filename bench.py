@@ -46,11 +46,13 @@ HBM_PEAK_GBS = 8000.0
 # several algorithmic ops into one instruction, so frac > 1 is possible.
 # Issue bound: one instruction advances one query row for a lane's 2 targets (128 cells per
 # wave-instruction); instructions per row of the column body (csrc/swbank_kernels.hip):
-# tile f16 merged 7.5, tile u16 merged 9, tile u16 Gotoh 11 (+0.1-0.7 of loop overhead).
+# f16 merged 7.5, f16 Gotoh 8.5, u16 merged 9, u16 Gotoh 11 (the column body both kernels
+# share; the tile kernel adds 0.1-0.7 per row of loop overhead, the wave kernel ~7 per step of
+# K rows plus the 63-step lane skew).
 OPS_PER_CELL = {"merged": 10, "gotoh": 11}
 VALU_PEAK_TOPS_16 = CUS * SIMD_PER_CU * 16 * 2 * CLK_GHZ / 1e3  # 78.6
 VALU_ISSUE_PER_SIMD_CLK = 0.25
-VALU_INSTR_PER_ROW = {"f16": 7.5, "u16": 9.0, "u16-gotoh": 11.0}
+VALU_INSTR_PER_ROW = {"f16": 7.5, "f16-gotoh": 8.5, "u16": 9.0, "u16-gotoh": 11.0}
 
 
 def valu_peak_gcups(mode: str) -> float:
@@ -94,14 +96,15 @@ def make_codes(seed: int, n: int, L: int, alpha: int = 4) -> np.ndarray:
 
 
 def pmc_traffic(workload: str):
-    """HBM bytes per score launch from the committed rocprofv3 PMC summary, if it matches."""
-    path = os.path.join(REPO, "profiles", "pmc_summary.json")
-    try:
-        d = json.load(open(path))
-        if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+    """HBM bytes per score launch from the committed rocprofv3 PMC summaries, if one matches
+    (profiles/pmc_summary.json: the headline; profiles/pmc_summary_<workload>.json: others)."""
+    for name in ("pmc_summary.json", f"pmc_summary_{workload}.json"):
+        try:
+            d = json.load(open(os.path.join(REPO, "profiles", name)))
+            if d.get("workload") == workload:
+                return d.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
     return None
 
 
@@ -273,10 +276,11 @@ def main():
     pack_s = pack_ms / max(launches, 1) / 1e3 * calls_per_step
     kernel = wl.bank.last_kernel()
     arith = "f16" if " f16" in kernel else "u16"
-    mode = arith if wl.model == "merged" else "u16-gotoh"
+    mode = arith if wl.model == "merged" else f"{arith}-gotoh"
     kernel_gcups = cells_rank / score_s / 1e9
-    # the issue bound is for the tile kernel's column body; the wave kernel's differs
-    peak_gcups = valu_peak_gcups(mode) if kernel.startswith("tile") else None
+    # issue bound of the column body (both kernels); the wave kernel's per-step overhead and
+    # lane skew come on top
+    peak_gcups = valu_peak_gcups(mode)
     ops = OPS_PER_CELL[wl.model]
     achieved_tops = ops * kernel_gcups / 1e3
     # algorithmic bytes: 1 B per residue read once per query + 4 B per score written

@@ -6,7 +6,10 @@ HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come from 
 --pmc passes (TCC slot budget), are in KiB, and FETCH_SIZE reads half the bytes of a wide
 coalesced stream on gfx950, so it is doubled (our 8-byte-per-lane code loads are not a
 calibrated width: the doubled figure is an estimate, within ~10% of the algorithmic bytes).
-usage: python scripts/collect_profiles.py ROUND PROF_DIR PMC_DIR WORKLOAD
+usage: python scripts/collect_profiles.py ROUND PROF_DIR PMC_DIR WORKLOAD [KERNEL [SUFFIX]]
+  KERNEL: substring of the kernel name the counters are averaged over (default score_kernel)
+  SUFFIX: file suffix for a second workload (kernel_stats_SUFFIX.csv, pmc_SUFFIX_*.csv,
+          pmc_summary_WORKLOAD.json); without it the files are the headline's
 """
 import csv
 import glob
@@ -16,18 +19,21 @@ import shutil
 import sys
 
 rnd, prof, pmc, workload = sys.argv[1:5]
+kname = sys.argv[5] if len(sys.argv) > 5 else "score_kernel"
+suffix = sys.argv[6] if len(sys.argv) > 6 else ""
+tag = f"_{suffix}" if suffix else ""
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(REPO, "profiles", rnd)
 os.makedirs(dst, exist_ok=True)
 for f in glob.glob(os.path.join(prof, "*kernel_stats.csv")):
-    shutil.copy(f, os.path.join(dst, "kernel_stats.csv"))
+    shutil.copy(f, os.path.join(dst, f"kernel_stats{tag}.csv"))
 
 
 def mean_counter(name):
     vals = []
     for f in glob.glob(os.path.join(pmc, "*", "pmc_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "score_kernel" in r["Kernel_Name"] and r["Counter_Name"] == name:
+            if kname in r["Kernel_Name"] and r["Counter_Name"] == name:
                 vals.append(float(r["Counter_Value"]))
     return sum(vals) / len(vals) if vals else None
 
@@ -44,7 +50,9 @@ if "FETCH_SIZE" in summary and "WRITE_SIZE" in summary:
     summary["hbm_bytes_note"] = "(2*FETCH_SIZE + WRITE_SIZE) KiB; FETCH doubled per gfx950 calibration"
 for f in glob.glob(os.path.join(pmc, "*", "pmc_counter_collection.csv")):
     sub = os.path.basename(os.path.dirname(f))
-    shutil.copy(f, os.path.join(dst, f"pmc_{sub}.csv"))
-json.dump(summary, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
-json.dump(summary, open(os.path.join(REPO, "profiles", "pmc_summary.json"), "w"), indent=1)
+    shutil.copy(f, os.path.join(dst, f"pmc{tag}_{sub}.csv"))
+summary["kernel"] = kname
+out = "pmc_summary.json" if not suffix else f"pmc_summary_{workload}.json"
+json.dump(summary, open(os.path.join(dst, out), "w"), indent=1)
+json.dump(summary, open(os.path.join(REPO, "profiles", out), "w"), indent=1)
 print(json.dumps(summary))
