@@ -90,6 +90,27 @@ def gotoh_block(mode, last, nrows=8):
     return out
 
 
+def pair_block(first, last, nrows=8):
+    """Pair-profile block (DNA, merged gaps): the substitution words of both targets come
+    ready-made from an LDS table of letter pairs, word p{i} = s(row i+1) for (lo, hi), so
+    there is no v_perm per row: 6.5 VALU per 2 cells.  Da carries D of the block's first row
+    in and of the next block's first row out; the first block computes it from dg + pw."""
+    out = ["v_pk_add_f16 %[Da], %[dg], %[pw]"] if first else []
+    for i in range(nrows):
+        dcur, dnext = ("%[Da]", "%[Db]") if i % 2 == 0 else ("%[Db]", "%[Da]")
+        up = "%[up]" if i == 0 else f"%[t{i - 1}]"
+        final = last and i == nrows - 1
+        out.append("s_nop 0" if final else f"v_pk_add_f16 {dnext}, %[h{i}], %[p{i}]")
+        out.append(f"v_pk_maximum3_f16 %[X], {up}, %[t{i}], %[t{i}]")
+        out.append(f"v_pk_add_f16 %[DN], {dcur}, %[noe]")
+        out.append("v_pk_add_f16 %[IN], %[X], %[ne]")
+        out.append(f"v_pk_maximum3_f16 %[h{i}], {dcur}, 0, %[X]")
+        out.append(f"v_pk_maximum3_f16 %[t{i}], %[DN], %[noe], %[IN]")
+        if i % 2 == 1:
+            out.append(f"v_pk_maximum3_f16 %[best], %[best], %[h{i - 1}], %[h{i}]")
+    return out
+
+
 def fmt(lines):
     return "".join(f'  "{ln}\\n\\t" \\\n' for ln in lines) + '  ""\n'
 
@@ -114,6 +135,10 @@ def main():
         parts.append(f"#define SWK_F16_COL{R}_HT {hts}\n")
         tbs = ", ".join(f'[tb{i}] "s"(lk.tab[{min(i + 1, R - 1)}])' for i in range(R))
         parts.append(f"#define SWK_F16_COL{R}_TB {tbs}\n")
+    # pair-profile blocks: first (with the column prologue), middle, last (final row)
+    parts.append("#define SWK_F16PAIR_F \\\n" + fmt(pair_block(True, False)))
+    parts.append("#define SWK_F16PAIR_M \\\n" + fmt(pair_block(False, False)))
+    parts.append("#define SWK_F16PAIR_L \\\n" + fmt(pair_block(False, True)))
     # 4-row single blocks (the wave kernel's K = 4: a whole column in one block)
     for mode in ("L", "P"):
         parts.append(f"#define SWK_F16M_{mode}_Z0_L1_R4 \\\n" + fmt(merged_block(mode, 0, 1, 4)))

@@ -38,7 +38,8 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                        const void* edge_in, void* edge_out, uint32_t ecols,
                                        int accum, int packed, const uint32_t* idx,
-                                       const uint32_t* nidx, uint32_t idx_base, hipStream_t st);
+                                       const uint32_t* nidx, uint32_t idx_base, int pair,
+                                       uint32_t pS1, uint32_t pS2, hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, hipStream_t st);
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
@@ -184,6 +185,10 @@ struct sw_bank {
   uint32_t nv16 = 0, PS16 = 0;  // PS16: f16 profile row stride (bytes)
   int32_t f16_neg = 0;     // most negative intermediate: -(o + 2e + |min s|)
   DevBuf<uint32_t> qtab16;
+  // f16 letter-pair table (DNA merged gaps, one segment of <= 4 waves): the tile kernel's
+  // PAIR variant; pair_bytes = 0 when the query does not qualify
+  DevBuf<uint32_t> qpair;
+  uint32_t pair_bytes = 0, pS1 = 0, pS2 = 0;
   DevBuf<uint32_t> fb_idx, fb_cnt;  // pairs an optimistic f16 pass re-scores in u16
   DevBuf<unsigned long long> best_key;  // sw_best_hit_device scratch
   struct Seg { int W; size_t off, off16; };  // rows = W*R (last may be shorter); word offsets
@@ -308,6 +313,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   (void)sw_bank_timing(b, &nl, &pm, &sm);
   b->qtab.release();
   b->qtab16.release();
+  b->qpair.release();
   b->stage.release();
   if (b->ev_ready) (void)hipEventDestroy(b->ev_ready);
   if (b->ev_used) (void)hipEventDestroy(b->ev_used);
@@ -534,6 +540,38 @@ static sw_status prepare(sw_bank* b) {
       std::memcpy(tab16.data() + sg.off16, qp.data(), qp.size() * 2);
     }
   }
+  // Letter-pair table for the PAIR tile kernel (SWBANK_PAIR=0 at launch time disables it):
+  // DNA merged gaps,
+  // the f16 LUT kernel's R = 32, one segment of at most 4 waves (the table's 25 slots then fit
+  // beside the ring at 4 workgroups per CU).  Slot (a, b) at 16 + a*S1 + b*S2 holds word k =
+  // {s(q_{k+1}, a), s(q_{k+1}, b)} (f16 halves; rows past the query -2048) and the row-0 word
+  // 4 bytes before it.  S2/16 = 1 and S1/16 = 4 (mod 16) put the 16 A/C/G/T slots on 16
+  // different 4-bank LDS groups.
+  std::vector<uint32_t> tpair;
+  uint32_t pS1 = 0, pS2 = 0;
+  if (f16 && !prof && !gotoh && !col0 && R == 32 && segs.size() == 1 && segs[0].W <= 4 &&
+      A == SW_DNA_ALPHA) {
+    const uint32_t NR = (uint32_t)segs[0].W * R, B = 4 * NR;
+    pS2 = (B + 15) / 16 * 16;
+    while ((pS2 / 16) % 16 != 1) pS2 += 16;
+    pS1 = (4 * pS2 + B + 15) / 16 * 16;
+    while ((pS1 / 16) % 16 != 4) pS1 += 16;
+    const uint32_t bytes = 16 + 4 * pS1 + 4 * pS2 + B;
+    tpair.assign(bytes / 4, 0xE800E800u);
+    auto word = [&](int r, int x, int y) -> uint32_t {  // row r of the segment, letters x, y
+      if (r >= qlen) return 0xE800E800u;
+      const int q = b->query[r];
+      return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)m[q * A + x]) |
+             (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)m[q * A + y]) << 16;
+    };
+    for (int x = 0; x < A; ++x)
+      for (int y = 0; y < A; ++y) {
+        const uint32_t base = (16 + x * pS1 + y * pS2) / 4;
+        for (uint32_t k = 0; k + 1 < NR; ++k) tpair[base + k] = word((int)k + 1, x, y);
+      }
+    for (int x = 0; x < A; ++x)  // row-0 words last: they may reuse word NR-1 of a slot
+      for (int y = 0; y < A; ++y) tpair[(16 + x * pS1 + y * pS2) / 4 - 1] = word(0, x, y);
+  }
   // wave-kernel layout of the same query: rows padded to 64K; queries past 1024 rows run as
   // 1024-row segments (K = 16), one table per segment, concatenated
   std::vector<uint32_t> wt, wt16;
@@ -594,7 +632,7 @@ static sw_status prepare(sw_bank* b) {
   }
   // the previous upload must have left the staging buffer before it is refilled
   HIPOK(b, hipEventSynchronize(b->ev_ready));
-  const size_t nbytes = (wt16.size() + wt.size() + tab.size() + tab16.size()) * 4;
+  const size_t nbytes = (wt16.size() + wt.size() + tab.size() + tab16.size() + tpair.size()) * 4;
   HIPOK(b, b->stage.reserve(nbytes));
   // earlier launches (any stream) must be done reading the tables this upload overwrites
   HIPOK(b, hipStreamWaitEvent(b->stream, b->ev_used, 0));
@@ -617,6 +655,10 @@ static sw_status prepare(sw_bank* b) {
   b->wseg_words16 = wt16.empty() ? 0 : wt16.size() / wsegs;
   HIPOK(b, upload(b->qtab, tab));
   if (f16) HIPOK(b, upload(b->qtab16, tab16));
+  if (!tpair.empty()) HIPOK(b, upload(b->qpair, tpair));
+  b->pair_bytes = (uint32_t)tpair.size() * 4;
+  b->pS1 = pS1;
+  b->pS2 = pS2;
   HIPOK(b, hipEventRecord(b->ev_ready, b->stream));
   b->f16 = f16;
   b->nv16 = (uint32_t)hN * 0x01010101u;
@@ -717,6 +759,8 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   // the f16 wave kernel carries profile offsets in 16-bit halves (24 letters + pad fit)
   if (use_f16 && b->prof && (size_t)(b->alpha + 1) * b->wPS16 > 65536) use_wave = false;
   const char* arith = opt16 ? "f16+u16-rescore" : use_f16 ? "f16" : "u16";
+  // the f16 pass of the tile kernel reads the letter-pair table when the query has one
+  const bool use_pair = use_f16 && b->pair_bytes != 0 && env_int("SWBANK_PAIR", 1) != 0;
   if (use_wave) {
     snprintf(b->last_kernel, sizeof(b->last_kernel), "wave %s%s K=%d segs=%d", arith,
              b->prof ? "-profile" : "", b->wK, b->wsegs);
@@ -747,7 +791,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
     }
   } else {
     snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=%zu", arith,
-             b->prof ? "-profile" : "", b->R, b->segs[0].W, nseg);
+             b->prof ? "-profile" : use_pair ? " pair" : "", b->R, b->segs[0].W, nseg);
   }
   // Segmented queries hand each segment's bottom row to the next through HBM: ntiles x ecols
   // x 512 B per edge buffer.  Past SWBANK_EDGE_MB (default 2048) the batch runs as
@@ -800,14 +844,17 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
       for (size_t s = 0; s < nseg; ++s) {
         const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
         void* eout = s + 1 < nseg ? b->edge[s & 1].p : nullptr;
+        const bool pair = f16 && use_pair;
         HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof, gotoh ? 1 : 0, f16 ? 1 : 0, res,
                                   offs, lens, np,
-                                  f16 ? b->qtab16.p + b->segs[s].off16
-                                      : b->qtab.p + b->segs[s].off,
+                                  pair ? b->qpair.p
+                                  : f16 ? b->qtab16.p + b->segs[s].off16
+                                        : b->qtab.p + b->segs[s].off,
                                   f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
-                                  f16 && b->prof ? b->PS16 : b->PS, b->pad, b->segs[s].W,
-                                  scores, ein, eout, ecols, s > 0 ? 1 : 0, packed ? 1 : 0, idx,
-                                  nidx, (uint32_t)p0, st));
+                                  pair ? b->pair_bytes : f16 && b->prof ? b->PS16 : b->PS,
+                                  b->pad, b->segs[s].W, scores, ein, eout, ecols, s > 0 ? 1 : 0,
+                                  packed ? 1 : 0, idx, nidx, (uint32_t)p0, pair ? 1 : 0, b->pS1,
+                                  b->pS2, st));
       }
     }
   }

@@ -404,22 +404,36 @@ __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t
   Lane2 t;
   size_t a = (size_t)tile * SWB_TILE + lane, b = a + 64;
   const bool va = a < n, vb = b < n;  // positions in the batch
+  // A lane past the batch end reads the tile's first target (position tile*128 always
+  // exists): its codes are discarded, but the full-chunk loads (8 bytes while every valid
+  // lane has >= 8 codes left) must stay inside a real target.
+  // A workgroup whose first tile lies past the batch end (the device-side count of an index
+  // list can be far below the launch size) dereferences nothing but lens[0] / record 0.
+  const size_t p0 = (size_t)tile * SWB_TILE;
+  if (p0 >= n) {
+    t.llo = t.lhi = 0u;
+    t.plo = t.phi = packed ? res + 6 : reinterpret_cast<const uint8_t*>(lens);
+    return t;
+  }
+  if (!va) a = p0;
+  if (!vb) b = p0;
   if (idx) {
-    a = va ? idx[a] : 0;
-    b = vb ? idx[b] : 0;
+    a = idx[a];
+    b = idx[b];
   }
   if (packed) {
     t.llo = va ? *reinterpret_cast<const uint16_t*>(res + a * SWB_RECORD + 4) : 0u;
     t.lhi = vb ? *reinterpret_cast<const uint16_t*>(res + b * SWB_RECORD + 4) : 0u;
-    t.plo = res + (va ? a : 0) * SWB_RECORD + 6;
-    t.phi = res + (vb ? b : 0) * SWB_RECORD + 6;
+    t.plo = res + a * SWB_RECORD + 6;
+    t.phi = res + b * SWB_RECORD + 6;
     return t;
   }
-  t.llo = va ? lens[a] : 0u;
-  t.lhi = vb ? lens[b] : 0u;
+  const uint32_t la = lens[a], lb = lens[b];
+  t.llo = va ? la : 0u;
+  t.lhi = vb ? lb : 0u;
   // an empty target still needs a readable address for the branch-free slow path
-  t.plo = t.llo ? res + offs[a] : reinterpret_cast<const uint8_t*>(lens);
-  t.phi = t.lhi ? res + offs[b] : reinterpret_cast<const uint8_t*>(lens);
+  t.plo = la ? res + offs[a] : reinterpret_cast<const uint8_t*>(lens);
+  t.phi = lb ? res + offs[b] : reinterpret_cast<const uint8_t*>(lens);
   return t;
 }
 
@@ -434,7 +448,8 @@ __device__ __forceinline__ void tile_chunks(const Lane2& t, size_t tlo, size_t t
     Lmin = min(Lmin, (uint32_t)__shfl_xor((int)Lmin, off));
   }
   nch = max(1, (int)((__builtin_amdgcn_readfirstlane(Lmax) + 7) / 8));
-  nfull = (int)(__builtin_amdgcn_readfirstlane(Lmin) / 8);
+  const uint32_t lm = __builtin_amdgcn_readfirstlane(Lmin);
+  nfull = lm == ~0u ? 0 : (int)(lm / 8);  // no valid lane (a tile past the end): no full loads
 }
 
 // Kernel arguments (one struct, passed by value).
@@ -462,6 +477,8 @@ struct ScoreArgs {
   const uint32_t* idx;
   const uint32_t* nidx;   // with idx: positions [0, min(n, *nidx - idx_base)) are valid
   uint32_t idx_base;
+  // PAIR (f16 DNA merged): letter-pair table strides; slot (a, b) at 16 + a*pS1 + b*pS2
+  uint32_t pS1, pS2;
 };
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -499,20 +516,29 @@ __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens
 // RTL's PE-to-PE registers).  A wave that finishes its part of the k-th tile folds its running
 // max into bestsh[k % W]; the last wave, which finishes that tile W-1 phases after wave 0,
 // writes the scores and clears the slot (wave 0 reuses it for tile k + W, >= W phases later).
-// LDS: bestsh[W][128] | bnd[64] | sink[8][64] | ein[2][8][64] (segments) |
-//      ring[(W-1)][2][8][64] {H~, G or F} | PROF: profile
-template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16>
+// LDS: PAIR: pair table (PS bytes) | bestsh[W][128] | bnd[64] | sink[8 or 1][64] |
+//      ein[2][8][64] (segments) | ring[(W-1)][2][8][64] {H~, G or F} | PROF: profile
+//
+// PAIR (DNA, merged gaps, f16): the substitution words come from an LDS table of letter
+// pairs instead of a v_perm per row.  Slot (a, b) (a = code of the low target, b = of the
+// high target) holds word k = {s(q_{k+1}, a), s(q_{k+1}, b)} as f16 halves at
+// 16 + a*pS1 + b*pS2 + 4k, and {s(q_0, a), s(q_0, b)} 4 bytes before it; the strides put the
+// 16 A/C/G/T slots on 16 different 4-bank groups (conflict-free ds_read_b128).  A column of
+// wave w reads its row words as 4 blocks of 8 (two ds_read_b128 each), one block ahead of
+// the asm block that consumes them: 6.5 VALU per 2 cells instead of 7.5.
+template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
   constexpr int C = 8;
+  static_assert(!PAIR || (R == 32 && F16 && !PROF && !GOTOH && !COL0), "PAIR: f16 merged R=32");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int W = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
   const bool seg_in = a.edge_in != nullptr, seg_out = a.edge_out != nullptr;
-  uint32_t* bestsh = smem;                                       // W x 128 words
-  uint2* bnd = reinterpret_cast<uint2*>(smem + W * SWB_TILE);    // row -1 boundary
+  uint32_t* bestsh = smem + (PAIR ? a.PS / 4 : 0);               // W x 128 words
+  uint2* bnd = reinterpret_cast<uint2*>(bestsh + W * SWB_TILE);  // row -1 boundary
   uint2* sink = bnd + 64;                                        // last wave's bottom row
-  uint2* ein = sink + C * 64;                                    // previous segment, 2 x 8 cols
+  uint2* ein = sink + (seg_out ? C * 64 : 64);                   // previous segment, 2 x 8 cols
   uint2* ring = ein + (seg_in ? 2 * C * 64 : 0);
   uint8_t* prof = reinterpret_cast<uint8_t*>(ring + (size_t)(W > 1 ? W - 1 : 0) * 2 * C * 64);
 
@@ -546,8 +572,12 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       dma_edge_chunk(a.edge_in + (size_t)tile * a.ecols * 64, ein, lane);
   }
   uint32_t nv = a.nv;
-  uint32_t tab[PROF ? 1 : R];
-  if constexpr (PROF) {
+  uint32_t tab[PROF || PAIR ? 1 : R];
+  if constexpr (PAIR) {
+    const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
+    for (uint32_t i = threadIdx.x; i < a.PS / 16; i += blockDim.x)
+      reinterpret_cast<uint4*>(smem)[i] = src[i];
+  } else if constexpr (PROF) {
     // query profile -> LDS (the ScoringModule's query + penalty registers)
     const uint32_t words = (a.pad + 1) * a.PS / 16;
     const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
@@ -580,6 +610,33 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   uint2 rlo, rhi;      // raw codes of the next chunk (prefetched one phase ahead)
   load_raw(cur, 0, nfull > 0, a.pad, packed, rlo, rhi);
   __syncthreads();
+
+  // PAIR: column state one column ahead: acur = this column's table address (slot + this
+  // wave's rows - 16), pA = its first 8 row words, pw = its row-0 word
+  const char* lp = reinterpret_cast<const char*>(smem);
+  const auto ld4 = [lp](uint32_t off) { return *reinterpret_cast<const uint4*>(lp + off); };
+  // the row-0 word: a relaxed atomic load, so LLVM does not merge it with the neighbouring
+  // 16-B reads (it splits them into ds_read2_b32 pairs otherwise)
+  const auto ld1 = [lp](uint32_t off) {
+    return __atomic_load_n(reinterpret_cast<const uint32_t*>(lp + off), __ATOMIC_RELAXED);
+  };
+  const uint32_t wofs = (uint32_t)wave * R * 4;
+  // codes clamped to N: lanes past the batch end (and codes >= 5 on the device API) would
+  // otherwise pick a slot outside the table, and a slot feeds both halves (one v_min each,
+  // SDWA byte-select)
+  const auto pair_addr = [&](uint32_t wl, uint32_t wh, int sh) {
+    return __umul24(min((wl >> sh) & 0xFFu, 4u), a.pS1) +
+           __umul24(min((wh >> sh) & 0xFFu, 4u), a.pS2) + wofs;
+  };
+  uint32_t acur = 0, pw = 0;
+  uint4 pA0 = {0, 0, 0, 0}, pA1 = {0, 0, 0, 0};
+  if constexpr (PAIR) {
+    acur = pair_addr(rlo.x, rhi.x, 0);
+    pA0 = ld4(acur + 16);
+    pA1 = ld4(acur + 32);
+    pw = ld1(acur + 12);
+  }
+  (void)pA0; (void)pA1; (void)pw; (void)acur; (void)wofs;
 
   // branch-free hand-off: wave 0 reads the top boundary (constant, stride 0, or the previous
   // segment's row), the last wave writes into an LDS sink (branches inside the column loop
@@ -675,6 +732,49 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           } else {
             column_merged<R, RB, false>(lk, diag, upX, Hl, Xl, best, S2, O2, E2);
           }
+        } else if constexpr (PAIR) {
+          // the next column's table address (its codes: this chunk, or byte 0 of the next)
+          const uint32_t nwl = jj + 1 < C ? (jj + 1 < 4 ? clo.x : clo.y) : rlo.x;
+          const uint32_t nwh = jj + 1 < C ? (jj + 1 < 4 ? chi.x : chi.y) : rhi.x;
+          const int nsh = jj + 1 < C ? 8 * ((jj + 1) & 3) : 0;
+          uint32_t Da, Db, X, DN, IN;
+          const uint32_t noe = as_u32(as_u16x2(NOE2)), ne = as_u32(as_u16x2(NE2));
+          u16x2 bst = best;
+#define SWK_PAIR_OUT(B, DA)                                                                   \
+  [h0] "+v"(Hl[B]), [h1] "+v"(Hl[B + 1]), [h2] "+v"(Hl[B + 2]), [h3] "+v"(Hl[B + 3]),          \
+      [h4] "+v"(Hl[B + 4]), [h5] "+v"(Hl[B + 5]), [h6] "+v"(Hl[B + 6]), [h7] "+v"(Hl[B + 7]),  \
+      [t0] "+v"(Xl[B]), [t1] "+v"(Xl[B + 1]), [t2] "+v"(Xl[B + 2]), [t3] "+v"(Xl[B + 3]),      \
+      [t4] "+v"(Xl[B + 4]), [t5] "+v"(Xl[B + 5]), [t6] "+v"(Xl[B + 6]), [t7] "+v"(Xl[B + 7]),  \
+      [Da] DA(Da), [Db] "=&v"(Db), [X] "=&v"(X), [DN] "=&v"(DN), [IN] "=&v"(IN),              \
+      [best] "+v"(bst)
+#define SWK_PAIR_IN(P0, P1, UP)                                                               \
+  [p0] "v"(P0.x), [p1] "v"(P0.y), [p2] "v"(P0.z), [p3] "v"(P0.w), [p4] "v"(P1.x),             \
+      [p5] "v"(P1.y), [p6] "v"(P1.z), [p7] "v"(P1.w), [up] "v"(UP), [noe] "s"(noe),           \
+      [ne] "s"(ne)
+          uint4 pB0 = ld4(acur + 48), pB1 = ld4(acur + 64);  // block 1
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile(SWK_F16PAIR_F
+                       : SWK_PAIR_OUT(0, "=&v")
+                       : SWK_PAIR_IN(pA0, pA1, upX), [dg] "v"(diag), [pw] "v"(pw));
+          pA0 = ld4(acur + 80);  // block 2
+          pA1 = ld4(acur + 96);
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile(SWK_F16PAIR_M : SWK_PAIR_OUT(8, "+v") : SWK_PAIR_IN(pB0, pB1, Xl[7]));
+          pB0 = ld4(acur + 112);  // block 3
+          pB1 = ld4(acur + 128);
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile(SWK_F16PAIR_M : SWK_PAIR_OUT(16, "+v") : SWK_PAIR_IN(pA0, pA1, Xl[15]));
+          acur = pair_addr(nwl, nwh, nsh);  // next column: block 0 and row-0 word
+          pA0 = ld4(acur + 16);
+          pA1 = ld4(acur + 32);
+          pw = ld1(acur + 12);
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile(SWK_F16PAIR_L : SWK_PAIR_OUT(24, "+v") : SWK_PAIR_IN(pB0, pB1, Xl[23]));
+#undef SWK_PAIR_OUT
+#undef SWK_PAIR_IN
+          (void)Db; (void)X; (void)DN; (void)IN;
+          best = bst;
+          upX = Xl[R - 1];
         } else if constexpr (F16) {
           // selector bytes {0x0C, code_lo, 0x0C, code_hi}: the LUT byte is the f16 high byte
           const uint32_t sel16 = 0x0Cu | ((uint32_t)(jj & 3) << 8) | (0x0Cu << 16) |
@@ -771,14 +871,14 @@ static unsigned persistent_grid(const void* fn, size_t ntiles, int threads, size
   return (unsigned)((ntiles + rounds - 1) / rounds);
 }
 
-template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16>
+template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false>
 static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st) {
   const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE;
   const size_t lds = (size_t)W * SWB_TILE * 4 +
-                     (size_t)(64 + 8 * 64 + (a.edge_in ? 2 * 8 * 64 : 0) +
+                     (size_t)(64 + (a.edge_out ? 8 * 64 : 64) + (a.edge_in ? 2 * 8 * 64 : 0) +
                               (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8 +
-                     (PROF ? prof_bytes : 0);
-  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16>;
+                     (PROF ? prof_bytes : 0) + (PAIR ? a.PS : 0);
+  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -1246,13 +1346,19 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                        const void* edge_in, void* edge_out, uint32_t ecols,
                                        int accum, int packed, const uint32_t* idx,
-                                       const uint32_t* nidx, uint32_t idx_base, hipStream_t st) {
+                                       const uint32_t* nidx, uint32_t idx_base, int pair,
+                                       uint32_t pS1, uint32_t pS2, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                          O,    E,    PS,   pad, scores, static_cast<const uint2*>(edge_in),
                          static_cast<uint2*>(edge_out), ecols, (uint32_t)accum, (uint32_t)packed,
-                         idx, nidx, idx_base};
+                         idx, nidx, idx_base, pS1, pS2};
   const uint32_t prof_bytes = (pad + 1) * PS;
+  if (pair) {  // PS = pair-table bytes
+    if (R == 32 && f16 && !prof && !gotoh && !col0)
+      return swk::launch_score<32, 4, false, false, false, true, true>(a, W, 0, st);
+    return hipErrorInvalidValue;
+  }
 #define SWK_CASE(RR, BB, C0, PF, GT, FH)                                                      \
   if (R == RR && RB == BB && col0 == C0 && prof == PF && gotoh == GT && f16 == FH)            \
     return swk::launch_score<RR, BB, (C0 != 0), (PF != 0), (GT != 0), (FH != 0)>(a, W,        \

@@ -15,16 +15,18 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["tile", "tile-u16", "wave", "wave-u16"])
+@pytest.fixture(autouse=True, params=["tile", "tile-lut", "tile-u16", "wave", "wave-u16"])
 def kernel_choice(request, monkeypatch):
     """Run every parity test through each score kernel: the tile kernel (waves = row blocks,
     lanes = targets) and the wave kernel (lanes = rows, DPP hand-off), each with its f16
     arithmetic where eligible ("tile", "wave": exact below the f16 bound, optimistic with a
-    u16 re-score above it) and forced to u16 ("-u16").  Past 1024 rows the wave kernel runs
-    the query as 1024-row segments."""
+    u16 re-score above it) and forced to u16 ("-u16").  "tile" takes the letter-pair table
+    for DNA queries of <= 128 rows; "tile-lut" forces the per-row LUT lookup instead.  Past
+    1024 rows the wave kernel runs the query as 1024-row segments."""
     kern = request.param.split("-")[0]
     monkeypatch.setenv("SWBANK_KERNEL", kern)
     monkeypatch.setenv("SWBANK_F16", "0" if request.param.endswith("-u16") else "1")
+    monkeypatch.setenv("SWBANK_PAIR", "0" if request.param.endswith("-lut") else "1")
     return request.param
 
 
@@ -148,7 +150,7 @@ def test_f16_bound_edges(bank, qlen, match, kernel_choice):
     res, offs, lens = O.pack_residues(seqs)
     want = O.score_batch(q, res, offs, lens, O.dna_matrix(match, -4), -12, -4)
     assert got[0] == match * qlen
-    if kernel_choice == "tile":
+    if kernel_choice in ("tile", "tile-lut"):
         # exact f16 within the bound; past it optimistic f16 with a u16 re-score of the pairs
         # above 2048 - max(s); a score with a non-zero f16 low byte (9) cannot use the
         # one-byte LUT and runs on the 2-byte f16 profile instead
@@ -343,7 +345,7 @@ def test_f16_gotoh_and_profile_paths(case, kernel_choice):
         want = O.score_batch(q, res, offs, lens, sub, go, ge, model)
         assert (got == want).all(), (kern, np.nonzero(got != want)[0][:5])
         smax = 5 if dna else 11
-        if kernel_choice == "tile":
+        if kernel_choice in ("tile", "tile-lut"):
             f16 = min(qlen, max(lens)) * smax + smax <= 2048
             assert kern.startswith("tile f16" + ("" if f16 else "+u16-rescore")), kern
         elif kernel_choice == "tile-u16":
@@ -505,3 +507,74 @@ def test_back_to_back_queries_on_a_user_stream():
         want = O.score_batch(qq, tg.reshape(-1), offs, np.full(len(idx), L, np.uint32),
                              O.dna_matrix(), -12, -4)
         assert (got[k][idx] == want).all(), k
+
+
+@pytest.mark.parametrize("qlen", [1, 8, 31, 32, 33, 64, 97, 127, 128])
+@pytest.mark.parametrize("params", [REF, (2, -3, -5, -2), (4, 0, -8, -2)])
+def test_pair_table_path(bank, qlen, params, kernel_choice):
+    """The letter-pair table (tile f16, DNA merged gaps, queries of 17-128 rows): all 25 letter
+    pairs incl. N on both sides (dense N), ragged lengths, several workgroup heights, and the
+    path assertion: "tile" takes the pair table, "tile-lut" the per-row LUT."""
+    rng = np.random.default_rng(qlen * 31 + params[0])
+    q, seqs = _random_case(rng, qlen, 300, 180, p_n=0.25)
+    seqs += [q.copy() for _ in range(3)]
+    bank.set_penalties(*params)
+    bank.load_query(q)
+    got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(params[0], params[1]), params[2],
+                         params[3])
+    kern = bank.last_kernel()
+    assert (got == want).all(), (kern, [(i, int(got[i]), int(want[i]))
+                                        for i in np.nonzero(got != want)[0][:8]])
+    if kernel_choice == "tile" and qlen > 16:  # <= 16 rows: the R = 16 LUT kernel
+        assert kern.startswith("tile f16 pair R=32"), kern
+    elif kernel_choice == "tile-lut":
+        assert kern.startswith("tile f16 R=") and "pair" not in kern, kern
+
+
+@pytest.mark.parametrize("qlen", [32, 64, 128])
+@pytest.mark.parametrize("tail", [1, 10, 63, 64, 65, 121, 127])
+def test_partial_last_tile_full_chunks(bank, qlen, tail):
+    """A last tile whose high-half lanes lie past the batch end while every valid target is
+    long (whole 8-code chunks for all valid lanes): the lanes past the end must not disturb
+    their low-half partners (the pair table feeds both halves from one slot)."""
+    rng = np.random.default_rng(qlen + 1000 * tail)
+    q = rng.integers(0, 4, qlen, dtype=np.uint8)
+    seqs = [rng.integers(0, 4, int(rng.integers(96, 120)), dtype=np.uint8)
+            for _ in range(3 * 128 + tail)]
+    bank.set_penalties(*REF)
+    bank.load_query(q)
+    got = bank.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)
+    assert (got == want).all(), [(i, int(got[i]), int(want[i]))
+                                 for i in np.nonzero(got != want)[0][:8]]
+
+
+def test_device_codes_past_n_read_as_n(bank):
+    """Device API: codes 5..7 (not validated there) score like N (code 4) in every kernel."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(5)
+    q, seqs = _random_case(rng, 100, 300, 150, p_n=0.0)
+    res, offs, lens = O.pack_residues(seqs)
+    hit = rng.random(len(res)) < 0.1
+    res_hi = res.copy()
+    res_hi[hit] = rng.integers(5, 8, int(hit.sum()))
+    res_n = res.copy()
+    res_n[hit] = 4
+    bank.set_penalties(*REF)
+    bank.load_query(q)
+    out = []
+    for r in (res_hi, res_n):
+        dev = torch.device("cuda", 0)
+        d_res = torch.from_numpy(r).to(dev)
+        d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
+        d_lens = torch.from_numpy(lens.astype(np.int32)).to(dev)
+        d_sc = torch.zeros(len(lens), dtype=torch.int32, device=dev)
+        bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), len(lens),
+                                int(lens.max()), d_sc.data_ptr(), 0)
+        torch.cuda.synchronize()
+        out.append(d_sc.cpu().numpy())
+    assert (out[0] == out[1]).all()
+    assert (out[1] == O.score_batch(q, res_n, offs, lens, O.dna_matrix(), -12, -4)).all()
