@@ -41,7 +41,7 @@ def mean_counter(name):
 summary = {"workload": workload}
 for c in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
           "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE", "SQ_INSTS_LDS",
-          "SQ_INSTS_SALU"):
+          "SQ_INSTS_SALU", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAIT_INST_LDS"):
     v = mean_counter(c)
     if v is not None:
         summary[c] = v

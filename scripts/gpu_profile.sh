@@ -15,7 +15,8 @@ rc=$?; echo "trace rc=$rc"; tail -1 "$OUT/prof_$TAG.log"
 if [ $rc -ne 0 ]; then exit $rc; fi
 for pass in "FETCH_SIZE" "WRITE_SIZE" \
             "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
-            "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY" ; do
+            "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY" \
+            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS" ; do
   name=$(echo $pass | cut -d' ' -f1)
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $pass --output-format csv \
     -d "$OUT/pmc_$TAG/$name" -o pmc -- python3 "$ROOT/bench.py" --profile-only --steps 3 --warmup 1 "$@" \
