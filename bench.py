@@ -46,13 +46,13 @@ HBM_PEAK_GBS = 8000.0
 # several algorithmic ops into one instruction, so frac > 1 is possible.
 # Issue bound: one instruction advances one query row for a lane's 2 targets (128 cells per
 # wave-instruction); instructions per row of the column body (csrc/swbank_kernels.hip):
-# f16 merged 7.5 (6.5 with the letter-pair table: no v_perm per row), f16 Gotoh 8.5, u16
+# f16 merged 6.5 (5.5 with the letter-pair table: no v_perm per row), f16 Gotoh 8.5, u16
 # merged 9, u16 Gotoh 11 (the column body both kernels share; the tile kernel adds 0.1-0.7 per
 # row of loop overhead, the wave kernel ~7 per step of K rows plus the 63-step lane skew).
 OPS_PER_CELL = {"merged": 10, "gotoh": 11}
 VALU_PEAK_TOPS_16 = CUS * SIMD_PER_CU * 16 * 2 * CLK_GHZ / 1e3  # 78.6
 VALU_ISSUE_PER_SIMD_CLK = 0.25
-VALU_INSTR_PER_ROW = {"f16": 7.5, "f16-pair": 6.5, "f16-gotoh": 8.5, "u16": 9.0,
+VALU_INSTR_PER_ROW = {"f16": 6.5, "f16-pair": 5.5, "f16-gotoh": 8.5, "u16": 9.0,
                       "u16-gotoh": 11.0}
 
 

@@ -2,15 +2,16 @@
 """Generate csrc/swbank_f16_rows.inc: asm text for one 8-row block of the f16 tile-kernel
 column, for both gap models and both substitution lookups.
 
-Merged gap matrix (the ScoreBank PE), per row with D = H(i-1,j-1) + s already computed:
+Merged gap matrix (the ScoreBank PE), scores as f16 multiples of 2^-11 so that the packed
+add's [0, 1] clamp is max(0, x); per row, with M = max(0, H(i-1,j-1) + s) already computed:
 
-    s'  = v_perm(...)                 substitution word of the next row (VOP3)
-    I   = max(Tup, Tl)                v_pk_maximum3_f16 (2-input form)
-    DN  = D + (-o-e)
-    D'  = Hl(old) + s'                next row's D
-    IN  = I + (-e)
-    H   = max(D, 0, I)       -> Hl
-    T   = max(DN, -o-e, IN)  -> Tl    (T = G - e: what the right and lower cells read)
+    s'  = v_perm(...)                 substitution word of the next row (VOP3; LUT/profile)
+    MO  = M + (-o)
+    T   = X(prev row) + (-e)   -> Tl  T of the previous row (= G - e: what the right and lower
+                                      cells read), written one group late
+    M'  = clamp(Hl(old) + s')         next row's M
+    H   = max(M, Tup, Tl)      -> Hl  (= max(M, I), I = max(Tup, Tl))
+    X   = max(MO, Tup, Tl)            G = max(M - o, I)
     best = max(best, H(prev row), H)  every second row
 
 Gotoh (ssearch36), E and F one step ahead and floored at 0:
@@ -32,7 +33,7 @@ target letters' profile words in VGPRs and a per-parity selector in an SGPR.
 No two dependent packed (VOP3P) ops are adjacent (gfx950 needs a wait state between them;
 v_perm_b32 -> VOP3P needs none), so a block needs no s_nop inside; LLVM adds one wait state
 per asm block.  D alternates between Da/Db by row parity.  The last block of a column ends
-with a row that has no successor: it starts with `s_nop 0` instead of the perm.
+with a row that has no successor: `s_nop 0` stands in for its next-row add.
 usage: python scripts/gen_f16_rows.py   (rewrites the .inc)
 """
 import os
@@ -51,21 +52,39 @@ def perm(mode, i):
 
 
 def merged_block(mode, zdown, last, nrows=8):
+    """Merged gap matrix with the clamp modifier: values are f16 multiples of 2^-11, so the
+    [0, 1] clamp of v_pk_add_f16 is max(0, x) on everything the exact path reaches, and the
+    diagonal add yields M = max(0, H(i-1,j-1) + s) directly.  Then I = max(Tup, Tl) never has
+    to be formed on its own: H = max(M, Tup, Tl) and G = max(M - o, Tup, Tl) are one max3 each
+    and T = G - e.  5.5 VALU per 2 cells (+ the substitution lookup).  T of row i is written
+    one group late (after the next row's M - o), so no two dependent packed ops are adjacent.
+    mode "L"/"P": perm lookups into S1; "pair": ready-made words p{i} (no lookup)."""
     out = []
     for i in range(nrows):
         dcur, dnext = ("%[Da]", "%[Db]") if i % 2 == 0 else ("%[Db]", "%[Da]")
         up = "%[up]" if i == 0 else ("%[noe]" if zdown else f"%[t{i - 1}]")
         final = last and i == nrows - 1
-        out.append("s_nop 0" if final else perm(mode, i))
-        out.append(f"v_pk_maximum3_f16 %[X], {up}, %[t{i}], %[t{i}]")
-        out.append(f"v_pk_add_f16 %[DN], {dcur}, %[noe]")
-        if not final:
-            out.append(f"v_pk_add_f16 {dnext}, %[h{i}], %[S1]")
-        out.append("v_pk_add_f16 %[IN], %[X], %[ne]")
-        out.append(f"v_pk_maximum3_f16 %[h{i}], {dcur}, 0, %[X]")
-        out.append(f"v_pk_maximum3_f16 %[t{i}], %[DN], %[noe], %[IN]")
+        if final:
+            nxt = ["s_nop 0"]
+        elif mode == "pair":
+            nxt = [f"v_pk_add_f16 {dnext}, %[h{i}], %[p{i}] clamp"]
+        else:
+            out.append(perm(mode, i))
+            nxt = [f"v_pk_add_f16 {dnext}, %[h{i}], %[S1] clamp"]
+        if i == 0:
+            out += nxt
+            out.append(f"v_pk_add_f16 %[DN], {dcur}, %[no]")
+        else:
+            out.append(f"v_pk_add_f16 %[DN], {dcur}, %[no]")
+            out.append(f"v_pk_add_f16 %[t{i - 1}], %[X], %[ne]")
+            out += nxt
+        out.append(f"v_pk_maximum3_f16 %[h{i}], {dcur}, {up}, %[t{i}]")
+        out.append(f"v_pk_maximum3_f16 %[X], %[DN], {up}, %[t{i}]")
         if i % 2 == 1:
             out.append(f"v_pk_maximum3_f16 %[best], %[best], %[h{i - 1}], %[h{i}]")
+    if nrows % 2 == 1:
+        out.append("s_nop 0")
+    out.append(f"v_pk_add_f16 %[t{nrows - 1}], %[X], %[ne]")
     return out
 
 
@@ -93,23 +112,10 @@ def gotoh_block(mode, last, nrows=8):
 def pair_block(first, last, nrows=8):
     """Pair-profile block (DNA, merged gaps): the substitution words of both targets come
     ready-made from an LDS table of letter pairs, word p{i} = s(row i+1) for (lo, hi), so
-    there is no v_perm per row: 6.5 VALU per 2 cells.  Da carries D of the block's first row
+    there is no v_perm per row: 5.5 VALU per 2 cells.  Da carries M of the block's first row
     in and of the next block's first row out; the first block computes it from dg + pw."""
-    out = ["v_pk_add_f16 %[Da], %[dg], %[pw]"] if first else []
-    for i in range(nrows):
-        dcur, dnext = ("%[Da]", "%[Db]") if i % 2 == 0 else ("%[Db]", "%[Da]")
-        up = "%[up]" if i == 0 else f"%[t{i - 1}]"
-        final = last and i == nrows - 1
-        out.append("s_nop 0" if final else f"v_pk_add_f16 {dnext}, %[h{i}], %[p{i}]")
-        out.append(f"v_pk_maximum3_f16 %[X], {up}, %[t{i}], %[t{i}]")
-        out.append(f"v_pk_add_f16 %[DN], {dcur}, %[noe]")
-        out.append("v_pk_add_f16 %[IN], %[X], %[ne]")
-        out.append(f"v_pk_maximum3_f16 %[h{i}], {dcur}, 0, %[X]")
-        out.append(f"v_pk_maximum3_f16 %[t{i}], %[DN], %[noe], %[IN]")
-        if i % 2 == 1:
-            out.append(f"v_pk_maximum3_f16 %[best], %[best], %[h{i - 1}], %[h{i}]")
-    return out
-
+    out = ["v_pk_add_f16 %[Da], %[dg], %[pw] clamp"] if first else []
+    return out + merged_block("pair", False, last, nrows)
 
 def fmt(lines):
     return "".join(f'  "{ln}\\n\\t" \\\n' for ln in lines) + '  ""\n'

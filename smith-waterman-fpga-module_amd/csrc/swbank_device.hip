@@ -235,6 +235,12 @@ struct sw_bank {
   std::vector<Ev> events;
 };
 
+// Scores in the f16 kernels are f16 multiples of 2^-11 (x as x/2048, swbank_kernels.hip), so
+// the packed add's [0, 1] clamp is max(0, x); -2048 (padding rows / letters) is 0xBC00.
+static inline uint16_t f16_score_bits(int v) {
+  return __builtin_bit_cast(uint16_t, (_Float16)((float)v * (1.0f / 2048.0f)));
+}
+
 static sw_status fail(sw_bank* b, sw_status st, const char* fmt, ...) {
   if (b) {
     va_list ap;
@@ -424,7 +430,7 @@ static sw_status prepare(sw_bank* b) {
   // (2-byte f16 entries) when f16 applies at all: faster than the u16 LUT kernel.
   bool lut_f16 = true;
   for (int i = 0; i < A * A; ++i) {
-    const uint16_t bits = __builtin_bit_cast(uint16_t, (_Float16)(float)m[i]);
+    const uint16_t bits = f16_score_bits(m[i]);
     lut_f16 = lut_f16 && (bits & 0xFFu) == 0;
   }
   const bool f16_range = -(o + 2 * e + (std::max(0, smax) - smin)) >= -2048;
@@ -491,10 +497,10 @@ static sw_status prepare(sw_bank* b) {
   // f16 variant of the LUT: each substitution score must be an f16 whose low byte is 0
   // (|s| <= 8 or a coarser even value), so the byte perm yields the exact f16 bits
   auto f16_hi = [](int v, uint8_t* out) {
-    const _Float16 h = (_Float16)(float)v;
-    const uint16_t bits = __builtin_bit_cast(uint16_t, h);
+    const uint16_t bits = f16_score_bits(v);
     *out = (uint8_t)(bits >> 8);
-    return (bits & 0xFFu) == 0 && (int)(float)h == v;
+    return (bits & 0xFFu) == 0 &&
+           (int)((float)__builtin_bit_cast(_Float16, bits) * 2048.0f) == v;
   };
   // LUT mode: one byte per entry (the f16 high byte); profile mode: two bytes (any |s| <= 127
   // is an exact f16), row stride PS16 = 2 x rows, 16 mod 256 like PS
@@ -510,7 +516,7 @@ static sw_status prepare(sw_bank* b) {
     }
   }
   if (f16 && !prof) {
-    tab16.assign(tab.size(), 0xE8E8E8E8u);  // padding rows: -2048
+    tab16.assign(tab.size(), 0xBCBCBCBCu);  // padding rows: -2048
     for (sw_bank::Seg& sg : segs) {
       const int r0 = (int)(&sg - segs.data()) * seg_rows;
       sg.off16 = sg.off;
@@ -527,14 +533,14 @@ static sw_status prepare(sw_bank* b) {
   } else if (f16) {
     PS16 = (uint32_t)((2 * Wseg * R + 15) / 16 * 16);
     PS16 += (16u + 256u - PS16 % 256u) % 256u;
-    const uint16_t padv = 0xE800u;  // -2048: padding letter and rows past the query
+    const uint16_t padv = 0xBC00u;  // -2048: padding letter and rows past the query
     for (sw_bank::Seg& sg : segs) {
       const int r0 = (int)(&sg - segs.data()) * seg_rows;
       std::vector<uint16_t> qp((size_t)(A + 1) * PS16 / 2, padv);
       for (int c = 0; c < A; ++c)
         for (int i = 0; i < sg.W * R && r0 + i < qlen && i < seg_rows; ++i)
           qp[(size_t)c * PS16 / 2 + i] =
-              __builtin_bit_cast(uint16_t, (_Float16)(float)m[b->query[r0 + i] * A + c]);
+              f16_score_bits(m[b->query[r0 + i] * A + c]);
       sg.off16 = tab16.size();
       tab16.resize(sg.off16 + qp.size() / 2);
       std::memcpy(tab16.data() + sg.off16, qp.data(), qp.size() * 2);
@@ -557,12 +563,12 @@ static sw_status prepare(sw_bank* b) {
     pS1 = (4 * pS2 + B + 15) / 16 * 16;
     while ((pS1 / 16) % 16 != 4) pS1 += 16;
     const uint32_t bytes = 16 + 4 * pS1 + 4 * pS2 + B;
-    tpair.assign(bytes / 4, 0xE800E800u);
+    tpair.assign(bytes / 4, 0xBC00BC00u);
     auto word = [&](int r, int x, int y) -> uint32_t {  // row r of the segment, letters x, y
-      if (r >= qlen) return 0xE800E800u;
+      if (r >= qlen) return 0xBC00BC00u;
       const int q = b->query[r];
-      return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)m[q * A + x]) |
-             (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)m[q * A + y]) << 16;
+      return (uint32_t)f16_score_bits(m[q * A + x]) |
+             (uint32_t)f16_score_bits(m[q * A + y]) << 16;
     };
     for (int x = 0; x < A; ++x)
       for (int y = 0; y < A; ++y) {
@@ -592,7 +598,7 @@ static sw_status prepare(sw_bank* b) {
       }
       if (f16) {
         const size_t b16 = wt16.size();
-        wt16.resize(b16 + wrows, 0xE8E8E8E8u);  // rows past the query: -2048
+        wt16.resize(b16 + wrows, 0xBCBCBCBCu);  // rows past the query: -2048
         for (int i = 0; i < nr; ++i) {
           uint32_t w = 0;
           for (int c = 0; c < 4; ++c) {
@@ -612,11 +618,11 @@ static sw_status prepare(sw_bank* b) {
       wt.resize(base + qp.size() / 4);
       std::memcpy(wt.data() + base, qp.data(), qp.size());
       if (f16) {
-        std::vector<uint16_t> q16((size_t)(A + 1) * wrows, 0xE800u);
+        std::vector<uint16_t> q16((size_t)(A + 1) * wrows, 0xBC00u);
         for (int c = 0; c < A; ++c)
           for (int i = 0; i < nr; ++i)
             q16[(size_t)c * wrows + i] =
-                __builtin_bit_cast(uint16_t, (_Float16)(float)m[b->query[r0 + i] * A + c]);
+                f16_score_bits(m[b->query[r0 + i] * A + c]);
         const size_t b16 = wt16.size();
         wt16.resize(b16 + q16.size() / 2);
         std::memcpy(wt16.data() + b16, q16.data(), q16.size() * 2);

@@ -108,8 +108,11 @@ __device__ __forceinline__ void column_merged(const LK& lk, u16x2& diag, u16x2& 
 // ---- one column of R rows, merged gap matrix, f16 arithmetic ------------------------------
 // Exact for integer scores |x| <= 2048 (the host routes a batch here only when the score
 // bound allows it, and when every substitution score is an f16 whose low byte is 0, so a
-// one-byte LUT entry is its high byte).  Signed arithmetic needs no clamps and no shift,
-// and v_pk_maximum3_f16 takes three inputs:
+// one-byte LUT entry is its high byte).  Signed arithmetic needs no shift, and
+// v_pk_maximum3_f16 takes three inputs.  Scores are stored as f16 multiples of 2^-11 (x as
+// x/2048): every integer |x| <= 2048 is then an exact normal f16 (or 0), and the [0, 1] clamp
+// modifier of v_pk_add_f16 is max(0, x) for free -- the asm columns (scripts/gen_f16_rows.py)
+// use it to form M = max(0, H(i-1,j-1) + s) in the diagonal add.  The C++ form below:
 //   D = H(i-1,j-1) + s      I = max(Tup, Tleft)      H = max(0, D, I)
 //   T = max(-o-e, D-o-e, I-e)  (= G - e, the gap value the right and lower neighbours see)
 // 8 VALU per lane per 2 cells (u16 form: 9).  Negative values never reach a positive one.
@@ -118,6 +121,14 @@ __device__ __forceinline__ f16x2 as_f16x2(u16x2 x) { return __builtin_bit_cast(f
 __device__ __forceinline__ u16x2 as_u16x2(f16x2 x) { return __builtin_bit_cast(u16x2, x); }
 __device__ __forceinline__ f16x2 fmax2(f16x2 a, f16x2 b) {
   return __builtin_elementwise_maximum(a, b);
+}
+// integer score <-> its f16 encoding (x / 2048); f16_pair: both halves (host side, ScoreArgs)
+__host__ __device__ inline uint32_t f16_pair(int x) {
+  const uint16_t h = __builtin_bit_cast(uint16_t, (_Float16)((float)x * (1.0f / 2048.0f)));
+  return (uint32_t)h * 0x10001u;
+}
+__device__ __forceinline__ int32_t f16_unscore(uint32_t bits) {
+  return (int32_t)((float)__builtin_bit_cast(_Float16, (unsigned short)bits) * 2048.0f);
 }
 template <int R, int RB, bool ZDOWN, class LK>
 __device__ __forceinline__ void column_merged_f16(const LK& lk, u16x2& diag_, u16x2& upT_,
@@ -191,12 +202,12 @@ __device__ __forceinline__ void column_gotoh_f16(const LK& lk, u16x2& diag_, u16
 #define SWK_F16_OUT_M(B) SWK_F16_HT(B), [X] "=&v"(X), [DN] "=&v"(DN), [IN] "=&v"(IN)
 #define SWK_F16_OUT_G(B) SWK_F16_HT(B), [EN] "=&v"(X), [HN] "=&v"(DN), [FN] "=&v"(IN), [F] "+v"(up)
 #define SWK_F16_IN_L(B)                                                                       \
-  [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up),            \
+  [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [no] "s"(no), [up] "v"(up),            \
       [tb0] "s"(lk.tab[B + 1]), [tb1] "s"(lk.tab[B + 2]), [tb2] "s"(lk.tab[B + 3]),           \
       [tb3] "s"(lk.tab[B + 4]), [tb4] "s"(lk.tab[B + 5]), [tb5] "s"(lk.tab[B + 6]),           \
       [tb6] "s"(lk.tab[B + 7]), [tb7] "s"(lk.tab[(B + 8) < R ? B + 8 : R - 1])
 #define SWK_F16_IN_P(B)                                                                       \
-  [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), \
+  [noe] "s"(noe), [ne] "s"(ne), [no] "s"(no), [up] "v"(up), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), \
       [lo0] "v"(lk.lo[B / 2]), [lo1] "v"(lk.lo[B / 2 + 1]), [lo2] "v"(lk.lo[B / 2 + 2]),       \
       [lo3] "v"(lk.lo[B / 2 + 3]), [lo4] "v"(lk.lo[(B + 8) < R ? B / 2 + 4 : B / 2 + 3]),      \
       [hi0] "v"(lk.hi[B / 2]), [hi1] "v"(lk.hi[B / 2 + 1]), [hi2] "v"(lk.hi[B / 2 + 2]),       \
@@ -220,7 +231,7 @@ __device__ __forceinline__ void column_gotoh_f16(const LK& lk, u16x2& diag_, u16
 template <int R, bool GOTOH, bool ZDOWN, class LK>
 __device__ __forceinline__ void column_f16_asm(const LK& lk, u16x2& diag_, u16x2& upX_,
                                                u16x2 (&Hl)[R], u16x2 (&Xl)[R], u16x2& best_,
-                                               uint32_t noe, uint32_t ne) {
+                                               uint32_t noe, uint32_t ne, uint32_t no) {
   static_assert(R % 8 == 0, "rows come in blocks of 8");
   constexpr bool PROF = !std::is_same<LK, LutLookup<R>>::value;
   uint32_t Da, Db, S1, X, DN, IN;
@@ -231,10 +242,10 @@ __device__ __forceinline__ void column_f16_asm(const LK& lk, u16x2& diag_, u16x2
 #define SWK_F16_COLASM(RR)                                                                    \
     asm volatile(                                                                             \
         "v_perm_b32 %[Da], %[nv], %[tz], %[sel]\n\t"                                          \
-        "v_pk_add_f16 %[Da], %[dg], %[Da]\n\t" SWK_F16M_L_Z0_COL##RR                          \
+        "v_pk_add_f16 %[Da], %[dg], %[Da] clamp\n\t" SWK_F16M_L_Z0_COL##RR                          \
         : SWK_F16_COL##RR##_HT, [Da] "=&v"(Da), [Db] "=&v"(Db), [S1] "=&v"(S1), [X] "=&v"(X), \
           [DN] "=&v"(DN), [IN] "=&v"(IN), [best] "+v"(best)                                  \
-        : [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up),     \
+        : [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [no] "s"(no), [up] "v"(up),     \
           [tz] "s"(lk.tab[0]), [dg] "v"(diag_), SWK_F16_COL##RR##_TB)
     if constexpr (R == 32) SWK_F16_COLASM(32);
     else SWK_F16_COLASM(16);
@@ -248,13 +259,13 @@ __device__ __forceinline__ void column_f16_asm(const LK& lk, u16x2& diag_, u16x2
   if constexpr (PROF)
     asm volatile(
         "v_perm_b32 %[Da], %[h0], %[l0], %[sA]\n\t"
-        "v_pk_add_f16 %[Da], %[dg], %[Da]"
+        "v_pk_add_f16 %[Da], %[dg], %[Da] clamp"
         : [Da] "=&v"(Da)
         : [h0] "v"(lk.hi[0]), [l0] "v"(lk.lo[0]), [sA] "s"(0x05040100u), [dg] "v"(diag_));
   else
     asm volatile(
         "v_perm_b32 %[Da], %[nv], %[t0], %[sel]\n\t"
-        "v_pk_add_f16 %[Da], %[dg], %[Da]"
+        "v_pk_add_f16 %[Da], %[dg], %[Da] clamp"
         : [Da] "=&v"(Da)
         : [nv] "v"(lk.nv), [t0] "s"(lk.tab[0]), [sel] "v"(lk.selw), [dg] "v"(diag_));
 #pragma unroll
@@ -298,11 +309,12 @@ __device__ __forceinline__ void column_f16_asm(const LK& lk, u16x2& diag_, u16x2
 template <int R, int RB, bool GOTOH, bool ZDOWN, class LK>
 __device__ __forceinline__ void column_f16(const LK& lk, u16x2& diag, u16x2& upX,
                                            u16x2 (&Hl)[R], u16x2 (&Xl)[R], u16x2& best,
-                                           f16x2 NOE2, f16x2 NE2) {
+                                           f16x2 NOE2, f16x2 NE2, f16x2 NO2) {
 #if SWK_F16_ASM
   column_f16_asm<R, GOTOH, ZDOWN>(lk, diag, upX, Hl, Xl, best, as_u32(as_u16x2(NOE2)),
-                                  as_u32(as_u16x2(NE2)));
+                                  as_u32(as_u16x2(NE2)), as_u32(as_u16x2(NO2)));
 #else
+  (void)NO2;
   if constexpr (GOTOH)
     column_gotoh_f16<R, RB>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
   else
@@ -479,6 +491,8 @@ struct ScoreArgs {
   uint32_t idx_base;
   // PAIR (f16 DNA merged): letter-pair table strides; slot (a, b) at 16 + a*pS1 + b*pS2
   uint32_t pS1, pS2;
+  // f16 kernels: f16_pair(-(o+e)), f16_pair(-e), f16_pair(-o)
+  uint32_t f16_noe, f16_ne, f16_no;
 };
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -563,8 +577,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
 
   for (int i = threadIdx.x; i < W * SWB_TILE; i += blockDim.x) bestsh[i] = 0;
   // row -1: u16 H~ = S, G/F = 0 | f16 H = 0, T = -(o+e)
-  const _Float16 fnoe = (_Float16)(-(float)(a.O + a.E)), fne = (_Float16)(-(float)a.E);
-  const f16x2 NOE2 = {fnoe, fnoe}, NE2 = {fne, fne};
+  // f16 encodings of -(o+e), -e, -o (host-computed, so they stay in SGPRs)
+  const f16x2 NOE2 = as_f16x2(as_u16x2(a.f16_noe)), NE2 = as_f16x2(as_u16x2(a.f16_ne)),
+              NO2 = as_f16x2(as_u16x2(a.f16_no));
   if (wave == 0) {
     bnd[lane] = F16 ? make_uint2(0u, GOTOH ? 0u : as_u32(as_u16x2(NOE2)))
                     : make_uint2(S | (S << 16), 0u);
@@ -706,9 +721,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           if (jj + 1 < C) load16(jj + 1, lkq);
           __builtin_amdgcn_sched_barrier(0);
           if (COL0 && jj == 0 && c == 0)
-            column_f16<R, RB, GOTOH, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+            column_f16<R, RB, GOTOH, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, NO2);
           else
-            column_f16<R, RB, GOTOH, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+            column_f16<R, RB, GOTOH, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, NO2);
         } else if constexpr (PROF) {
           ProfLookup<R> lk;
           const uint32_t blo = min((wlo >> (8 * (jj & 3))) & 0xFFu, padc);
@@ -738,7 +753,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           const uint32_t nwh = jj + 1 < C ? (jj + 1 < 4 ? chi.x : chi.y) : rhi.x;
           const int nsh = jj + 1 < C ? 8 * ((jj + 1) & 3) : 0;
           uint32_t Da, Db, X, DN, IN;
-          const uint32_t noe = as_u32(as_u16x2(NOE2)), ne = as_u32(as_u16x2(NE2));
+          const uint32_t noe = as_u32(as_u16x2(NOE2)), ne = as_u32(as_u16x2(NE2)),
+                 no = as_u32(as_u16x2(NO2));
           u16x2 bst = best;
 #define SWK_PAIR_OUT(B, DA)                                                                   \
   [h0] "+v"(Hl[B]), [h1] "+v"(Hl[B + 1]), [h2] "+v"(Hl[B + 2]), [h3] "+v"(Hl[B + 3]),          \
@@ -750,7 +766,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
 #define SWK_PAIR_IN(P0, P1, UP)                                                               \
   [p0] "v"(P0.x), [p1] "v"(P0.y), [p2] "v"(P0.z), [p3] "v"(P0.w), [p4] "v"(P1.x),             \
       [p5] "v"(P1.y), [p6] "v"(P1.z), [p7] "v"(P1.w), [up] "v"(UP), [noe] "s"(noe),           \
-      [ne] "s"(ne)
+      [ne] "s"(ne), [no] "s"(no)
           uint4 pB0 = ld4(acur + 48), pB1 = ld4(acur + 64);  // block 1
           __builtin_amdgcn_sched_barrier(0);
           asm volatile(SWK_F16PAIR_F
@@ -782,9 +798,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           const LutLookup<R> lk{tab, nv, __builtin_amdgcn_perm(whi, wlo, sel16) | 0x000C000Cu};
           __builtin_amdgcn_sched_barrier(0);
           if (COL0 && jj == 0 && c == 0)
-            column_f16<R, RB, GOTOH, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+            column_f16<R, RB, GOTOH, true>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, NO2);
           else
-            column_f16<R, RB, GOTOH, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+            column_f16<R, RB, GOTOH, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, NO2);
         } else {
           // selector: byte 0 = code of the low target, byte 2 = code of the high target
           const uint32_t sel =
@@ -820,8 +836,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           bs[lane] = 0;
           bs[lane + 64] = 0;
           if constexpr (F16) {  // f16 bit patterns of non-negative integers -> int
-            blo = (int32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)blo);
-            bhi = (int32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)bhi);
+            blo = f16_unscore((uint32_t)blo);
+            bhi = f16_unscore((uint32_t)bhi);
           }
           const size_t slo = a.idx && tlo < n ? a.idx[tlo] : tlo;
           const size_t shi = a.idx && thi < n ? a.idx[thi] : thi;
@@ -1006,30 +1022,31 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
       [lo4] "v"(lk.lo[SWK_CLAMP(B / 2 + 4, K / 2)]), [hi0] "v"(lk.hi[B / 2]),                  \
       [hi1] "v"(lk.hi[SWK_CLAMP(B / 2 + 1, K / 2)]), [hi2] "v"(lk.hi[SWK_CLAMP(B / 2 + 2, K / 2)]), \
       [hi3] "v"(lk.hi[SWK_CLAMP(B / 2 + 3, K / 2)]), [hi4] "v"(lk.hi[SWK_CLAMP(B / 2 + 4, K / 2)])
-#define SWK_W_IN_LM(B) [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up), SWK_W_TB(B)
+#define SWK_W_IN_LM(B) [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [no] "s"(no), [up] "v"(up), SWK_W_TB(B)
 #define SWK_W_IN_LG(B) [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), SWK_W_TB(B)
 #define SWK_W_IN_PM(B)                                                                        \
-  [noe] "s"(noe), [ne] "s"(ne), [up] "v"(up), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), \
+  [noe] "s"(noe), [ne] "s"(ne), [no] "s"(no), [up] "v"(up), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), \
       SWK_W_LH(B)
 #define SWK_W_IN_PG(B) [noe] "s"(noe), [ne] "s"(ne), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), SWK_W_LH(B)
 
 template <int K, bool GOTOH, class LK>
 __device__ __forceinline__ void column_f16_lane_asm(const LK& lk, u16x2& diag_, u16x2& upX_,
                                                     u16x2 (&Hl)[K], u16x2 (&Xl)[K],
-                                                    u16x2& best_, uint32_t noe, uint32_t ne) {
+                                                    u16x2& best_, uint32_t noe, uint32_t ne,
+                                                    uint32_t no) {
   constexpr bool PROF = !std::is_same<LK, LaneLutLookup<K>>::value;
   uint32_t Da, Db, S1, X, DN, IN;
   u16x2 best = best_, up = upX_;
   if constexpr (PROF)
     asm volatile(
         "v_perm_b32 %[Da], %[h0], %[l0], %[sA]\n\t"
-        "v_pk_add_f16 %[Da], %[dg], %[Da]"
+        "v_pk_add_f16 %[Da], %[dg], %[Da] clamp"
         : [Da] "=&v"(Da)
         : [h0] "v"(lk.hi[0]), [l0] "v"(lk.lo[0]), [sA] "s"(0x05040100u), [dg] "v"(diag_));
   else
     asm volatile(
         "v_perm_b32 %[Da], %[nv], %[t0], %[sel]\n\t"
-        "v_pk_add_f16 %[Da], %[dg], %[Da]"
+        "v_pk_add_f16 %[Da], %[dg], %[Da] clamp"
         : [Da] "=&v"(Da)
         : [nv] "v"(lk.nv), [t0] "v"(lk.lut[0]), [sel] "v"(lk.selw), [dg] "v"(diag_));
   if constexpr (K == 4) {
@@ -1117,11 +1134,13 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
     else return x | (y << 16) | 0x0C000C00u;
   };
   const uint32_t padsel = code_word(pad, pad);
-  const _Float16 fnoe = (_Float16)(-(float)(a.O + a.E)), fne = (_Float16)(-(float)a.E);
-  const f16x2 NOE2 = {fnoe, fnoe}, NE2 = {fne, fne};
+  // f16 encodings of -(o+e), -e, -o (host-computed, so they stay in SGPRs)
+  const f16x2 NOE2 = as_f16x2(as_u16x2(a.f16_noe)), NE2 = as_f16x2(as_u16x2(a.f16_ne)),
+              NO2 = as_f16x2(as_u16x2(a.f16_no));
   const u16x2 H0 = F16 ? (u16x2){0, 0} : S2;                          // H of row/col -1
   const u16x2 X0 = (F16 && !GOTOH) ? as_u16x2(NOE2) : (u16x2){0, 0};  // T/G/E/F of row/col -1
-  const uint32_t noe = as_u32(as_u16x2(NOE2)), ne = as_u32(as_u16x2(NE2));
+  const uint32_t noe = as_u32(as_u16x2(NOE2)), ne = as_u32(as_u16x2(NE2)),
+                 no = as_u32(as_u16x2(NO2));
 
   uint32_t lut[PROF ? 1 : K];
   if constexpr (!PROF) {
@@ -1211,13 +1230,13 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
         if constexpr (COL0)
           column_merged_f16_mask<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, z);
         else
-          column_f16_lane_asm<K, GOTOH>(lk, diag, upX, Hl, Xl, best, noe, ne);
+          column_f16_lane_asm<K, GOTOH>(lk, diag, upX, Hl, Xl, best, noe, ne, no);
       } else {
         const LaneLutLookup<K> lk{lut, nv, let};
         if constexpr (COL0)
           column_merged_f16_mask<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, z);
         else
-          column_f16_lane_asm<K, GOTOH>(lk, diag, upX, Hl, Xl, best, noe, ne);
+          column_f16_lane_asm<K, GOTOH>(lk, diag, upX, Hl, Xl, best, noe, ne, no);
       }
     } else if constexpr (PROF) {
       ProfLookupK<K> lk;
@@ -1275,8 +1294,8 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
   // max over the wave's rows, per target (f16: non-negative integers -> int)
   uint32_t bx = best.x, by = best.y;
   if constexpr (F16) {
-    bx = (uint32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)bx);
-    by = (uint32_t)(float)__builtin_bit_cast(_Float16, (unsigned short)by);
+    bx = (uint32_t)f16_unscore(bx);
+    by = (uint32_t)f16_unscore(by);
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
@@ -1352,7 +1371,9 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
   const swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                          O,    E,    PS,   pad, scores, static_cast<const uint2*>(edge_in),
                          static_cast<uint2*>(edge_out), ecols, (uint32_t)accum, (uint32_t)packed,
-                         idx, nidx, idx_base, pS1, pS2};
+                         idx, nidx, idx_base, pS1, pS2,
+                         swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
+                         swk::f16_pair(-(int)O)};
   const uint32_t prof_bytes = (pad + 1) * PS;
   if (pair) {  // PS = pair-table bytes
     if (R == 32 && f16 && !prof && !gotoh && !col0)
@@ -1445,7 +1466,9 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
                          static_cast<const uint2*>(edge_in), static_cast<uint2*>(edge_out), ecols,
-                         (uint32_t)accum, (uint32_t)packed, nullptr, nullptr, 0u};
+                         (uint32_t)accum, (uint32_t)packed, nullptr, nullptr, 0u, 0u, 0u,
+                         swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
+                         swk::f16_pair(-(int)O)};
   const uint32_t prof_bytes = (pad + 1) * PS;
 #define SWK_WCASE(KK, C0, PF, GT)                                                         \
   if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                                 \
