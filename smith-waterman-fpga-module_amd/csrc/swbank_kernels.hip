@@ -628,20 +628,30 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
 
   // PAIR: column state one column ahead: acur = this column's table address (slot + this
   // wave's rows - 16), pA = its first 8 row words, pw = its row-0 word
-  const char* lp = reinterpret_cast<const char*>(smem);
-  const auto ld4 = [lp](uint32_t off) { return *reinterpret_cast<const uint4*>(lp + off); };
+  // Table addresses are absolute LDS byte addresses (smem's link-time address folded into
+  // wofs once), so a column's address needs no add for the base.
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) const u32x4 lds_u4;
+  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+  const auto ld4 = [](uint32_t addr) { return __builtin_bit_cast(uint4, *(lds_u4*)(size_t)addr); };
   // the row-0 word: a relaxed atomic load, so LLVM does not merge it with the neighbouring
   // 16-B reads (it splits them into ds_read2_b32 pairs otherwise)
-  const auto ld1 = [lp](uint32_t off) {
-    return __atomic_load_n(reinterpret_cast<const uint32_t*>(lp + off), __ATOMIC_RELAXED);
+  const auto ld1 = [](uint32_t addr) {
+    return __atomic_load_n((lds_u32*)(size_t)addr, __ATOMIC_RELAXED);
   };
-  const uint32_t wofs = (uint32_t)wave * R * 4;
+  const uint32_t wofs = (uint32_t)wave * R * 4 + (uint32_t)(size_t)(lds_void_ptr)smem;
   // codes clamped to N: lanes past the batch end (and codes >= 5 on the device API) would
   // otherwise pick a slot outside the table, and a slot feeds both halves (one v_min each,
   // SDWA byte-select)
+  // (3 VALU: {a, b} as u16 halves by one v_perm, clamped by one v_pk_min_u16, then
+  // a*pS1 + b*pS2 + wofs by one v_dot2_u32_u16; the host keeps pS1, pS2 < 65536)
+  const u16x2 pS12 = {(unsigned short)a.pS1, (unsigned short)a.pS2};
   const auto pair_addr = [&](uint32_t wl, uint32_t wh, int sh) {
-    return __umul24(min((wl >> sh) & 0xFFu, 4u), a.pS1) +
-           __umul24(min((wh >> sh) & 0xFFu, 4u), a.pS2) + wofs;
+    const uint32_t sel = (uint32_t)(sh >> 3) | 0x0C00u | ((uint32_t)(4 + (sh >> 3)) << 16) |
+                         0x0C000000u;
+    const u16x2 ab = __builtin_elementwise_min(as_u16x2(__builtin_amdgcn_perm(wh, wl, sel)),
+                                               (u16x2){4, 4});
+    return __builtin_amdgcn_udot2(ab, pS12, wofs, false);
   };
   uint32_t acur = 0, pw = 0;
   uint4 pA0 = {0, 0, 0, 0}, pA1 = {0, 0, 0, 0};
