@@ -18,7 +18,11 @@
 #include <mutex>
 #include <numeric>
 #include <thread>
+#include <chrono>
 #include <vector>
+#if defined(__SSE2__)
+#include <emmintrin.h>
+#endif
 
 #include "swbank.h"
 #include "swbank_internal.h"
@@ -95,6 +99,9 @@ struct PinBuf {
 
 // Host worker threads for the host-buffer feeder (gather / scatter of a chunk): run(f) calls
 // f(part) for part = 0..size()-1, part 0 on the calling thread, and returns when all are done.
+// A host-API call runs several short jobs per chunk back to back, so idle workers spin on the
+// job counter for up to 200 us before they sleep (a futex wake-up per job cost more than the
+// jobs), and the caller spins for the last part to finish.
 class HostPool {
  public:
   explicit HostPool(unsigned n) : n_(std::max(1u, n)) {
@@ -103,8 +110,8 @@ class HostPool {
   ~HostPool() {
     {
       std::lock_guard<std::mutex> g(m_);
-      stop_ = true;
-      ++gen_;
+      stop_.store(true);
+      gen_.fetch_add(1);
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
@@ -115,44 +122,50 @@ class HostPool {
       f(0);
       return;
     }
+    job_ = &f;
+    pending_.store(n_ - 1, std::memory_order_relaxed);
     {
-      std::lock_guard<std::mutex> g(m_);
-      job_ = &f;
-      pending_ = n_ - 1;
-      ++gen_;
+      std::lock_guard<std::mutex> g(m_);  // a worker about to sleep re-checks gen_ under m_
+      gen_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
     f(0);
-    std::unique_lock<std::mutex> l(m_);
-    done_.wait(l, [&] { return pending_ == 0; });
+    while (pending_.load(std::memory_order_acquire) != 0) relax();
     job_ = nullptr;
   }
 
  private:
+  static void relax() {
+#if defined(__SSE2__)
+    _mm_pause();
+#endif
+  }
   void loop(unsigned i) {
     uint64_t seen = 0;
     for (;;) {
-      const std::function<void(unsigned)>* job;
-      {
-        std::unique_lock<std::mutex> l(m_);
-        cv_.wait(l, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (stop_) return;
-        job = job_;
+      const auto t0 = std::chrono::steady_clock::now();
+      for (unsigned it = 1; gen_.load(std::memory_order_acquire) == seen; ++it) {
+        relax();
+        if ((it & 255) == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+          std::unique_lock<std::mutex> l(m_);
+          cv_.wait(l, [&] { return gen_.load() != seen; });
+        }
       }
-      (*job)(i);
-      std::lock_guard<std::mutex> g(m_);
-      if (--pending_ == 0) done_.notify_one();
+      seen = gen_.load(std::memory_order_acquire);
+      if (stop_.load()) return;
+      (*job_)(i);
+      pending_.fetch_sub(1, std::memory_order_acq_rel);
     }
   }
   unsigned n_;
   std::vector<std::thread> th_;
   std::mutex m_;
-  std::condition_variable cv_, done_;
-  const std::function<void(unsigned)>* job_ = nullptr;
-  unsigned pending_ = 0;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
+  std::condition_variable cv_;
+  const std::function<void(unsigned)>* job_ = nullptr;  // published by gen_ (release/acquire)
+  std::atomic<unsigned> pending_{0};
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<bool> stop_{false};
 };
 }  // namespace
 
@@ -697,12 +710,14 @@ static sw_status range_check(sw_bank* b, uint32_t max_len) {
   return SW_OK;
 }
 
-// packed: d_res holds n 64-byte CAPI records (2-bit codes); d_offs/d_lens are unused.
+// packed (SWK_PACK_*): RECORDS: d_res holds n 64-byte CAPI records (2-bit codes), d_offs and
+// d_lens are unused; STREAM: 2-bit codes, d_offs in bytes (the host feeder's DNA chunks).
 // perm/perm_n (optional, tile kernel): pass 0 visits the targets in the order perm[0..n)
 // (target numbers; *perm_n = n on the device), e.g. longest first; the wave kernel ignores it.
 static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                         const uint32_t* d_lens, size_t n, uint32_t max_len, int32_t* d_scores,
-                        hipStream_t st, bool packed = false, const uint32_t* perm = nullptr,
+                        hipStream_t st, uint32_t packed = SWK_PACK_BYTES,
+                        const uint32_t* perm = nullptr,
                         const uint32_t* perm_n = nullptr) {
   sw_bank::Ev ev{};
   if (b->timing) {
@@ -716,6 +731,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   if (b->timing) HIPOK(b, hipEventRecord(ev.b, st));
   HIPOK(b, hipStreamWaitEvent(st, b->ev_ready, 0));  // the query tables are uploaded
   const size_t nseg = b->segs.size();
+  const bool rec = packed == SWK_PACK_RECORDS;
   const uint32_t ecols = (max_len + 7) / 8 * 8;
   const size_t ntiles = (n + SWB_TILE - 1) / SWB_TILE;
   const bool gotoh = b->cfg.gap_model == SW_GAP_GOTOH;
@@ -787,12 +803,12 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
         void* eout = sg + 1 < b->wsegs ? b->edge[sg & 1].p : nullptr;
         HIPOK(b, swk_launch_wave(
                      b->wK, b->col0, b->prof, gotoh ? 1 : 0, use_f16 ? 1 : 0, ein, eout, ecols,
-                     sg > 0 ? 1 : 0, packed ? d_res + p0 * SWB_RECORD : d_res,
-                     packed ? d_offs : d_offs + p0, packed ? d_lens : d_lens + p0, np,
+                     sg > 0 ? 1 : 0, rec ? d_res + p0 * SWB_RECORD : d_res,
+                     rec ? d_offs : d_offs + p0, rec ? d_lens : d_lens + p0, np,
                      use_f16 ? b->wtab16.p + sg * b->wseg_words16 : b->wtab.p + sg * b->wseg_words,
                      use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
                      use_f16 && b->prof ? b->wPS16 : b->wPS, b->pad, d_scores + p0,
-                     packed ? 1 : 0, st));
+                     (int)packed, st));
       }
     }
   } else {
@@ -836,7 +852,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
       if (pass == 0 && perm) {  // whole arrays, visited through the permutation
         idx = perm + p0;
         nidx = perm_n;
-      } else if (pass == 0 && packed) {
+      } else if (pass == 0 && rec) {
         res = d_res + p0 * SWB_RECORD;
         scores = d_scores + p0;
       } else if (pass == 0) {
@@ -859,7 +875,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                                   f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
                                   pair ? b->pair_bytes : f16 && b->prof ? b->PS16 : b->PS,
                                   b->pad, b->segs[s].W, scores, ein, eout, ecols, s > 0 ? 1 : 0,
-                                  packed ? 1 : 0, idx, nidx, (uint32_t)p0, pair ? 1 : 0, b->pS1,
+                                  (int)packed, idx, nidx, (uint32_t)p0, pair ? 1 : 0, b->pS1,
                                   b->pS2, st));
       }
     }
@@ -1001,8 +1017,8 @@ struct Chunk {
   size_t c0, c1, bytes;
 };
 
-// Runs the feeder: gather(slot, chunk) fills the host slot (false: bad input, message set),
-// the slot goes to the device on the copy stream, score(dslot, chunk, d_scores) launches the
+// Runs the feeder: gather(slot, chunk) fills the host slot and returns how many leading bytes
+// of it to copy (0: bad input, message set); they go to the device on the copy stream, score(dslot, chunk, d_scores) launches the
 // kernel on the bank stream; the scores come back to the pinned hscores in input order.
 template <class GatherF, class ScoreF>
 static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, GatherF gather,
@@ -1021,14 +1037,15 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     const int s = (int)(i % sw_bank::NSLOT);
     const Chunk& c = chunks[i];
     if (i >= (size_t)sw_bank::NSLOT) HIPOK(b, hipEventSynchronize(b->h2d_done[s]));
-    if (!gather(b->hslot[s].p, c)) {
+    const size_t bytes = gather(b->hslot[s].p, c);
+    if (bytes == 0) {
       (void)hipStreamSynchronize(b->stream);
       (void)hipStreamSynchronize(b->copy_stream);
       return SW_ERR_ARG;
     }
     if (i >= (size_t)sw_bank::NSLOT)
       HIPOK(b, hipStreamWaitEvent(b->copy_stream, b->kern_done[s], 0));
-    HIPOK(b, hipMemcpyAsync(b->dslot[s].p, b->hslot[s].p, c.bytes, hipMemcpyHostToDevice,
+    HIPOK(b, hipMemcpyAsync(b->dslot[s].p, b->hslot[s].p, bytes, hipMemcpyHostToDevice,
                             b->copy_stream));
     HIPOK(b, hipEventRecord(b->h2d_done[s], b->copy_stream));
     HIPOK(b, hipStreamWaitEvent(b->stream, b->h2d_done[s], 0));
@@ -1054,6 +1071,40 @@ static SlotTail slot_tail(size_t tail_at, size_t cnt) {
   return {tail_at, tail_at + cnt * 4, tail_at + cnt * 8};
 }
 
+// l code bytes -> ceil(l/4) bytes of 2-bit codes, 4 per byte LSB first (the CAPI host's
+// charTo2bit order, aligner_Header.c:25-40).  Returns the OR of all l codes: the packing is
+// valid only when it is <= 3 (a DNA chunk without N).
+static inline uint32_t pack_2bit(const uint8_t* src, uint32_t l, uint8_t* dst) {
+  uint32_t j = 0, orc = 0;
+#if defined(__SSE2__)
+  __m128i orv = _mm_setzero_si128();
+  const __m128i m16 = _mm_set1_epi16(0x000F), m32 = _mm_set1_epi32(0xFF);
+  for (; j + 16 <= l; j += 16) {  // 16 codes -> 4 bytes
+    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + j));
+    orv = _mm_or_si128(orv, v);
+    __m128i x = _mm_and_si128(_mm_or_si128(v, _mm_srli_epi16(v, 6)), m16);  // 2 codes / u16
+    x = _mm_and_si128(_mm_or_si128(x, _mm_srli_epi32(x, 12)), m32);        // 4 codes / u32
+    x = _mm_packus_epi16(_mm_packs_epi32(x, x), x);
+    const uint32_t w = (uint32_t)_mm_cvtsi128_si32(x);
+    std::memcpy(dst + j / 4, &w, 4);
+  }
+  orv = _mm_or_si128(orv, _mm_srli_si128(orv, 8));
+  orv = _mm_or_si128(orv, _mm_srli_si128(orv, 4));
+  orv = _mm_or_si128(orv, _mm_srli_si128(orv, 2));
+  orv = _mm_or_si128(orv, _mm_srli_si128(orv, 1));
+  orc = (uint32_t)_mm_cvtsi128_si32(orv) & 0xFFu;
+#endif
+  for (; j < l; j += 4) {
+    uint32_t byte = 0;
+    for (uint32_t t = 0; t < 4 && j + t < l; ++t) {
+      orc |= src[j + t];
+      byte |= (uint32_t)(src[j + t] & 3u) << (2 * t);
+    }
+    dst[j / 4] = (uint8_t)byte;
+  }
+  return orc;
+}
+
 extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const uint64_t* offsets,
                                     const uint32_t* lens, size_t n, int32_t* scores_out) {
   if (!b) return SW_ERR_ARG;
@@ -1065,97 +1116,162 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const u
   if (st != SW_OK) return st;
   if ((st = feeder_init(b)) != SW_OK) return st;
 
-  // chunks in input order, cut at ~chunk_target() code bytes
-  uint32_t max_len = 0;
-  size_t total = 0;
-  for (size_t k = 0; k < n; ++k) {
-    max_len = std::max(max_len, lens[k]);
-    total += lens[k];
-  }
-  if (max_len && !residues) return fail(b, SW_ERR_ARG, "null residues");
-  if ((st = range_check(b, max_len)) != SW_OK) return st;
-  const size_t target = chunk_target(total);
-  std::vector<Chunk> chunks;
-  std::vector<uint32_t> chunk_max;
-  for (size_t k = 0, c0 = 0, acc = 0, ml = 0; k < n; ++k) {
-    acc += lens[k];
-    ml = std::max<size_t>(ml, lens[k]);
-    if (acc >= target || k + 1 == n) {
-      const size_t cnt = k + 1 - c0;
-      // slot: codes (16-B aligned) | offsets u64 | lens | perm | count
-      chunks.push_back({c0, k + 1, align16(align16(acc) + cnt * 16 + 4)});
-      chunk_max.push_back((uint32_t)ml);
-      c0 = k + 1;
-      acc = 0;
-      ml = 0;
-    }
-  }
+  // Two passes over the lengths on the pool (inline for small batches): total and longest,
+  // then the chunk cuts in input order, after target k when the running code count crosses a
+  // multiple of chunk_target().
   HostPool& pool = *b->pool;
   const unsigned T = pool.size();
+  const unsigned P = n >= 65536 ? T : 1;
+  const size_t pstep = (n + P - 1) / P;
+  const auto run_parts = [&](const std::function<void(unsigned)>& f) {
+    if (P > 1) pool.run(f);
+    else f(0u);
+  };
+  std::vector<size_t> psum(P + 1, 0);
+  std::vector<uint32_t> pmax(P, 0);
+  run_parts([&](unsigned p) {
+    size_t acc = 0;
+    uint32_t m = 0;
+    for (size_t k = std::min(n, p * pstep); k < std::min(n, (p + 1) * pstep); ++k) {
+      acc += lens[k];
+      m = std::max(m, lens[k]);
+    }
+    psum[p + 1] = acc;
+    pmax[p] = m;
+  });
+  for (unsigned p = 0; p < P; ++p) psum[p + 1] += psum[p];
+  const size_t total = psum[P];
+  const uint32_t max_len = *std::max_element(pmax.begin(), pmax.end());
+  if (max_len && !residues) return fail(b, SW_ERR_ARG, "null residues");
+  if ((st = range_check(b, max_len)) != SW_OK) return st;
+  // slot: offsets u64 | lens | perm | count (SlotTail) | codes at codes_at(cnt): one byte per
+  // residue, or, for a DNA chunk without N, the 2-bit stream (a quarter of the PCIe bytes;
+  // SWBANK_PACK2=0 disables), each target from a byte boundary, 16 zero bytes after the last
+  const auto codes_at = [](size_t cnt) { return align16(cnt * 16 + 4); };
+  const size_t target = chunk_target(total);
+  std::vector<std::vector<std::pair<size_t, size_t>>> pcut(P);  // (end position, code prefix)
+  run_parts([&](unsigned p) {
+    size_t acc = psum[p];
+    for (size_t k = std::min(n, p * pstep); k < std::min(n, (p + 1) * pstep); ++k) {
+      const size_t before = acc / target;
+      acc += lens[k];
+      if (acc / target != before && k + 1 < n) pcut[p].push_back({k + 1, acc});
+    }
+  });
+  std::vector<Chunk> chunks;
+  size_t c0 = 0, a0 = 0;
+  const auto add_chunk = [&](size_t c1, size_t a1) {
+    chunks.push_back({c0, c1, codes_at(c1 - c0) + align16(a1 - a0 + 16)});
+    c0 = c1;
+    a0 = a1;
+  };
+  for (const auto& cuts : pcut)
+    for (const auto& ca : cuts) add_chunk(ca.first, ca.second);
+  add_chunk(n, total);
+  std::vector<uint32_t> chunk_max(chunks.size(), 0);  // set by the chunk's gather
   const uint32_t alpha = (uint32_t)b->alpha;
+  const bool pack2 = b->alpha == SW_DNA_ALPHA && env_int("SWBANK_PACK2", 1) != 0;
   HIPOK(b, hipSetDevice(b->device));
-  const auto offs_at = [&](const Chunk& c) { return c.bytes - align16((c.c1 - c.c0) * 16 + 4); };
-  std::vector<char> has_perm(chunks.size(), 0);
-  std::vector<size_t> part(T + 1);
+  std::vector<char> has_perm(chunks.size(), 0), two_bit(chunks.size(), 0);
+  std::vector<size_t> part(T + 1), part2(T + 1);
+  std::vector<uint32_t> partmax(T);
   std::atomic<size_t> bad{SIZE_MAX};
+  std::atomic<uint32_t> wide{0};
   size_t gi = 0, si = 0;
-  const auto gather = [&](uint8_t* slot, const Chunk& c) -> bool {
-    const size_t cnt = c.c1 - c.c0, oa = offs_at(c);
-    const SlotTail tl = slot_tail(oa + cnt * 8, cnt);
-    uint64_t* so = reinterpret_cast<uint64_t*>(slot + oa);
+  const auto gather = [&](uint8_t* slot, const Chunk& c) -> size_t {
+    const size_t cnt = c.c1 - c.c0, ca = codes_at(cnt);
+    const SlotTail tl = slot_tail(cnt * 8, cnt);
+    uint64_t* so = reinterpret_cast<uint64_t*>(slot);
     uint32_t* sl = reinterpret_cast<uint32_t*>(slot + tl.lens_at);
-    // two passes over the pool's parts: code bytes per part, then copy at the prefix
+    uint8_t* codes = slot + ca;
+    // two passes over the pool's parts: code bytes (and 2-bit bytes) per part, then each part
+    // writes at its prefix
     const size_t step = (cnt + T - 1) / T;
     std::fill(part.begin(), part.end(), 0);
+    std::fill(part2.begin(), part2.end(), 0);
     pool.run([&](unsigned p) {
-      size_t acc = 0;
-      for (size_t k = c.c0 + std::min(cnt, p * step); k < c.c0 + std::min(cnt, (p + 1) * step); ++k)
+      size_t acc = 0, acc2 = 0;
+      uint32_t m = 0;
+      for (size_t k = c.c0 + std::min(cnt, p * step); k < c.c0 + std::min(cnt, (p + 1) * step);
+           ++k) {
         acc += lens[k];
-      part[p + 1] = acc;
-    });
-    for (unsigned p = 0; p < T; ++p) part[p + 1] += part[p];
-    pool.run([&](unsigned p) {
-      size_t at = part[p];
-      for (size_t i = std::min(cnt, p * step); i < std::min(cnt, (p + 1) * step); ++i) {
-        const size_t k = c.c0 + i;
-        const uint32_t l = lens[k];
-        const uint8_t* src = residues + offsets[k];
-        uint8_t* d = slot + at;
-        uint8_t m = 0;
-        for (uint32_t j = 0; j < l; ++j) {  // copy + alphabet check, vectorised
-          const uint8_t v = src[j];
-          d[j] = v;
-          m = v > m ? v : m;
-        }
-        if (l && m >= alpha) {
-          size_t cur = bad.load();
-          while (k < cur && !bad.compare_exchange_weak(cur, k)) {
-          }
-        }
-        so[i] = at;
-        sl[i] = l;
-        at += l;
+        acc2 += (lens[k] + 3) / 4;
+        m = std::max(m, lens[k]);
       }
+      part[p + 1] = acc;
+      part2[p + 1] = acc2;
+      partmax[p] = m;
     });
-    if (bad.load() != SIZE_MAX) {
-      const size_t k = bad.load();
-      uint8_t m = 0;
-      for (uint32_t j = 0; j < lens[k]; ++j) m = std::max(m, residues[offsets[k] + j]);
-      fail(b, SW_ERR_ARG, "target %zu code %u outside alphabet", k, (unsigned)m);
-      return false;
+    chunk_max[gi] = *std::max_element(partmax.begin(), partmax.end());
+    for (unsigned p = 0; p < T; ++p) {
+      part[p + 1] += part[p];
+      part2[p + 1] += part2[p];
     }
+    bool two = pack2;
+    if (two) {  // optimistic: any code > 3 (N, or outside the alphabet) -> the byte path
+      wide = 0;
+      pool.run([&](unsigned p) {
+        size_t at = part2[p];
+        uint32_t orc = 0;
+        for (size_t i = std::min(cnt, p * step); i < std::min(cnt, (p + 1) * step); ++i) {
+          const size_t k = c.c0 + i;
+          const uint32_t l = lens[k];
+          orc |= pack_2bit(residues + offsets[k], l, codes + at);
+          so[i] = at;
+          sl[i] = l;
+          at += (l + 3) / 4;
+        }
+        if (orc > 3u) wide = 1;
+      });
+      two = wide.load() == 0;
+      if (two) std::memset(codes + part2[T], 0, 16);  // a last chunk reads 1 byte past
+    }
+    if (!two) {
+      pool.run([&](unsigned p) {
+        size_t at = part[p];
+        for (size_t i = std::min(cnt, p * step); i < std::min(cnt, (p + 1) * step); ++i) {
+          const size_t k = c.c0 + i;
+          const uint32_t l = lens[k];
+          const uint8_t* src = residues + offsets[k];
+          uint8_t* d = codes + at;
+          uint8_t m = 0;
+          for (uint32_t j = 0; j < l; ++j) {  // copy + alphabet check, vectorised
+            const uint8_t v = src[j];
+            d[j] = v;
+            m = v > m ? v : m;
+          }
+          if (l && m >= alpha) {
+            size_t cur = bad.load();
+            while (k < cur && !bad.compare_exchange_weak(cur, k)) {
+            }
+          }
+          so[i] = at;
+          sl[i] = l;
+          at += l;
+        }
+      });
+      if (bad.load() != SIZE_MAX) {
+        const size_t k = bad.load();
+        uint8_t m = 0;
+        for (uint32_t j = 0; j < lens[k]; ++j) m = std::max(m, residues[offsets[k] + j]);
+        fail(b, SW_ERR_ARG, "target %zu code %u outside alphabet", k, (unsigned)m);
+        return 0;
+      }
+    }
+    two_bit[gi] = two;
     has_perm[gi++] = chunk_perm(pool, sl, cnt, reinterpret_cast<uint32_t*>(slot + tl.perm_at));
     *reinterpret_cast<uint32_t*>(slot + tl.cnt_at) = (uint32_t)cnt;
-    return true;
+    return ca + (two ? align16(part2[T] + 16) : align16(part[T]));
   };
   const auto score = [&](uint8_t* dslot, const Chunk& c, int32_t* d_scores) -> sw_status {
-    const size_t cnt = c.c1 - c.c0, oa = offs_at(c);
-    const SlotTail tl = slot_tail(oa + cnt * 8, cnt);
+    const size_t cnt = c.c1 - c.c0;
+    const SlotTail tl = slot_tail(cnt * 8, cnt);
     const bool pm = has_perm[si];
+    const uint32_t mode = two_bit[si] ? SWK_PACK_STREAM : SWK_PACK_BYTES;
     const uint32_t ml = chunk_max[si++];
-    return launch(b, dslot, reinterpret_cast<const uint64_t*>(dslot + oa),
+    return launch(b, dslot + codes_at(cnt), reinterpret_cast<const uint64_t*>(dslot),
                   reinterpret_cast<const uint32_t*>(dslot + tl.lens_at), cnt, ml, d_scores,
-                  b->stream, false,
+                  b->stream, mode,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.perm_at) : nullptr,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr);
   };
@@ -1199,7 +1315,8 @@ extern "C" sw_status sw_score_records_device(sw_bank* b, const void* d_records, 
   if ((st = range_check(b, SWB_RECORD_MAX)) != SW_OK) return st;
   HIPOK(b, hipSetDevice(b->device));
   return launch(b, static_cast<const uint8_t*>(d_records), nullptr, nullptr, n, SWB_RECORD_MAX,
-                d_scores, stream ? reinterpret_cast<hipStream_t>(stream) : b->stream, true);
+                d_scores, stream ? reinterpret_cast<hipStream_t>(stream) : b->stream,
+                SWK_PACK_RECORDS);
 }
 
 extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
@@ -1236,7 +1353,7 @@ extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
   std::atomic<size_t> bad{SIZE_MAX};
   std::atomic<uint32_t> cmax{0};
   size_t gi = 0, si = 0;
-  const auto gather = [&](uint8_t* slot, const Chunk& c) -> bool {
+  const auto gather = [&](uint8_t* slot, const Chunk& c) -> size_t {
     const size_t cnt = c.c1 - c.c0;
     const SlotTail tl = slot_tail(cnt * SWB_RECORD, cnt);
     uint32_t* sl = reinterpret_cast<uint32_t*>(slot + tl.lens_at);
@@ -1264,19 +1381,19 @@ extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
     if (bad.load() != SIZE_MAX) {
       const size_t k = bad.load();
       fail(b, SW_ERR_ARG, "record %zu length %u > %u", k, rlen(k), SWB_RECORD_MAX);
-      return false;
+      return 0;
     }
     has_perm[gi] = chunk_perm(pool, sl, cnt, reinterpret_cast<uint32_t*>(slot + tl.perm_at));
     chunk_max[gi++] = cmax.load();
     *reinterpret_cast<uint32_t*>(slot + tl.cnt_at) = (uint32_t)cnt;
-    return true;
+    return c.bytes;
   };
   const auto score = [&](uint8_t* dslot, const Chunk& c, int32_t* d_scores) -> sw_status {
     const size_t cnt = c.c1 - c.c0;
     const SlotTail tl = slot_tail(cnt * SWB_RECORD, cnt);
     const bool pm = has_perm[si];
     const uint32_t ml = chunk_max[si++];
-    return launch(b, dslot, nullptr, nullptr, cnt, ml, d_scores, b->stream, true,
+    return launch(b, dslot, nullptr, nullptr, cnt, ml, d_scores, b->stream, SWK_PACK_RECORDS,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.perm_at) : nullptr,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr);
   };

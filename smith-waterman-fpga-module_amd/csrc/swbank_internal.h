@@ -16,4 +16,11 @@
 #define SWB_RECORD 64
 #define SWB_RECORD_MAX 232u
 
+/* Target layouts the kernels read (ScoreArgs.packed): one code byte per residue; 64-byte CAPI
+ * records; a 2-bit stream (4 codes per byte, LSB first, each target starting on a byte, offsets
+ * in bytes; the host feeder packs DNA chunks without N into it). */
+#define SWK_PACK_BYTES 0u
+#define SWK_PACK_RECORDS 1u
+#define SWK_PACK_STREAM 2u
+
 #endif

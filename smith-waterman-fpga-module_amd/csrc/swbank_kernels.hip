@@ -375,11 +375,19 @@ __device__ __forceinline__ uint2 pad_tail(uint2 w, uint32_t j0, uint32_t len, ui
 }
 
 __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint32_t pad,
-                                         bool packed, uint2& lo, uint2& hi) {
+                                         uint32_t packed, uint2& lo, uint2& hi) {
   const uint32_t j0 = (uint32_t)c * 8;
-  if (packed) {  // CAPI records: 2 bytes per 8 codes, always inside the 58-byte data field
-    const uint32_t x = *reinterpret_cast<const uint16_t*>(t.plo + 2 * c);
-    const uint32_t y = *reinterpret_cast<const uint16_t*>(t.phi + 2 * c);
+  if (packed) {  // 2-bit codes, 2 bytes per 8 codes
+    // CAPI records: always inside the 58-byte data field; 2-bit stream: the chunk index is
+    // clamped to the target's last chunk (an empty target reads 2 bytes at its dummy address;
+    // a last chunk may read 1 byte past the target, which the host pads)
+    uint32_t cl = (uint32_t)c, ch = (uint32_t)c;
+    if (packed == SWK_PACK_STREAM) {
+      cl = min(cl, max((t.llo + 7) / 8, 1u) - 1);
+      ch = min(ch, max((t.lhi + 7) / 8, 1u) - 1);
+    }
+    const uint32_t x = *reinterpret_cast<const uint16_t*>(t.plo + 2 * cl);
+    const uint32_t y = *reinterpret_cast<const uint16_t*>(t.phi + 2 * ch);
     lo = unpack8(x);
     hi = unpack8(y);
     if (!full) {
@@ -412,7 +420,7 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint3
 // optimistic f16 pass flagged).
 __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t* offs,
                                               const uint32_t* lens, size_t n, int tile, int lane,
-                                              bool packed, const uint32_t* idx) {
+                                              uint32_t packed, const uint32_t* idx) {
   Lane2 t;
   size_t a = (size_t)tile * SWB_TILE + lane, b = a + 64;
   const bool va = a < n, vb = b < n;  // positions in the batch
@@ -424,7 +432,7 @@ __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t
   const size_t p0 = (size_t)tile * SWB_TILE;
   if (p0 >= n) {
     t.llo = t.lhi = 0u;
-    t.plo = t.phi = packed ? res + 6 : reinterpret_cast<const uint8_t*>(lens);
+    t.plo = t.phi = packed == SWK_PACK_RECORDS ? res + 6 : reinterpret_cast<const uint8_t*>(lens);
     return t;
   }
   if (!va) a = p0;
@@ -433,7 +441,7 @@ __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t
     a = idx[a];
     b = idx[b];
   }
-  if (packed) {
+  if (packed == SWK_PACK_RECORDS) {
     t.llo = va ? *reinterpret_cast<const uint16_t*>(res + a * SWB_RECORD + 4) : 0u;
     t.lhi = vb ? *reinterpret_cast<const uint16_t*>(res + b * SWB_RECORD + 4) : 0u;
     t.plo = res + a * SWB_RECORD + 6;
@@ -483,7 +491,8 @@ struct ScoreArgs {
   uint2* edge_out;
   uint32_t ecols;
   uint32_t accum;
-  uint32_t packed;        // res = 64-byte CAPI records (2-bit codes); offs/lens unused
+  uint32_t packed;        // SWK_PACK_*: code bytes | 64-byte CAPI records (2-bit codes;
+                          // offs/lens unused) | 2-bit stream (offs in bytes, lens in codes)
   // optional position -> target map: positions [0, *nidx) score targets idx[k] (scores are
   // written to scores[idx[k]]); used to re-score the pairs an optimistic f16 pass flagged
   const uint32_t* idx;
@@ -509,12 +518,13 @@ __device__ __forceinline__ void dma_edge_chunk(const uint2* src, uint2* dst, int
 
 // Chunk count of a tile (uniform), from the lengths alone.
 __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens, size_t n,
-                                        int tile, int lane, bool packed, const uint32_t* idx) {
+                                        int tile, int lane, uint32_t packed, const uint32_t* idx) {
   const size_t a = (size_t)tile * SWB_TILE + lane, b = a + 64;
   auto len = [&](size_t k) -> uint32_t {
     if (k >= n) return 0u;
     if (idx) k = idx[k];
-    return packed ? *reinterpret_cast<const uint16_t*>(res + k * SWB_RECORD + 4) : lens[k];
+    return packed == SWK_PACK_RECORDS ? *reinterpret_cast<const uint16_t*>(res + k * SWB_RECORD + 4)
+                                      : lens[k];
   };
   uint32_t L = max(len(a), len(b));
 #pragma unroll
@@ -564,7 +574,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int ntiles = (int)((n + SWB_TILE - 1) / SWB_TILE);
   const int G = (int)gridDim.x;
   int total = 0;  // chunks of all this workgroup's tiles: every wave runs total + W - 1 phases
-  const bool packed = a.packed != 0;
+  const uint32_t packed = a.packed;
   for (int t = blockIdx.x; t < ntiles; t += G)
     total += tile_nch(a.res, a.lens, n, t, lane, packed, a.idx);
 
@@ -1115,15 +1125,15 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
   const size_t tA = 2 * pair, tB = tA + 1;
   const size_t n = a.n;
   if (tA >= n) return;  // whole wave
-  const bool packed = a.packed != 0;
-  const uint32_t LA = packed ? *reinterpret_cast<const uint16_t*>(a.res + tA * SWB_RECORD + 4)
-                             : a.lens[tA];
+  const bool packed = a.packed != SWK_PACK_BYTES, rec = a.packed == SWK_PACK_RECORDS;
+  const uint32_t LA = rec ? *reinterpret_cast<const uint16_t*>(a.res + tA * SWB_RECORD + 4)
+                          : a.lens[tA];
   const uint32_t LB = tB >= n ? 0u
-                      : packed ? *reinterpret_cast<const uint16_t*>(a.res + tB * SWB_RECORD + 4)
-                               : a.lens[tB];
-  const uint8_t* pA = packed ? a.res + tA * SWB_RECORD + 6 : a.res + (LA ? a.offs[tA] : 0);
-  const uint8_t* pB = packed ? a.res + (tB < n ? tB : tA) * SWB_RECORD + 6
-                             : a.res + (LB ? a.offs[tB] : 0);
+                      : rec ? *reinterpret_cast<const uint16_t*>(a.res + tB * SWB_RECORD + 4)
+                            : a.lens[tB];
+  const uint8_t* pA = rec ? a.res + tA * SWB_RECORD + 6 : a.res + (LA ? a.offs[tA] : 0);
+  const uint8_t* pB = rec ? a.res + (tB < n ? tB : tA) * SWB_RECORD + 6
+                          : a.res + (LB ? a.offs[tB] : 0);
   const int Lmax = (int)__builtin_amdgcn_readfirstlane(max(LA, LB));
   const uint32_t S = a.S, pad = a.pad;
   const u16x2 S2 = {(unsigned short)S, (unsigned short)S};

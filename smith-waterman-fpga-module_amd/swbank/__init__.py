@@ -260,7 +260,7 @@ class ScoreBank:
         res = np.ascontiguousarray(residues, dtype=np.uint8)
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
         ln = np.ascontiguousarray(lens, dtype=np.uint32)
-        out = np.zeros(len(ln), dtype=np.int32)
+        out = np.empty(len(ln), dtype=np.int32)  # every entry written by the library
         if len(ln) == 0:
             return out
         self._check(lib().sw_score_batch(self._h, _p(res), _p(offs), _p(ln), len(ln), _p(out)))

@@ -116,3 +116,39 @@ def test_feeder_records_many_chunks(monkeypatch):
         with pytest.raises(S.SwbankError) as ei:
             bank.score_records(recs)
         assert ei.value.status == S.ERR_ARG and "record 40000" in str(ei.value)
+
+
+@pytest.mark.parametrize("case", ["merged", "gotoh", "profile", "long-query", "wave"])
+def test_feeder_two_bit_chunks(monkeypatch, case):
+    """DNA chunks without N cross PCIe as the 2-bit stream (SWK_PACK_STREAM, each target from
+    a byte boundary); a chunk holding an N falls back to code bytes.  Ragged lengths 0-300
+    (every residue count mod 4/8/16, empty targets), N only in the middle of the batch, several
+    chunks in flight: the scores equal the byte path's (SWBANK_PACK2=0) and the oracle's."""
+    monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
+    if case == "profile":
+        monkeypatch.setenv("SWBANK_PROFILE", "1")
+    if case == "wave":
+        monkeypatch.setenv("SWBANK_KERNEL", "wave")
+    rng = np.random.default_rng(len(case) * 7919)
+    res, offs, lens = _ragged(rng, 24000, 0, 300)  # ~3.6 MB of codes: 3-4 chunks
+    mid = slice(int(offs[10000]), int(offs[10400]))
+    res[mid][rng.random(mid.stop - mid.start) < 0.05] = 4  # N in one chunk only
+    qlen = 700 if case == "long-query" else 120
+    q = rng.integers(0, 4, qlen, dtype=np.uint8)
+    gotoh = case == "gotoh"
+    params = (5, -4, -10, -1) if gotoh else REF
+    with S.ScoreBank(gap_model=S.GAP_GOTOH if gotoh else S.GAP_MERGED) as bank:
+        bank.set_penalties(*params)
+        bank.load_query(q)
+        got = bank.score_batch(res, offs, lens)
+        kern = bank.last_kernel()
+        monkeypatch.setenv("SWBANK_PACK2", "0")
+        ref = bank.score_batch(res, offs, lens)
+    assert np.array_equal(got, ref), kern
+    if case == "wave":
+        assert kern.startswith("wave"), kern
+    sel = np.concatenate([np.arange(10000, 10400), rng.choice(len(lens), 1500, replace=False)])
+    sub = [res[int(offs[k]):int(offs[k]) + int(lens[k])] for k in sel]
+    want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(*params[:2]), *params[2:],
+                         O.GAP_GOTOH if gotoh else O.GAP_MERGED)
+    assert np.array_equal(got[sel], want), kern
