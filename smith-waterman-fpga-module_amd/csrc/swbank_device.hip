@@ -1105,6 +1105,34 @@ static inline uint32_t pack_2bit(const uint8_t* src, uint32_t l, uint8_t* dst) {
   return orc;
 }
 
+// l code bytes -> ceil(l/2) bytes of 4-bit codes, low nibble first.  Returns the largest code
+// (the packing is valid when it is below the alphabet size, at most 15).
+static inline uint32_t pack_4bit(const uint8_t* src, uint32_t l, uint8_t* dst) {
+  uint32_t j = 0, mx = 0;
+#if defined(__SSE2__)
+  __m128i mv = _mm_setzero_si128();
+  const __m128i m16 = _mm_set1_epi16(0x00FF);
+  for (; j + 16 <= l; j += 16) {  // 16 codes -> 8 bytes
+    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + j));
+    mv = _mm_max_epu8(mv, v);
+    __m128i x = _mm_and_si128(_mm_or_si128(v, _mm_srli_epi16(v, 4)), m16);
+    x = _mm_packus_epi16(x, x);
+    _mm_storel_epi64(reinterpret_cast<__m128i*>(dst + j / 2), x);
+  }
+  mv = _mm_max_epu8(mv, _mm_srli_si128(mv, 8));
+  mv = _mm_max_epu8(mv, _mm_srli_si128(mv, 4));
+  mv = _mm_max_epu8(mv, _mm_srli_si128(mv, 2));
+  mv = _mm_max_epu8(mv, _mm_srli_si128(mv, 1));
+  mx = (uint32_t)_mm_cvtsi128_si32(mv) & 0xFFu;
+#endif
+  for (; j < l; j += 2) {
+    const uint32_t a = src[j], c = j + 1 < l ? src[j + 1] : 0u;
+    mx = std::max(mx, std::max(a, c));
+    dst[j / 2] = (uint8_t)((a & 15u) | (c & 15u) << 4);
+  }
+  return mx;
+}
+
 extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const uint64_t* offsets,
                                     const uint32_t* lens, size_t n, int32_t* scores_out) {
   if (!b) return SW_ERR_ARG;
@@ -1170,10 +1198,14 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const u
   add_chunk(n, total);
   std::vector<uint32_t> chunk_max(chunks.size(), 0);  // set by the chunk's gather
   const uint32_t alpha = (uint32_t)b->alpha;
-  const bool pack2 = b->alpha == SW_DNA_ALPHA && env_int("SWBANK_PACK2", 1) != 0;
+  // DNA: the 2-bit stream while the chunks hold no N; from the first chunk with N on, the
+  // 4-bit stream (2-bit attempts would be discarded packing passes where N is common)
+  const bool dna_pack = b->alpha == SW_DNA_ALPHA && env_int("SWBANK_PACK2", 1) != 0;
+  bool pack2 = dna_pack;
   HIPOK(b, hipSetDevice(b->device));
-  std::vector<char> has_perm(chunks.size(), 0), two_bit(chunks.size(), 0);
-  std::vector<size_t> part(T + 1), part2(T + 1);
+  std::vector<char> has_perm(chunks.size(), 0);
+  std::vector<uint32_t> chunk_mode(chunks.size(), SWK_PACK_BYTES);
+  std::vector<size_t> part(T + 1), part2(T + 1), part4(T + 1);
   std::vector<uint32_t> partmax(T);
   std::atomic<size_t> bad{SIZE_MAX};
   std::atomic<uint32_t> wide{0};
@@ -1189,26 +1221,31 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const u
     const size_t step = (cnt + T - 1) / T;
     std::fill(part.begin(), part.end(), 0);
     std::fill(part2.begin(), part2.end(), 0);
+    std::fill(part4.begin(), part4.end(), 0);
     pool.run([&](unsigned p) {
-      size_t acc = 0, acc2 = 0;
+      size_t acc = 0, acc2 = 0, acc4 = 0;
       uint32_t m = 0;
       for (size_t k = c.c0 + std::min(cnt, p * step); k < c.c0 + std::min(cnt, (p + 1) * step);
            ++k) {
         acc += lens[k];
         acc2 += (lens[k] + 3) / 4;
+        acc4 += (lens[k] + 1) / 2;
         m = std::max(m, lens[k]);
       }
       part[p + 1] = acc;
       part2[p + 1] = acc2;
+      part4[p + 1] = acc4;
       partmax[p] = m;
     });
     chunk_max[gi] = *std::max_element(partmax.begin(), partmax.end());
     for (unsigned p = 0; p < T; ++p) {
       part[p + 1] += part[p];
       part2[p + 1] += part2[p];
+      part4[p + 1] += part4[p];
     }
+    uint32_t mode = SWK_PACK_BYTES;
     bool two = pack2;
-    if (two) {  // optimistic: any code > 3 (N, or outside the alphabet) -> the byte path
+    if (two) {  // optimistic: any code > 3 (N, or outside the alphabet) -> 4 bits or bytes
       wide = 0;
       pool.run([&](unsigned p) {
         size_t at = part2[p];
@@ -1224,9 +1261,34 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const u
         if (orc > 3u) wide = 1;
       });
       two = wide.load() == 0;
-      if (two) std::memset(codes + part2[T], 0, 16);  // a last chunk reads 1 byte past
+      if (two) {
+        std::memset(codes + part2[T], 0, 16);  // a last chunk reads 1 byte past
+        mode = SWK_PACK_STREAM;
+      } else {
+        pack2 = false;
+      }
     }
-    if (!two) {
+    if (mode == SWK_PACK_BYTES && dna_pack) {  // 4-bit: every code below the alphabet size
+      wide = 0;
+      pool.run([&](unsigned p) {
+        size_t at = part4[p];
+        uint32_t mx = 0;
+        for (size_t i = std::min(cnt, p * step); i < std::min(cnt, (p + 1) * step); ++i) {
+          const size_t k = c.c0 + i;
+          const uint32_t l = lens[k];
+          mx = std::max(mx, pack_4bit(residues + offsets[k], l, codes + at));
+          so[i] = at;
+          sl[i] = l;
+          at += (l + 1) / 2;
+        }
+        if (mx >= alpha) wide = 1;
+      });
+      if (wide.load() == 0) {
+        std::memset(codes + part4[T], 0, 16);  // a last chunk reads up to 3 bytes past
+        mode = SWK_PACK_NIBBLE;
+      }
+    }
+    if (mode == SWK_PACK_BYTES) {
       pool.run([&](unsigned p) {
         size_t at = part[p];
         for (size_t i = std::min(cnt, p * step); i < std::min(cnt, (p + 1) * step); ++i) {
@@ -1258,16 +1320,18 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const u
         return 0;
       }
     }
-    two_bit[gi] = two;
+    chunk_mode[gi] = mode;
     has_perm[gi++] = chunk_perm(pool, sl, cnt, reinterpret_cast<uint32_t*>(slot + tl.perm_at));
     *reinterpret_cast<uint32_t*>(slot + tl.cnt_at) = (uint32_t)cnt;
-    return ca + (two ? align16(part2[T] + 16) : align16(part[T]));
+    return ca + (mode == SWK_PACK_STREAM   ? align16(part2[T] + 16)
+                 : mode == SWK_PACK_NIBBLE ? align16(part4[T] + 16)
+                                           : align16(part[T]));
   };
   const auto score = [&](uint8_t* dslot, const Chunk& c, int32_t* d_scores) -> sw_status {
     const size_t cnt = c.c1 - c.c0;
     const SlotTail tl = slot_tail(cnt * 8, cnt);
     const bool pm = has_perm[si];
-    const uint32_t mode = two_bit[si] ? SWK_PACK_STREAM : SWK_PACK_BYTES;
+    const uint32_t mode = chunk_mode[si];
     const uint32_t ml = chunk_max[si++];
     return launch(b, dslot + codes_at(cnt), reinterpret_cast<const uint64_t*>(dslot),
                   reinterpret_cast<const uint32_t*>(dslot + tl.lens_at), cnt, ml, d_scores,

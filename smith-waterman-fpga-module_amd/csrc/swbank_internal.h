@@ -22,5 +22,7 @@
 #define SWK_PACK_BYTES 0u
 #define SWK_PACK_RECORDS 1u
 #define SWK_PACK_STREAM 2u
+/* 4-bit stream: 2 codes per byte, low nibble first (DNA chunks that hold an N). */
+#define SWK_PACK_NIBBLE 3u
 
 #endif

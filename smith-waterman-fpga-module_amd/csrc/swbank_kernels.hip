@@ -365,6 +365,13 @@ __device__ __forceinline__ uint2 unpack8(uint32_t b) {
                     ((b >> 8) & 3u) | ((b >> 2) & 0x300u) | ((b << 4) & 0x30000u) |
                         ((b << 10) & 0x3000000u));
 }
+// 8 four-bit codes (low nibble first) -> 8 code bytes: the nibbles of even and odd codes
+// apart, then one v_perm per 4 codes interleaves them.
+__device__ __forceinline__ uint2 unpack8n(uint32_t x) {
+  const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
+  return make_uint2(__builtin_amdgcn_perm(hi, lo, 0x05010400u),
+                    __builtin_amdgcn_perm(hi, lo, 0x07030602u));
+}
 // Past-the-end codes of a chunk -> pad (bytes k with j0 + k >= len).
 __device__ __forceinline__ uint2 pad_tail(uint2 w, uint32_t j0, uint32_t len, uint32_t pad) {
   const uint32_t n = len > j0 ? min(len - j0, 8u) : 0u;  // valid codes in this chunk
@@ -377,7 +384,16 @@ __device__ __forceinline__ uint2 pad_tail(uint2 w, uint32_t j0, uint32_t len, ui
 __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint32_t pad,
                                          uint32_t packed, uint2& lo, uint2& hi) {
   const uint32_t j0 = (uint32_t)c * 8;
-  if (packed) {  // 2-bit codes, 2 bytes per 8 codes
+  if (packed == SWK_PACK_NIBBLE) {  // 4-bit stream, 4 bytes per 8 codes, clamped like below
+    const uint32_t cl = min((uint32_t)c, max((t.llo + 7) / 8, 1u) - 1);
+    const uint32_t ch = min((uint32_t)c, max((t.lhi + 7) / 8, 1u) - 1);
+    lo = unpack8n(*reinterpret_cast<const uint32_t*>(t.plo + 4 * cl));
+    hi = unpack8n(*reinterpret_cast<const uint32_t*>(t.phi + 4 * ch));
+    if (!full) {
+      lo = pad_tail(lo, j0, t.llo, pad);
+      hi = pad_tail(hi, j0, t.lhi, pad);
+    }
+  } else if (packed) {  // 2-bit codes, 2 bytes per 8 codes
     // CAPI records: always inside the 58-byte data field; 2-bit stream: the chunk index is
     // clamped to the target's last chunk (an empty target reads 2 bytes at its dummy address;
     // a last chunk may read 1 byte past the target, which the host pads)
@@ -1126,6 +1142,7 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
   const size_t n = a.n;
   if (tA >= n) return;  // whole wave
   const bool packed = a.packed != SWK_PACK_BYTES, rec = a.packed == SWK_PACK_RECORDS;
+  const bool nib = a.packed == SWK_PACK_NIBBLE;
   const uint32_t LA = rec ? *reinterpret_cast<const uint16_t*>(a.res + tA * SWB_RECORD + 4)
                           : a.lens[tA];
   const uint32_t LB = tB >= n ? 0u
@@ -1196,7 +1213,10 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
     if (even && (t & 63) == 0) {  // next 64 columns of both targets, one code pair per lane
       const uint32_t c = (uint32_t)t + lane;
       uint32_t x = pad, y = pad;
-      if (packed) {
+      if (nib) {
+        if (c < LA) x = (pA[c >> 1] >> (4 * (c & 1))) & 15u;
+        if (c < LB) y = (pB[c >> 1] >> (4 * (c & 1))) & 15u;
+      } else if (packed) {
         if (c < LA) x = (pA[c >> 2] >> (2 * (c & 3))) & 3u;
         if (c < LB) y = (pB[c >> 2] >> (2 * (c & 3))) & 3u;
       } else {
