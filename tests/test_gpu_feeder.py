@@ -121,7 +121,8 @@ def test_feeder_records_many_chunks(monkeypatch):
 @pytest.mark.parametrize("case", ["merged", "gotoh", "profile", "long-query", "wave"])
 def test_feeder_two_bit_chunks(monkeypatch, case):
     """DNA chunks without N cross PCIe as the 2-bit stream (SWK_PACK_STREAM, each target from
-    a byte boundary); a chunk holding an N falls back to code bytes.  Ragged lengths 0-300
+    a byte boundary); the chunk holding an N and those after it cross as 4-bit codes
+    (SWK_PACK_NIBBLE).  Ragged lengths 0-300
     (every residue count mod 4/8/16, empty targets), N only in the middle of the batch, several
     chunks in flight: the scores equal the byte path's (SWBANK_PACK2=0) and the oracle's."""
     monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
