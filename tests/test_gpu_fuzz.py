@@ -1,6 +1,8 @@
 """Seeded fuzz: random alphabets, matrices, gap penalties, gap models, query and target
 lengths (incl. empty, 1, segment and f16-bound edges), homologous and random targets —
 every case bit-exact against the oracle, through tile/wave x f16/u16 (the autouse fixture)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -56,7 +58,12 @@ def _case(seed):
     return dna, A, sub, pen, go, ge, model, q, seqs
 
 
-@pytest.mark.parametrize("seed", range(150))
+#  SWBANK_FUZZ_SEEDS=n (default 150) / SWBANK_FUZZ_BASE=b: seeds b .. b+n-1 (long soak runs)
+_BASE = int(os.environ.get("SWBANK_FUZZ_BASE", "0"))
+_SEEDS = int(os.environ.get("SWBANK_FUZZ_SEEDS", "150"))
+
+
+@pytest.mark.parametrize("seed", range(_BASE, _BASE + _SEEDS))
 def test_fuzz_vs_oracle(seed):
     dna, A, sub, pen, go, ge, model, q, seqs = _case(seed)
     with S.ScoreBank(alphabet=S.ALPHABET_DNA if dna else S.ALPHABET_PROTEIN,
