@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--qlen", type=int, default=128)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--ragged", action="store_true", help="lengths uniform in [L/2, L]")
+    ap.add_argument("--n-frac", type=float, default=0.0,
+                    help="fraction of residues set to N (the feeder then sends 4-bit chunks)")
     args = ap.parse_args()
     import swbank as S
     from oracle import oracle as O
@@ -33,8 +35,10 @@ def main():
     offs = np.zeros(n, np.uint64)
     offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
     res = O.random_codes(2, int(lens.sum()), 4)
+    if args.n_frac > 0:
+        res[rng.random(res.size) < args.n_frac] = 4
     cells = float(args.qlen) * float(lens.sum())
-    out = {"n": n, "L": L, "qlen": args.qlen, "ragged": args.ragged}
+    out = {"n": n, "L": L, "qlen": args.qlen, "ragged": args.ragged, "n_frac": args.n_frac}
     with S.ScoreBank(device=0) as bank:
         bank.set_penalties(5, -4, -12, -4)
         bank.load_query(q)
@@ -48,7 +52,7 @@ def main():
         out["host_api_ms"] = round(min(ts) * 1e3, 2)
         out["host_api_gcups"] = round(cells / min(ts) / 1e9, 1)
         out["kernel"] = bank.last_kernel()
-        if not args.ragged and L <= S.RECORD_MAX_BASES:
+        if not args.ragged and not args.n_frac and L <= S.RECORD_MAX_BASES:
             recs = S.make_records(res.reshape(n, L))
             bank.score_records(recs)
             ts = []
