@@ -3,11 +3,17 @@
 
 Default workload (BASELINE.json configs[2], the 1-GPU GCUPS config; north_star "100 bp x
 500 bp batches"): the reference query ``data/query100.fa`` (128 bp, committed as a fixture)
-scored against a data500-shaped batch — ``--reps`` copies of 499 synthetic, seeded, uniform
-ACGT 128-bp targets per GPU (``data/generate.py:6-23`` shape; splitmix64, seed 1000+rank).
-Penalties 5/-4/-12/-4 (data/smith-waterman.py:6-10), merged gap model (the ScoreBank PE).
+scored against a SYNTHETIC data500-shaped batch — ``--reps`` x 499 seeded, uniform ACGT
+128-bp targets per GPU (the shape of ``data/data500.fa`` and of ``data/generate.py:6-23``;
+splitmix64, seed 1000+rank).  Penalties 5/-4/-12/-4 (data/smith-waterman.py:6-10), merged gap
+model (the ScoreBank PE).
 
 Other workloads (``--workload``), same JSON line:
+  data500        the literal reference batch ``data/data500.fa`` (committed fixture), replicated
+                 ``--reps`` times per GPU (cross-check of the synthetic default).
+  ragged         query100.fa x ``--reps`` x 499 synthetic targets per GPU with lengths uniform in
+                 [64, 150] and 0.1 % N (real reads are not uniform): the device API sorts them
+                 longest first on the device.
   reads150x1k    configs[3]: per GPU ``--reads`` synthetic 150-bp reads x a fixed slice of
                  ``--slice`` 1-kbp targets (every read x every target of the slice); each
                  1-kbp target is the bank query (2 segments of 512 rows), the reads the batch.
@@ -38,27 +44,38 @@ sys.path.insert(0, REPO)
 # MI355X constants (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 CUS, SIMD_PER_CU, CLK_GHZ = 256, 4, 2.4
 HBM_PEAK_GBS = 8000.0
-# VALU roofline.  Algorithmic work = 10 ops per cell for the merged-gap
-# recurrence, 11 for Gotoh (1 select, 6 max, 3 add).  Peak = packed 16-bit VALU rate: packed
-# ops (v_pk_*_f16/u16) and v_perm_b32 issue one wave64 instruction per 4 cycles per SIMD
-# (scripts/ubench/valu_rate.hip on MI355X: 0.244-0.27 wave-instr/SIMD/cycle at 2.4 GHz; f32
-# ops reach 0.44) = 16 lanes x 2 halves per clock per SIMD -> 78.6 T ops/s.  max3 and perm fuse
-# several algorithmic ops into one instruction, so frac > 1 is possible.
-# Issue bound: one instruction advances one query row for a lane's 2 targets (128 cells per
-# wave-instruction); instructions per row of the column body (csrc/swbank_kernels.hip):
-# f16 merged 6.5 (5.5 with the letter-pair table: no v_perm per row), f16 Gotoh 8.5, u16
-# merged 9, u16 Gotoh 11 (the column body both kernels share; the tile kernel adds 0.1-0.7 per
-# row of loop overhead, the wave kernel ~7 per step of K rows plus the 63-step lane skew).
+# The path is bound by VALU issue, not HBM or MFMA.
+# Ceiling (roofline.peak): a SIMD issues one wave64 VALU instruction per 4 cycles (packed
+# 16-bit ops, v_perm_b32 and 32-bit integer ops alike: scripts/ubench/valu_rate.hip measured
+# 0.244-0.27 wave-instr/SIMD/cycle), and one packed 16-bit instruction advances one query row
+# for 64 lanes x 2 targets = 128 cells.  The fewest such instructions per row the recurrence
+# needs on gfx950 (DESIGN §6 derivation: every add is its own instruction because no
+# instruction fuses an add into a max; v_pk_maximum3_f16 takes 3 inputs; the add's clamp is
+# max(0, .) for free; substitution words come from an LDS letter-pair table, off the VALU):
+#   merged (the ScoreBank PE): M = clamp(Hd + s), H = max3(M, Tu, Tl), MO = M - o,
+#     G = max3(MO, Tu, Tl), T = G - e, best = max3(best, H, H') per 2 rows -> 5.5
+#   Gotoh: D = clamp(Hd + s), H = max3(D, E, F), HN = H - o - e, E' = max3(0, HN, E - e) (2),
+#     F' = max3(0, HN, F - e) (2), best 0.5 -> 7.5
+# peak GCUPS = 1024 SIMDs x 2.4 GHz x 0.25 x 128 / that count; kernel-independent, so frac <= 1.
+# The kernel's own instruction stream (issue_bound_gcups / issue_frac) and the SURVEY's
+# 10-ops-per-cell unit (ops_basis, frac > 1 because max3 / clamp fuse ops) are side fields.
 OPS_PER_CELL = {"merged": 10, "gotoh": 11}
 VALU_PEAK_TOPS_16 = CUS * SIMD_PER_CU * 16 * 2 * CLK_GHZ / 1e3  # 78.6
 VALU_ISSUE_PER_SIMD_CLK = 0.25
+MIN_INSTR_PER_ROW = {"merged": 5.5, "gotoh": 7.5}
+# the kernels' own column bodies (csrc/swbank_kernels.hip): f16 merged 6.5 (5.5 with the
+# letter-pair table), f16 Gotoh 8.5, u16 merged 9, u16 Gotoh 11; the tile kernel adds 0.1-0.7
+# per row of loop overhead, the wave kernel ~7 per step of K rows plus the 63-step lane skew
 VALU_INSTR_PER_ROW = {"f16": 6.5, "f16-pair": 5.5, "f16-gotoh": 8.5, "u16": 9.0,
                       "u16-gotoh": 11.0}
 
 
+def gcups_at(instr_per_row: float) -> float:
+    return CUS * SIMD_PER_CU * CLK_GHZ * VALU_ISSUE_PER_SIMD_CLK * 128 / instr_per_row
+
+
 def valu_peak_gcups(mode: str) -> float:
-    per_row = VALU_INSTR_PER_ROW[mode]
-    return CUS * SIMD_PER_CU * CLK_GHZ * VALU_ISSUE_PER_SIMD_CLK * 128 / per_row
+    return gcups_at(VALU_INSTR_PER_ROW[mode])
 PEN = (5, -4, -12, -4)
 
 
@@ -68,9 +85,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="q100xdata500",
-                    choices=["q100xdata500", "reads150x1k", "protein512x1k"])
+                    choices=["q100xdata500", "data500", "ragged", "reads150x1k", "protein512x1k"])
     ap.add_argument("--reps", type=int, default=2048,
-                    help="q100xdata500: copies of the 499-target data500 batch per GPU")
+                    help="q100xdata500 / data500 / ragged: copies of the 499-target data500 "
+                         "batch per GPU")
     ap.add_argument("--target-len", type=int, default=128)
     ap.add_argument("--reads", type=int, default=131072, help="reads150x1k: reads per GPU")
     ap.add_argument("--slice", type=int, default=16, help="reads150x1k: 1-kbp targets")
@@ -109,43 +127,78 @@ def pmc_traffic(workload: str):
     return None
 
 
+def ragged_batch(seed: int, n: int, lo: int = 64, hi: int = 150, p_n: float = 0.001):
+    """n synthetic DNA reads with lengths uniform in [lo, hi] and ~p_n N codes (seeded, the
+    same splitmix64 stream as make_codes): (codes, offsets u64, lens u32)."""
+    from oracle.oracle import random_codes, splitmix64_bytes
+    lens = (lo + (splitmix64_bytes(seed + 7, 2 * n).view(np.uint16).astype(np.uint32)
+                  % (hi - lo + 1))).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(lens.sum())
+    res = random_codes(seed, total, 4)
+    if p_n > 0:
+        u = splitmix64_bytes(seed + 11, 2 * total).view(np.uint16)
+        res[u < int(p_n * 65536)] = 4
+    return res, offs, lens
+
+
 class Workload:
-    """One rank's share: a list of (bank, query) jobs over one resident batch."""
+    """One rank's share: a list of (bank, query) jobs over one resident batch
+    (res / offs / lens: the batch's codes, offsets and lengths on the host)."""
 
     def __init__(self, args, rank, dev, S, torch):
         self.args = args
-        w = args.workload
-        if w == "q100xdata500":
-            q = load_query()
-            n, L = 499 * args.reps, args.target_len
-            self.batch = make_codes(1000 + rank, n, L)
-            self.queries = [q]
+        self.rank = rank
+        w = self.kind = args.workload
+        self.model = "merged"
+        self.params = {"penalties": list(PEN), "gap_model": "merged (ScoreBank PE)"}
+        self.sub = None
+        if w in ("q100xdata500", "data500", "ragged"):
+            self.queries = [load_query()]
             self.bank = S.ScoreBank(device=dev.index)
             self.bank.set_penalties(*PEN)
-            self.model = "merged"
+        if w == "q100xdata500":
+            n, L = 499 * args.reps, args.target_len
+            self.set_uniform(make_codes(1000 + rank, n, L))
             self.name = f"query100x{n}x{L}"
-            self.desc = (f"query100.fa (128 bp) x data500-shaped batch: {args.reps} x 499 "
-                         f"synthetic {L}-bp ACGT targets per GPU (BASELINE configs[2])")
-            self.params = {"penalties": list(PEN), "gap_model": "merged (ScoreBank PE)"}
+            self.desc = (f"query100.fa (128 bp) x synthetic data500-shaped batch: {args.reps} x "
+                         f"499 seeded uniform-ACGT {L}-bp targets per GPU (the shape of "
+                         f"data/data500.fa; BASELINE configs[2])")
+        elif w == "data500":
+            from oracle.oracle import encode_dna, golden_fasta, read_fasta
+            lib = [encode_dna(sq) for _, sq in read_fasta(golden_fasta("data500.fa"))]
+            if len({len(t) for t in lib}) != 1:
+                raise SystemExit("data500.fa: expected equal-length targets")
+            self.set_uniform(np.tile(np.stack(lib), (args.reps, 1)))
+            self.name = f"query100xdata500x{args.reps}"
+            self.desc = (f"query100.fa (128 bp) x the literal data/data500.fa (499 x "
+                         f"{len(lib[0])} bp) replicated {args.reps}x per GPU (BASELINE configs[2])")
+        elif w == "ragged":
+            n = 499 * args.reps
+            self.res, self.offs, self.lens = ragged_batch(1000 + rank, n)
+            self.n, self.L = n, int(self.lens.max())
+            self.name = f"query100xragged{n}"
+            self.desc = (f"query100.fa (128 bp) x {n} synthetic reads per GPU, lengths uniform in "
+                         f"[64, 150], 0.1% N (device API: on-device longest-first sort)")
         elif w == "reads150x1k":
             n, L = args.reads, 150
-            self.batch = make_codes(2000 + rank, n, L)
+            self.set_uniform(make_codes(2000 + rank, n, L))
             self.queries = list(make_codes(77, args.slice, 1000))  # the fixed 1-kbp slice
             self.bank = S.ScoreBank(device=dev.index)
             self.bank.set_penalties(*PEN)
-            self.model = "merged"
             self.name = f"reads150x{n}x1k{args.slice}"
             self.desc = (f"{n} synthetic 150-bp reads per GPU x a slice of {args.slice} "
                          f"synthetic 1-kbp targets (BASELINE configs[3]); target = bank query "
                          f"(2 x 512-row segments), reads = batch")
-            self.params = {"penalties": list(PEN), "gap_model": "merged (ScoreBank PE)"}
-        else:
+        elif w == "protein512x1k":
             n, L = args.ptargets, 1000
-            self.batch = make_codes(3000 + rank, n, L, 20)
+            self.set_uniform(make_codes(3000 + rank, n, L, 20))
             self.queries = [make_codes(99, 1, 512, 20)[0]]
             self.bank = S.ScoreBank(device=dev.index, alphabet=S.ALPHABET_PROTEIN,
                                     gap_model=S.GAP_GOTOH)
             from oracle.oracle import BLOSUM62
+            self.sub = BLOSUM62
             self.bank.set_matrix(BLOSUM62, -11, -1)
             self.model = "gotoh"
             self.name = f"protein512x{n}x1k"
@@ -153,20 +206,47 @@ class Workload:
                          f"gap -11/-1, Gotoh (BASELINE configs[4])")
             self.params = {"matrix": "BLOSUM62", "gap_open": -11, "gap_extend": -1,
                            "gap_model": "gotoh (ssearch36)"}
-        self.n, self.L = n, L
-        self.d_res = torch.from_numpy(self.batch.reshape(-1)).to(dev)
-        self.d_offs = torch.arange(n, dtype=torch.int64, device=dev) * L
-        self.d_lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+        n = self.n
+        self.d_res = torch.from_numpy(self.res).to(dev)
+        self.d_offs = torch.from_numpy(self.offs.view(np.int64)).to(dev)
+        self.d_lens = torch.from_numpy(self.lens.view(np.int32)).to(dev)
         self.d_sc = torch.zeros((len(self.queries), n), dtype=torch.int32, device=dev)
         self.d_rec = None
         if getattr(args, "records", False):
-            if w != "q100xdata500" or L > S.RECORD_MAX_BASES:
+            if w != "q100xdata500" or self.L > S.RECORD_MAX_BASES:
                 raise SystemExit("--records: q100xdata500 with targets <= 232 bp only")
-            self.d_rec = torch.from_numpy(S.make_records(self.batch).reshape(-1)).to(dev)
+            self.d_rec = torch.from_numpy(
+                S.make_records(self.res.reshape(n, self.L)).reshape(-1)).to(dev)
             self.desc += "; targets as CAPI 2-bit sequence_t records"
         if len(self.queries) == 1:
             self.bank.load_query(self.queries[0])
-        self.cells = sum(len(q) for q in self.queries) * n * L
+        self.cells = sum(len(q) for q in self.queries) * int(self.lens.sum(dtype=np.uint64))
+
+    def set_uniform(self, batch: np.ndarray):
+        n, L = batch.shape
+        self.res = np.ascontiguousarray(batch).reshape(-1)
+        self.offs = np.arange(n, dtype=np.uint64) * L
+        self.lens = np.full(n, L, dtype=np.uint32)
+        self.n, self.L = n, L
+
+    def regen_prefix(self, rank: int, m: int):
+        """The first m targets of rank `rank`'s batch, regenerated from its seed (rank 0 checks
+        the slices it gathered from the other ranks): (res, offs, lens)."""
+        w = self.kind
+        if w == "q100xdata500":
+            b = make_codes(1000 + rank, m, self.L)
+        elif w == "reads150x1k":
+            b = make_codes(2000 + rank, m, self.L)
+        elif w == "protein512x1k":
+            b = make_codes(3000 + rank, m, self.L, 20)
+        elif w == "data500":
+            b = self.res.reshape(self.n, self.L)[:m]
+        else:
+            res, offs, lens = ragged_batch(1000 + rank, self.n)
+            end = int(offs[m - 1] + lens[m - 1])
+            return res[:end], offs[:m], lens[:m]
+        return (np.ascontiguousarray(b).reshape(-1), np.arange(m, dtype=np.uint64) * self.L,
+                np.full(m, self.L, np.uint32))
 
     def run(self, stream, d_sc=None):
         d_sc = self.d_sc if d_sc is None else d_sc
@@ -191,7 +271,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs (not used by the driver): SWBENCH_BACKEND=gloo with SWBENCH_SHARE_GPU=1
-    # runs several ranks on one GPU to exercise the multi-rank flow
+    # runs several ranks on one GPU to exercise the multi-rank flow (tests/test_gpu_bench.py)
     backend = os.environ.get("SWBENCH_BACKEND", "nccl")
     if os.environ.get("SWBENCH_SHARE_GPU") == "1":
         local = 0
@@ -281,14 +361,13 @@ def main():
     if mode == "f16" and " pair " in kernel:
         mode = "f16-pair"
     kernel_gcups = cells_rank / score_s / 1e9
-    # issue bound of the column body (both kernels); the wave kernel's per-step overhead and
-    # lane skew come on top
-    peak_gcups = valu_peak_gcups(mode)
+    peak = gcups_at(MIN_INSTR_PER_ROW[wl.model])          # kernel-independent ceiling
+    own = valu_peak_gcups(mode)                           # this kernel's column body
     ops = OPS_PER_CELL[wl.model]
     achieved_tops = ops * kernel_gcups / 1e3
     # algorithmic bytes: 1 B per residue read once per query + 4 B per score written
-    per_target = S.RECORD_BYTES if wl.d_rec is not None else wl.L
-    alg_bytes = len(wl.queries) * wl.n * (per_target + 4) + sum(len(q) for q in wl.queries)
+    per_target = S.RECORD_BYTES * wl.n if wl.d_rec is not None else int(wl.lens.sum())
+    alg_bytes = len(wl.queries) * (per_target + 4 * wl.n) + sum(len(q) for q in wl.queries)
     traffic = pmc_traffic(wl.name)
 
     out = {
@@ -303,13 +382,13 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": arith,
-        "data": "synthetic",
+        "data": "synthetic" if wl.kind != "data500" else "reference fixture data/data500.fa",
         "config": {
             "workload": wl.desc,
             "query_len": [int(len(q)) for q in wl.queries][:1][0],
             "queries": len(wl.queries),
             "targets_per_gpu": wl.n,
-            "target_len": wl.L,
+            "target_len": wl.L if wl.kind != "ragged" else "64-150",
             **wl.params,
             "parallelism": f"dp{world}: pairs sharded, RCCL gather of scores to rank 0",
         },
@@ -317,15 +396,21 @@ def main():
         "kernel_ms": {"pack": round(pack_s * 1e3, 4), "score": round(score_s * 1e3, 4)},
         "roofline": {
             "bound": "valu",
-            "achieved": round(achieved_tops, 2),
-            "peak": round(VALU_PEAK_TOPS_16, 1),
-            "unit": (f"T ops/s ({ops} algorithmic int ops per cell, SURVEY 8.2; peak = packed "
-                     f"16-bit VALU, 1024 SIMDs x 32 ops/clk x {CLK_GHZ} GHz, measured issue rate)"),
-            "frac": round(achieved_tops / VALU_PEAK_TOPS_16, 4),
+            "achieved": round(kernel_gcups, 1),
+            "peak": round(peak, 1),
+            "unit": (f"GCUPS (peak = VALU issue ceiling: 1024 SIMDs x {CLK_GHZ} GHz x 1 wave64 "
+                     f"instr / 4 clk x 128 cells / {MIN_INSTR_PER_ROW[wl.model]} instr per row, "
+                     f"the fewest packed-16 instructions the {wl.model} recurrence needs on "
+                     f"gfx950, DESIGN §6)"),
+            "frac": round(kernel_gcups / peak, 4),
             "traffic": traffic,
-            "kernel_gcups": round(kernel_gcups, 1),
-            "issue_bound_gcups": round(peak_gcups, 1) if peak_gcups else None,
-            "issue_frac": round(kernel_gcups / peak_gcups, 4) if peak_gcups else None,
+            "issue_bound_gcups": round(own, 1),
+            "issue_frac": round(kernel_gcups / own, 4),
+            "ops_basis": {"achieved_tops": round(achieved_tops, 2),
+                          "peak_tops": round(VALU_PEAK_TOPS_16, 1),
+                          "frac": round(achieved_tops / VALU_PEAK_TOPS_16, 4),
+                          "unit": f"T int ops/s at {ops} algorithmic ops per cell (SURVEY 8.2); "
+                                  "max3 / clamp fuse ops, so > 1 is possible"},
         },
         "roofline_hbm": {
             "bound": "hbm",
@@ -338,13 +423,14 @@ def main():
         "cpu_baseline": None,
     }
 
+    last = bufs[(nstep[0] - 1) % 2]
     if rank == 0 and world == 1 and wl.d_rec is None and len(wl.queries) == 1:
-        out["pcie_inclusive"] = host_api_rate(wl, bufs[(nstep[0] - 1) % 2])
-    if rank == 0 and world == 1 and args.cpu_seconds > 0 and args.workload == "q100xdata500":
+        out["pcie_inclusive"] = host_api_rate(wl, last)
+    if rank == 0 and world == 1 and args.cpu_seconds > 0 and wl.kind == "q100xdata500":
         out["cpu_baseline"], out["parity_sample"] = cpu_baseline(
-            wl.queries[0], wl.batch, bufs[(nstep[0] - 1) % 2][0], wl.L, args.cpu_seconds)
+            wl.queries[0], wl.res.reshape(wl.n, wl.L), last[0], wl.L, args.cpu_seconds)
     elif rank == 0:
-        out["parity_sample"] = parity_sample(wl, bufs[(nstep[0] - 1) % 2])
+        out["parity_sample"] = parity_sample(wl, [g for g in gather] if gather else [last])
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -357,40 +443,38 @@ def host_api_rate(wl, d_sc, iters=5):
     """The same batch through the host-buffer API (sw_score_batch: host arrays in, scores out;
     gather, PCIe both ways and the kernel inside the clock) -- reported next to `value`, which
     is the HBM-resident rate.  Also checks its scores against the device-API run."""
-    n, L = wl.n, wl.L
-    res = wl.batch.reshape(-1)
-    offs = np.arange(n, dtype=np.uint64) * L
-    lens = np.full(n, L, dtype=np.uint32)
-    got = wl.bank.score_batch(res, offs, lens)  # first call sizes the pinned staging slots
+    got = wl.bank.score_batch(wl.res, wl.offs, wl.lens)  # first call sizes the pinned slots
     best = float("inf")
     for _ in range(iters):
         t0 = time.perf_counter()
-        wl.bank.score_batch(res, offs, lens)
+        wl.bank.score_batch(wl.res, wl.offs, wl.lens)
         best = min(best, time.perf_counter() - t0)
     same = bool(np.array_equal(got, d_sc[0].cpu().numpy()))
-    return {"value": round(len(wl.queries[0]) * n * L / best / 1e9, 1), "unit": "GCUPS",
+    return {"value": round(wl.cells / best / 1e9, 1), "unit": "GCUPS",
             "ms": round(best * 1e3, 3), "matches_device_api": same,
             "api": "sw_score_batch: host buffers, gather + PCIe + kernel + scores back, best of "
                    f"{iters}"}
 
 
-def parity_sample(wl, d_sc, m=256):
-    """Every query's scores for the first m targets of this rank's batch, re-computed by the
-    oracle (test infrastructure) and compared: the bench's own bit-exactness evidence."""
+def parity_sample(wl, per_rank, m=256):
+    """Every query's scores for the first m targets of every rank's batch (rank 0's own, and
+    at N>1 the slices it gathered from the others, regenerated from their seeds), re-computed
+    by the oracle (test infrastructure) and compared: the bench's own bit-exactness evidence."""
     from oracle import oracle as O
-    gpu = d_sc.cpu().numpy()
-    m = min(m, wl.n)
-    offs = (np.arange(m, dtype=np.uint64) * wl.L)
-    lens = np.full(m, wl.L, dtype=np.uint32)
     if wl.model == "gotoh":
-        sub, go, ge, model = O.BLOSUM62, -11, -1, O.GAP_GOTOH
+        sub, go, ge, model = wl.sub, -11, -1, O.GAP_GOTOH
     else:
         sub, go, ge, model = O.dna_matrix(PEN[0], PEN[1]), PEN[2], PEN[3], O.GAP_MERGED
-    mism = 0
-    for k, q in enumerate(wl.queries):
-        cpu = O.score_batch(q, wl.batch[:m].reshape(-1), offs, lens, sub, go, ge, model)
-        mism += int((cpu != gpu[k][:m]).sum())
-    return {"targets": m * len(wl.queries), "mismatches": mism}
+    m = min(m, wl.n)
+    mism, checked = 0, 0
+    for r, sc in enumerate(per_rank):
+        gpu = sc.cpu().numpy()
+        res, offs, lens = wl.regen_prefix(r, m)
+        for k, q in enumerate(wl.queries):
+            cpu = O.score_batch(q, res, offs, lens, sub, go, ge, model)
+            mism += int((cpu != gpu[k][:m]).sum())
+            checked += m
+    return {"targets": checked, "ranks": len(per_rank), "mismatches": mism}
 
 
 def cpu_baseline(q, tg, d_sc, L, budget_s):

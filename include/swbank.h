@@ -50,7 +50,9 @@
 extern "C" {
 #endif
 
-#define SWBANK_ABI_VERSION 1
+/* ABI 2: ids on the batch calls and the batch best hit (ScoreBank_v2.v:39-43), multi-device
+ * banks (sw_config.n_devices / devices[]), scores past the 16-bit lanes (int32 re-score). */
+#define SWBANK_ABI_VERSION 2
 
 typedef int32_t sw_status;
 enum {
@@ -58,7 +60,7 @@ enum {
   SW_ERR_ARG = -1,         /* bad argument (NULL pointer, code out of alphabet, ...)      */
   SW_ERR_NO_DEVICE = -2,   /* no HIP device / not gfx950                                 */
   SW_ERR_HIP = -3,         /* HIP runtime error (text in sw_last_error)                  */
-  SW_ERR_RANGE = -4,       /* score range of the 16-bit lanes could overflow             */
+  SW_ERR_RANGE = -4,       /* substitution span > 254 or gap penalties past the kernels  */
   SW_ERR_STATE = -5,       /* penalties or query not loaded yet                          */
   SW_ERR_NOMEM = -6,       /* host or device allocation failed                           */
   SW_ERR_IO = -7,          /* file I/O or parse error (FASTA helpers)                    */
@@ -76,12 +78,21 @@ enum { SW_DNA_T = 0, SW_DNA_C = 1, SW_DNA_A = 2, SW_DNA_G = 3, SW_DNA_N = 4 };
 #define SW_DNA_ALPHA 5
 #define SW_PROTEIN_ALPHA 24 /* ARNDCQEGHILKMFPSTWYVBZX* */
 
+#define SW_MAX_DEVICES 16
+
 typedef struct sw_config {
   int32_t device;        /* HIP device ordinal; -1 = current device                       */
   int32_t alphabet;      /* SW_ALPHABET_*                                                 */
   int32_t gap_model;     /* SW_GAP_*                                                      */
   uint32_t max_query_len;/* 0 = library maximum (sw_max_query_len())                      */
   uint32_t flags;        /* reserved, 0                                                   */
+  /* Multi-device bank (≙ MODULES scoring modules behind one PrioEncoder,
+   * ScoreBank_v2.v:76-148): n_devices > 1 spreads every host batch over devices[0..n)
+   * (length-balanced deal, one host thread per device) and gathers the scores on devices[0]
+   * with one RCCL gather (rccl.h ncclCommInitAll + ncclGather) when the devices are distinct,
+   * else with device copies.  0 or 1 = the single device `device`. */
+  int32_t n_devices;
+  int32_t devices[SW_MAX_DEVICES];
 } sw_config;
 
 typedef struct sw_bank sw_bank;
@@ -108,19 +119,37 @@ sw_status sw_set_matrix(sw_bank *bank, const int8_t *matrix, int32_t alpha, int3
 sw_status sw_load_query(sw_bank *bank, uint64_t id, const uint8_t *codes, uint32_t len);
 
 /* ---- target stream -> scores ----------------------------------------------------------- */
-/* Host buffers, blocking.  Target k = residues[offsets[k] .. offsets[k]+lens[k]) (codes).
+/* Host buffers, blocking.  Target k = residues[offsets[k] .. offsets[k]+lens[k]) (codes),
+ * tagged ids[k] (the RTL's 48-bit record ID, ScoreBank_v2.v:26-28,39-41; NULL = the index k).
  * scores_out[k] = max local-alignment score of (query, target k).  The bank feeds the batch in
  * chunks through pinned staging on its own worker threads and a copy stream (gather, PCIe and
- * scoring overlap), so host buffers need no pinning or layout; n < 2^32. */
+ * scoring overlap), so host buffers need no pinning or layout; n < 2^32.  The call also records
+ * the batch's best hit for sw_batch_best.  A multi-device bank deals the batch over its
+ * devices and gathers the scores back in input order. */
 sw_status sw_score_batch(sw_bank *bank, const uint8_t *residues, const uint64_t *offsets,
-                         const uint32_t *lens, size_t n, int32_t *scores_out);
+                         const uint32_t *lens, const uint64_t *ids, size_t n,
+                         int32_t *scores_out);
 
 /* Device buffers, asynchronous on `stream` (a hipStream_t; NULL = the bank's stream).
- * max_len must be >= every lens[k]. d_scores receives int32 scores in input order.
- * Nothing is copied to or from the host. */
+ * max_len must be >= every lens[k]; targets are visited in the caller's order unless their
+ * lengths differ, then longest first (an on-device length sort).  d_scores receives int32
+ * scores in input order.  With d_ids (device, may be NULL) the call also records the batch's
+ * best hit on the device (sw_batch_best); without, it records nothing.  Nothing is copied to
+ * or from the host.  Single-device banks only (SW_ERR_UNSUPPORTED on a multi-device bank). */
 sw_status sw_score_batch_device(sw_bank *bank, const uint8_t *d_residues,
-                                const uint64_t *d_offsets, const uint32_t *d_lens, size_t n,
-                                uint32_t max_len, int32_t *d_scores, void *stream);
+                                const uint64_t *d_offsets, const uint32_t *d_lens,
+                                const uint64_t *d_ids, size_t n, uint32_t max_len,
+                                int32_t *d_scores, void *stream);
+
+/* Best hit of the last batch call (≙ the bank's max / vld_max outputs, ScoreBank_v2.v:42-43):
+ * the lowest input index with the maximum score, its id (ids[index], the record's ID for
+ * sw_score_records, else the index) and score.  Waits for a device call's stream.
+ * SW_ERR_STATE when the last call tracked no best hit (a device call without d_ids). */
+sw_status sw_batch_best(sw_bank *bank, uint64_t *best_id, int32_t *best_score,
+                        uint64_t *best_index);
+
+/* Devices of the bank (1 for a single-device bank); writes min(count, cap) ordinals. */
+int32_t sw_bank_devices(const sw_bank *bank, int32_t *devices, int32_t cap);
 
 /* ---- CAPI record path: the reference host's packed wire format ---------
  * A record is the 64-byte `sequence_t` of capi_sample_aligner/.../aligner_Header.h:19-24:
@@ -132,13 +161,14 @@ sw_status sw_score_batch_device(sw_bank *bank, const uint8_t *d_residues,
 #define SW_RECORD_BYTES 64
 #define SW_RECORD_MAX_BASES 232
 sw_status sw_load_query_record(sw_bank *bank, const void *record);
-/* Host records in, unbiased scores out in input order (the kernel reads the 2-bit codes). */
+/* Host records in, unbiased scores out in input order (the kernel reads the 2-bit codes); the
+ * best hit (sw_batch_best) carries the record's ID.  Multi-device banks deal the records. */
 sw_status sw_score_records(sw_bank *bank, const void *records, size_t n, int32_t *scores_out);
 /* Device-resident records (n x 64 B) -> device scores, asynchronous on `stream`. */
 sw_status sw_score_records_device(sw_bank *bank, const void *d_records, size_t n,
                                   int32_t *d_scores, void *stream);
 
-/* Best hit of the last sw_score_batch (≙ max / vld_max): the lowest index with the maximum
+/* Best hit of a host score vector (≙ max / vld_max): the lowest index with the maximum
  * score; *best_id = ids ? ids[index] : index. */
 sw_status sw_best_hit(sw_bank *bank, const int32_t *scores, const uint64_t *ids, size_t n,
                       uint64_t *best_id, int32_t *best_score);

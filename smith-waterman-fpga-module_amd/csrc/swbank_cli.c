@@ -8,12 +8,16 @@
  *     271-285), one per library record, in library order (the RTL printed completion order).
  *
  * Usage: swbank -q query.fa -l library.fa [-p match,mismatch,open,extend] [-P] [-g]
- *               [-d device] [-o out.txt] [-T] [-R scores.txt]
+ *               [-d device[,device...]] [-o out.txt] [-T] [-R scores.txt] [-b]
  *   -p  penalties (default 5,-4,-12,-4: ScoreBank_v1_tb.sv:16-19, data/smith-waterman.py:6-10)
  *   -P  protein mode (BLOSUM62; -p gives only open,extend)      -g  Gotoh gap model
  *   -T  testbench transcript format "@     0ns: %10s score: \t%d"
  *   -R  also write an ssearch36 "-R" score file (data/score500.txt layout: one line per
  *       library record with name, length, score, record index and byte offset)
+ *   -d  HIP device, or a comma list for a multi-device bank (the library is dealt over the
+ *       devices, length-balanced, and the scores gathered back with RCCL; ScoreBank_v2.v:76-148
+ *       spreads targets over MODULES the same way)
+ *   -b  also print the bank's best hit ("best: >name score: S", ≙ max / vld_max) to stderr
  * FASTA: '>' starts a record (name = first token); sequence lines are concatenated; CR/LF,
  * blank lines and lower case are accepted; bytes outside the alphabet encode to N (DNA) or X
  * (protein), which score as mismatches (the testbench left them undefined, the CAPI host
@@ -100,21 +104,33 @@ fail:
 static void usage(const char *argv0) {
   fprintf(stderr,
           "usage: %s -q query.fa -l library.fa [-p match,mismatch,open,extend] [-P] [-g]\n"
-          "          [-d device] [-o out.txt] [-T] [-R scores.txt]\n",
+          "          [-d device[,device...]] [-o out.txt] [-T] [-R scores.txt] [-b]\n",
           argv0);
 }
 
 int main(int argc, char **argv) {
   const char *qpath = NULL, *lpath = NULL, *opath = NULL, *pen = NULL, *rpath = NULL;
-  int protein = 0, gotoh = 0, device = -1, transcript = 0, opt;
-  while ((opt = getopt(argc, argv, "q:l:p:Pgd:o:TR:h")) != -1) {
+  int protein = 0, gotoh = 0, device = -1, transcript = 0, best = 0, opt;
+  int ndev = 0, devs[SW_MAX_DEVICES];
+  while ((opt = getopt(argc, argv, "q:l:p:Pgd:o:TR:bh")) != -1) {
     switch (opt) {
       case 'q': qpath = optarg; break;
       case 'l': lpath = optarg; break;
       case 'p': pen = optarg; break;
       case 'P': protein = 1; break;
       case 'g': gotoh = 1; break;
-      case 'd': device = atoi(optarg); break;
+      case 'd': {
+        char *p = optarg, *end;
+        ndev = 0;
+        while (*p && ndev < SW_MAX_DEVICES) {
+          devs[ndev++] = (int)strtol(p, &end, 10);
+          if (end == p || (*end && *end != ',')) return usage(argv[0]), 1;
+          p = *end ? end + 1 : end;
+        }
+        device = devs[0];
+        break;
+      }
+      case 'b': best = 1; break;
       case 'o': opath = optarg; break;
       case 'T': transcript = 1; break;
       case 'R': rpath = optarg; break;
@@ -149,6 +165,10 @@ int main(int argc, char **argv) {
   sw_config cfg;
   sw_config_default(&cfg);
   cfg.device = device;
+  if (ndev > 1) { /* multi-device bank */
+    cfg.n_devices = ndev;
+    memcpy(cfg.devices, devs, sizeof(int) * (size_t)ndev);
+  }
   cfg.alphabet = alphabet;
   cfg.gap_model = gotoh ? SW_GAP_GOTOH : SW_GAP_MERGED;
   sw_bank *bank = NULL;
@@ -185,7 +205,7 @@ int main(int argc, char **argv) {
     lens[k] = (uint32_t)l;
     pos += l;
   }
-  if (st == SW_OK) st = sw_score_batch(bank, res, offs, lens, lib.n, scores);
+  if (st == SW_OK) st = sw_score_batch(bank, res, offs, lens, NULL, lib.n, scores);
   if (st != SW_OK) {
     fprintf(stderr, "swbank: %s: %s\n", sw_status_string(st), sw_last_error(bank));
     sw_bank_destroy(bank);
@@ -205,6 +225,10 @@ int main(int argc, char **argv) {
       fprintf(out, "%s score: %d\n", nm, scores[k]);
   }
   if (opath) fclose(out);
+  uint64_t bid = 0;
+  int32_t bsc = 0;
+  if (best && lib.n && sw_batch_best(bank, &bid, &bsc, NULL) == SW_OK)
+    fprintf(stderr, "best: >%s score: %d\n", lib.names[bid], bsc);
   if (rpath) { /* ssearch36 -R layout (data/score500.txt:1-3,502-503) */
     FILE *rf = fopen(rpath, "w");
     if (!rf) {

@@ -3,7 +3,9 @@
 // Call surface mirrors ScoreBank_v2 (reference ScoreBank/ScoreBank_v2.v:30-44): penalties once,
 // a query once, then any number of target batches; one max score per target.  See
 // include/swbank.h for the per-function reference citations.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: librccl is dlopen-ed by the first multi-device bank
 
 #include <algorithm>
 #include <cmath>
@@ -45,9 +47,20 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        const uint32_t* nidx, uint32_t idx_base, int pair,
                                        uint32_t pS1, uint32_t pS2, hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
-                                   unsigned long long* key, uint64_t* out, hipStream_t st);
+                                   unsigned long long* key, uint64_t* out, uint64_t* out_index,
+                                   hipStream_t st);
+extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max_len,
+                                    uint32_t* perm, uint32_t* perm_n, uint32_t* scratch,
+                                    hipStream_t st);
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
                                     uint32_t* idx, uint32_t* count, hipStream_t st);
+extern "C" size_t swk_i32_waves(size_t n, uint32_t scols, size_t budget_bytes);
+extern "C" hipError_t swk_launch_i32(int gotoh, const uint8_t* res, const uint64_t* offs,
+                                     const uint32_t* lens, size_t n, int packed,
+                                     const uint32_t* idx, const uint32_t* nidx, uint32_t idx_base,
+                                     const void* prof, uint32_t nstrips, uint32_t qlen,
+                                     uint32_t pad, uint32_t O, uint32_t E, int32_t* scores,
+                                     void* scratch, uint32_t scols, size_t waves, hipStream_t st);
 
 namespace {
 int env_int(const char* name, int dflt) {
@@ -203,6 +216,11 @@ struct sw_bank {
   DevBuf<uint32_t> qpair;
   uint32_t pair_bytes = 0, pS1 = 0, pS2 = 0;
   DevBuf<uint32_t> fb_idx, fb_cnt;  // pairs an optimistic f16 pass re-scores in u16
+  // int32 re-score of the pairs past the 16-bit lanes (built on first use per query):
+  // [strip][letter 0..pad][lane] 4 x int16, strips of 256 rows; per-wave scratch rows
+  bool i32_ready = false;
+  uint32_t i32_strips = 0;
+  DevBuf<uint2> i32prof, i32scr;
   DevBuf<unsigned long long> best_key;  // sw_best_hit_device scratch
   struct Seg { int W; size_t off, off16; };  // rows = W*R (last may be shorter); word offsets
                                               // in qtab and qtab16
@@ -233,7 +251,28 @@ struct sw_bank {
   DevBuf<uint32_t> lens;
   DevBuf<int32_t> scores;
 
-  char last_kernel[96] = {0};
+  char last_kernel[160] = {0};
+
+  // best hit of the last batch call (sw_batch_best, ≙ max / vld_max): 0 none, 1 on the host,
+  // 2 pending on the device (best_dev = {id, score, index} after best_ev)
+  int best_kind = 0;
+  uint64_t best_id = 0, best_index = 0;
+  int32_t best_score = 0;
+  DevBuf<uint64_t> best_dev;
+  hipEvent_t best_ev = nullptr;
+
+  // multi-device bank (cfg.n_devices > 1): one child bank per device, a host thread per device
+  // (dpool part d drives kids[d]), scores gathered on kids[0]'s device (grecv) by RCCL or copies
+  std::vector<sw_bank*> kids;
+  std::unique_ptr<HostPool> dpool;
+  std::vector<void*> comms;  // ncclComm_t per device (RCCL gather), empty -> copy gather
+  unsigned pool_threads = 0; // feeder threads (0: host_threads(); children share the host)
+  DevBuf<int32_t> grecv;
+  PinBuf hrecv;
+  // on-device longest-first order of a ragged device batch (sw_score_batch_device):
+  // dperm = visiting order + count, dsort = histogram / scan scratch
+  DevBuf<uint32_t> dperm, dsort;
+  bool is_multi() const { return !kids.empty(); }
 
   // Query tables are rewritten in place by prepare() while earlier launches may still read
   // them on the caller's stream: the upload (on the bank stream) waits for ev_used (recorded
@@ -278,6 +317,51 @@ extern "C" int32_t sw_device_count(void) {
   return n;
 }
 
+// RCCL for the multi-device score gather (SURVEY §8 e: ncclCommInitAll, rccl.h:236, and
+// ncclGather, rccl.h:745).  Loaded on first use so single-device users never map it; in a
+// process where PyTorch already mapped its librccl.so.1 that copy is reused (same SONAME).
+namespace {
+struct Rccl {
+  bool ok = false;
+  char err[160] = {0};
+  decltype(&ncclCommInitAll) commInitAll = nullptr;
+  decltype(&ncclCommDestroy) commDestroy = nullptr;
+  decltype(&ncclGather) gather = nullptr;
+  decltype(&ncclGetErrorString) errorString = nullptr;
+};
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      snprintf(r.err, sizeof(r.err), "dlopen librccl.so.1: %s", dlerror());
+      return;
+    }
+    r.commInitAll = reinterpret_cast<decltype(&ncclCommInitAll)>(dlsym(h, "ncclCommInitAll"));
+    r.commDestroy = reinterpret_cast<decltype(&ncclCommDestroy)>(dlsym(h, "ncclCommDestroy"));
+    r.gather = reinterpret_cast<decltype(&ncclGather)>(dlsym(h, "ncclGather"));
+    r.errorString = reinterpret_cast<decltype(&ncclGetErrorString)>(dlsym(h, "ncclGetErrorString"));
+    r.ok = r.commInitAll && r.commDestroy && r.gather && r.errorString;
+    if (!r.ok) snprintf(r.err, sizeof(r.err), "librccl.so.1 lacks ncclCommInitAll/ncclGather");
+  });
+  return r;
+}
+}  // namespace
+
+static sw_status check_device(int dev) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SW_ERR_NO_DEVICE;
+  if (dev < 0 || dev >= ndev) return SW_ERR_NO_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return SW_ERR_NO_DEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SW_ERR_NO_DEVICE;
+  return SW_OK;
+}
+
+static unsigned host_threads_total();
+
 extern "C" sw_status sw_bank_create(sw_bank** out, const sw_config* cfg_in) {
   if (!out) return SW_ERR_ARG;
   *out = nullptr;
@@ -289,17 +373,73 @@ extern "C" sw_status sw_bank_create(sw_bank** out, const sw_config* cfg_in) {
   if (cfg.alphabet != SW_ALPHABET_DNA && cfg.alphabet != SW_ALPHABET_PROTEIN) return SW_ERR_ARG;
   if (cfg.gap_model != SW_GAP_MERGED && cfg.gap_model != SW_GAP_GOTOH) return SW_ERR_ARG;
   if (cfg.max_query_len > SWB_MAX_QUERY) return SW_ERR_UNSUPPORTED;
+  if (cfg.n_devices < 0 || cfg.n_devices > SW_MAX_DEVICES) return SW_ERR_ARG;
 
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SW_ERR_NO_DEVICE;
-  int dev = cfg.device;
-  if (dev < 0) {
-    if (hipGetDevice(&dev) != hipSuccess) return SW_ERR_NO_DEVICE;
+  if (cfg.n_devices >= 1) {
+    // Multi-device bank (≙ MODULES ScoringModules behind one PrioEncoder, ScoreBank_v2.v:76-148):
+    // a child bank per device; every host batch is dealt over them.
+    for (int d = 0; d < cfg.n_devices; ++d) {
+      const sw_status st = check_device(cfg.devices[d]);
+      if (st != SW_OK) return st;
+    }
+    sw_bank* b = new (std::nothrow) sw_bank();
+    if (!b) return SW_ERR_NOMEM;
+    b->cfg = cfg;
+    b->device = cfg.devices[0];
+    b->alpha = cfg.alphabet == SW_ALPHABET_DNA ? SW_DNA_ALPHA : SW_PROTEIN_ALPHA;
+    for (int d = 0; d < cfg.n_devices; ++d) {
+      sw_config kc = cfg;
+      kc.n_devices = 0;
+      kc.device = cfg.devices[d];
+      sw_bank* k = nullptr;
+      const sw_status st = sw_bank_create(&k, &kc);
+      if (st != SW_OK) {
+        sw_bank_destroy(b);
+        return st;
+      }
+      k->pool_threads = std::max(2u, host_threads_total() / (unsigned)cfg.n_devices);
+      b->kids.push_back(k);
+    }
+    b->dpool.reset(new (std::nothrow) HostPool((unsigned)cfg.n_devices));
+    b->pool.reset(new (std::nothrow) HostPool(host_threads_total()));
+    if (!b->dpool || !b->pool) {
+      sw_bank_destroy(b);
+      return SW_ERR_NOMEM;
+    }
+    // RCCL gather when every device is distinct (RCCL refuses two ranks on one device) unless
+    // SWBANK_GATHER=copy; SWBANK_GATHER=rccl makes an RCCL failure an error instead of a
+    // fallback to device copies.
+    const char* gm = std::getenv("SWBANK_GATHER");
+    const bool force_copy = gm && std::strcmp(gm, "copy") == 0;
+    const bool force_rccl = gm && std::strcmp(gm, "rccl") == 0;
+    bool distinct = true;
+    for (int i = 0; i < cfg.n_devices; ++i)
+      for (int j = 0; j < i; ++j) distinct = distinct && cfg.devices[i] != cfg.devices[j];
+    if (!force_copy && (distinct || force_rccl)) {
+      const Rccl& r = rccl();
+      ncclResult_t nr = ncclSuccess;
+      if (r.ok) {
+        std::vector<ncclComm_t> comms((size_t)cfg.n_devices);
+        nr = r.commInitAll(comms.data(), cfg.n_devices, cfg.devices);
+        if (nr == ncclSuccess) b->comms.assign(comms.begin(), comms.end());
+      }
+      if (b->comms.empty() && force_rccl) {
+        sw_bank_destroy(b);
+        return SW_ERR_UNSUPPORTED;
+      }
+      if (b->comms.empty())
+        snprintf(b->err, sizeof(b->err), "RCCL unavailable (%s), gathering with device copies",
+                 r.ok ? r.errorString(nr) : r.err);
+    }
+    (void)hipSetDevice(b->device);
+    *out = b;
+    return SW_OK;
   }
-  if (dev >= ndev) return SW_ERR_NO_DEVICE;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return SW_ERR_NO_DEVICE;
-  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SW_ERR_NO_DEVICE;
+
+  int dev = cfg.device;
+  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return SW_ERR_NO_DEVICE;
+  const sw_status dst = check_device(dev);
+  if (dst != SW_OK) return dst;
 
   sw_bank* b = new (std::nothrow) sw_bank();
   if (!b) return SW_ERR_NOMEM;
@@ -325,6 +465,18 @@ extern "C" sw_status sw_bank_create(sw_bank** out, const sw_config* cfg_in) {
 
 extern "C" void sw_bank_destroy(sw_bank* b) {
   if (!b) return;
+  if (b->is_multi() || !b->comms.empty()) {
+    const Rccl& r = rccl();
+    for (void* c : b->comms) (void)r.commDestroy(static_cast<ncclComm_t>(c));
+    for (sw_bank* k : b->kids) sw_bank_destroy(k);
+    b->dpool.reset();
+    b->pool.reset();
+    (void)hipSetDevice(b->device);
+    b->grecv.release();
+    b->hrecv.release();
+    delete b;
+    return;
+  }
   (void)hipSetDevice(b->device);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   uint64_t nl;
@@ -336,9 +488,15 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->stage.release();
   if (b->ev_ready) (void)hipEventDestroy(b->ev_ready);
   if (b->ev_used) (void)hipEventDestroy(b->ev_used);
+  if (b->best_ev) (void)hipEventDestroy(b->best_ev);
   b->fb_idx.release();
   b->fb_cnt.release();
   b->best_key.release();
+  b->best_dev.release();
+  b->i32prof.release();
+  b->i32scr.release();
+  b->dperm.release();
+  b->dsort.release();
   b->wtab.release();
   b->wtab16.release();
   b->edge[0].release();
@@ -361,9 +519,22 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   delete b;
 }
 
+extern "C" int32_t sw_bank_devices(const sw_bank* b, int32_t* devices, int32_t cap) {
+  if (!b) return 0;
+  const int32_t n = b->is_multi() ? (int32_t)b->kids.size() : 1;
+  for (int32_t i = 0; devices && i < std::min(n, cap); ++i)
+    devices[i] = b->is_multi() ? b->kids[(size_t)i]->device : b->device;
+  return n;
+}
+
 extern "C" const char* sw_last_error(const sw_bank* b) { return b ? b->err : "null bank"; }
 
 extern "C" const char* sw_last_kernel(const sw_bank* b) { return b ? b->last_kernel : ""; }
+
+static void copy_kernel_name(sw_bank* b, const char* gather) {
+  snprintf(b->last_kernel, sizeof(b->last_kernel), "multi[%zu] gather=%s: %s", b->kids.size(),
+           gather, b->kids[0]->last_kernel);
+}
 
 static sw_status set_matrix_impl(sw_bank* b, const int8_t* m, int alpha, int32_t go,
                                  int32_t ge) {
@@ -378,9 +549,23 @@ static sw_status set_matrix_impl(sw_bank* b, const int8_t* m, int alpha, int32_t
   return SW_OK;
 }
 
+// Multi-device bank: apply a call to every child bank (the first failure's text is the bank's).
+template <class F>
+static sw_status each_kid(sw_bank* b, F&& f) {
+  for (sw_bank* k : b->kids) {
+    const sw_status st = f(k);
+    if (st != SW_OK) return fail(b, st, "device %d: %s", k->device, k->err);
+  }
+  return SW_OK;
+}
+
 extern "C" sw_status sw_set_penalties(sw_bank* b, int32_t match, int32_t mismatch,
                                       int32_t gap_open, int32_t gap_extend) {
   if (!b) return SW_ERR_ARG;
+  if (b->is_multi())
+    return each_kid(b, [&](sw_bank* k) {
+      return sw_set_penalties(k, match, mismatch, gap_open, gap_extend);
+    });
   if (b->cfg.alphabet != SW_ALPHABET_DNA)
     return fail(b, SW_ERR_ARG, "sw_set_penalties needs a DNA bank; use sw_set_matrix");
   int8_t m[SW_DNA_ALPHA * SW_DNA_ALPHA];
@@ -392,6 +577,8 @@ extern "C" sw_status sw_set_penalties(sw_bank* b, int32_t match, int32_t mismatc
 extern "C" sw_status sw_set_matrix(sw_bank* b, const int8_t* m, int32_t alpha, int32_t gap_open,
                                    int32_t gap_extend) {
   if (!b || !m) return SW_ERR_ARG;
+  if (b->is_multi())
+    return each_kid(b, [&](sw_bank* k) { return sw_set_matrix(k, m, alpha, gap_open, gap_extend); });
   const int want = b->cfg.alphabet == SW_ALPHABET_DNA ? SW_DNA_ALPHA : SW_PROTEIN_ALPHA;
   if (alpha != want) return fail(b, SW_ERR_ARG, "matrix alphabet %d, bank expects %d", alpha, want);
   return set_matrix_impl(b, m, alpha, gap_open, gap_extend);
@@ -399,6 +586,8 @@ extern "C" sw_status sw_set_matrix(sw_bank* b, const int8_t* m, int32_t alpha, i
 
 extern "C" sw_status sw_load_query(sw_bank* b, uint64_t id, const uint8_t* codes, uint32_t len) {
   if (!b || (!codes && len)) return SW_ERR_ARG;
+  if (b->is_multi())
+    return each_kid(b, [&](sw_bank* k) { return sw_load_query(k, id, codes, len); });
   const uint32_t cap = b->cfg.max_query_len ? b->cfg.max_query_len : SWB_MAX_QUERY;
   if (len > cap)
     return fail(b, SW_ERR_UNSUPPORTED, "query length %u exceeds the bank maximum %u", len, cap);
@@ -696,17 +885,43 @@ static sw_status prepare(sw_bank* b) {
   b->prof = prof;
   b->smax = smax;
   b->col0 = col0;
+  b->i32_ready = false;
   b->dirty = false;
   return SW_OK;
 }
 
-static sw_status range_check(sw_bank* b, uint32_t max_len) {
-  const uint64_t qlen = b->query.size();
-  const uint64_t cells = std::min<uint64_t>(qlen, max_len);
-  const uint64_t top = cells * (uint64_t)std::max(0, b->smax) + b->S;
-  if (top > 65535u)
-    return fail(b, SW_ERR_RANGE, "max score bound %llu exceeds the 16-bit lanes",
-                (unsigned long long)top);
+// int32 re-score state, built on first use per (penalties, query): the per-strip profile of
+// swk_launch_i32 ([strip][letter 0..pad][lane] 4 x int16: rows 4l..4l+3 of a 256-row strip;
+// letter = min(code, pad) as in the 16-bit kernels, the padding letter scoring S - 255 like
+// their padding row), uploaded on the bank stream like the other query tables.
+static sw_status prepare_i32(sw_bank* b) {
+  if (b->i32_ready) return SW_OK;
+  const int A = b->alpha;
+  const int8_t* m = b->matrix.data();
+  const uint32_t qlen = (uint32_t)b->query.size();
+  const uint32_t strips = std::max(1u, (qlen + 255) / 256), pad = b->pad;
+  if (pad + 1 > 25) return fail(b, SW_ERR_UNSUPPORTED, "int32 kernel: alphabet %d too large", A);
+  std::vector<int16_t> h((size_t)strips * (pad + 1) * 64 * 4, 0);
+  for (uint32_t s = 0; s < strips; ++s)
+    for (uint32_t c = 0; c <= pad; ++c)
+      for (uint32_t l = 0; l < 64; ++l)
+        for (uint32_t k = 0; k < 4; ++k) {
+          const uint32_t r = s * 256 + 4 * l + k;
+          int v = 0;
+          if (r < qlen) v = c < (uint32_t)A ? m[b->query[r] * A + c] : (int)b->S - 255;
+          h[(((size_t)s * (pad + 1) + c) * 64 + l) * 4 + k] = (int16_t)v;
+        }
+  HIPOK(b, hipSetDevice(b->device));
+  HIPOK(b, hipEventSynchronize(b->ev_ready));  // the staging buffer is free again
+  HIPOK(b, b->stage.reserve(h.size() * 2));
+  HIPOK(b, b->i32prof.reserve(h.size() / 4));
+  HIPOK(b, hipStreamWaitEvent(b->stream, b->ev_used, 0));
+  std::memcpy(b->stage.p, h.data(), h.size() * 2);
+  HIPOK(b, hipMemcpyAsync(b->i32prof.p, b->stage.p, h.size() * 2, hipMemcpyHostToDevice,
+                          b->stream));
+  HIPOK(b, hipEventRecord(b->ev_ready, b->stream));
+  b->i32_strips = strips;
+  b->i32_ready = true;
   return SW_OK;
 }
 
@@ -718,7 +933,19 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                         const uint32_t* d_lens, size_t n, uint32_t max_len, int32_t* d_scores,
                         hipStream_t st, uint32_t packed = SWK_PACK_BYTES,
                         const uint32_t* perm = nullptr,
-                        const uint32_t* perm_n = nullptr) {
+                        const uint32_t* perm_n = nullptr, bool dsort = false) {
+  // Past the 16-bit lanes (min(|q|, max|t|) * max(s) + max(s) > 65535) the 16-bit passes are
+  // still exact for every pair scoring <= 65535 - max(s); the pairs above are re-scored by the
+  // int32 kernel through an index list (swk_launch_i32).
+  const uint64_t bound = std::min<uint64_t>(b->query.size(), max_len) *
+                             (uint64_t)std::max(0, b->smax) + (uint64_t)std::max(0, b->smax);
+  const bool need32 = bound > 65535u || env_int("SWBANK_I32", 0) != 0;
+  if (need32) {
+    if (n > 0xFFFFFFFFull)
+      return fail(b, SW_ERR_RANGE, "batches past the 16-bit score bound hold < 2^32 targets");
+    const sw_status ps = prepare_i32(b);
+    if (ps != SW_OK) return ps;
+  }
   sw_bank::Ev ev{};
   if (b->timing) {
     HIPOK(b, hipEventCreate(&ev.a));
@@ -730,6 +957,9 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   // interval (a..b) is empty and kept only for ABI stability
   if (b->timing) HIPOK(b, hipEventRecord(ev.b, st));
   HIPOK(b, hipStreamWaitEvent(st, b->ev_ready, 0));  // the query tables are uploaded
+  // bank-owned scratch (edge rows, re-score lists, the device sort order, int32 scratch) is
+  // reused by every call: a call on another stream waits for the previous call to finish
+  HIPOK(b, hipStreamWaitEvent(st, b->ev_used, 0));
   const size_t nseg = b->segs.size();
   const bool rec = packed == SWK_PACK_RECORDS;
   const uint32_t ecols = (max_len + 7) / 8 * 8;
@@ -815,6 +1045,16 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
     snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=%zu", arith,
              b->prof ? "-profile" : use_pair ? " pair" : "", b->R, b->segs[0].W, nseg);
   }
+  // A device batch (dsort) visits its targets longest first, sorted on the device, so every
+  // tile holds similar lengths (a tile runs to its longest lane); SWBANK_DSORT=0 disables.
+  if (dsort && !use_wave && !perm && packed == SWK_PACK_BYTES && ntiles > 1 &&
+      n <= 0xFFFFFFFFull && env_int("SWBANK_DSORT", 1) != 0) {
+    HIPOK(b, b->dperm.reserve(n + 1));
+    HIPOK(b, b->dsort.reserve(2048));
+    HIPOK(b, swk_sort_lens(d_lens, n, max_len, b->dperm.p, b->dperm.p + n, b->dsort.p, st));
+    perm = b->dperm.p;
+    perm_n = b->dperm.p + n;
+  }
   // Segmented queries hand each segment's bottom row to the next through HBM: ntiles x ecols
   // x 512 B per edge buffer.  Past SWBANK_EDGE_MB (default 2048) the batch runs as
   // consecutive position ranges, each with its own edge rows.
@@ -880,6 +1120,23 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
       }
     }
   }
+  if (need32) {  // pairs above the 16-bit lanes' exact range -> int32 re-score
+    const uint32_t scols = std::max(max_len, 1u);
+    const size_t budget = (size_t)std::max(1, env_int("SWBANK_EDGE_MB", 2048)) << 20;
+    const size_t waves = swk_i32_waves(n, scols, budget);
+    HIPOK(b, b->fb_idx.reserve(n));
+    HIPOK(b, b->fb_cnt.reserve(1));
+    HIPOK(b, b->i32scr.reserve(waves * 2 * scols));
+    // SWBANK_I32=1 (tests): every pair through the int32 kernel
+    const int32_t thresh = bound > 65535u ? 65535 - std::max(0, b->smax) : -1;
+    HIPOK(b, swk_flag_high(d_scores, n, thresh, b->fb_idx.p, b->fb_cnt.p, st));
+    HIPOK(b, swk_launch_i32(gotoh ? 1 : 0, d_res, d_offs, d_lens, n, (int)packed, b->fb_idx.p,
+                            b->fb_cnt.p, 0, b->i32prof.p, b->i32_strips,
+                            (uint32_t)b->query.size(), b->pad, b->O, b->E, d_scores, b->i32scr.p,
+                            scols, waves, st));
+    const size_t L = strlen(b->last_kernel);
+    snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " +i32-rescore");
+  }
   HIPOK(b, hipEventRecord(b->ev_used, st));  // the next table upload waits for this
   if (b->timing) {
     HIPOK(b, hipEventRecord(ev.c, st));
@@ -888,19 +1145,58 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   return SW_OK;
 }
 
+// Record the batch best hit on the device (sw_batch_best reads it after best_ev).
+static sw_status track_best_device(sw_bank* b, const int32_t* d_scores, const uint64_t* d_ids,
+                                   size_t n, hipStream_t st) {
+  if (n > 0xFFFFFFFFull) return SW_OK;  // the key holds a 32-bit index: not tracked
+  HIPOK(b, b->best_key.reserve(1));
+  HIPOK(b, b->best_dev.reserve(3));
+  HIPOK(b, swk_best_hit(d_scores, d_ids, n, b->best_key.p, b->best_dev.p, b->best_dev.p + 2, st));
+  if (!b->best_ev) HIPOK(b, hipEventCreateWithFlags(&b->best_ev, hipEventDisableTiming));
+  HIPOK(b, hipEventRecord(b->best_ev, st));
+  b->best_kind = 2;
+  return SW_OK;
+}
+
 extern "C" sw_status sw_score_batch_device(sw_bank* b, const uint8_t* d_res,
                                            const uint64_t* d_offs, const uint32_t* d_lens,
-                                           size_t n, uint32_t max_len, int32_t* d_scores,
-                                           void* stream) {
+                                           const uint64_t* d_ids, size_t n, uint32_t max_len,
+                                           int32_t* d_scores, void* stream) {
   if (!b) return SW_ERR_ARG;
+  if (b->is_multi())
+    return fail(b, SW_ERR_UNSUPPORTED, "device buffers need a single-device bank");
+  b->best_kind = 0;
   if (n == 0) return SW_OK;
   if (!d_res || !d_offs || !d_lens || !d_scores) return fail(b, SW_ERR_ARG, "null device buffer");
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
-  if ((st = range_check(b, max_len)) != SW_OK) return st;
   HIPOK(b, hipSetDevice(b->device));
-  return launch(b, d_res, d_offs, d_lens, n, max_len, d_scores,
-                stream ? reinterpret_cast<hipStream_t>(stream) : b->stream);
+  hipStream_t hs = stream ? reinterpret_cast<hipStream_t>(stream) : b->stream;
+  if ((st = launch(b, d_res, d_offs, d_lens, n, max_len, d_scores, hs, SWK_PACK_BYTES, nullptr,
+                   nullptr, true)) != SW_OK)
+    return st;
+  return d_ids ? track_best_device(b, d_scores, d_ids, n, hs) : SW_OK;
+}
+
+extern "C" sw_status sw_batch_best(sw_bank* b, uint64_t* best_id, int32_t* best_score,
+                                   uint64_t* best_index) {
+  if (!b) return SW_ERR_ARG;
+  if (b->best_kind == 2) {
+    uint64_t h[3];
+    HIPOK(b, hipSetDevice(b->device));
+    HIPOK(b, hipEventSynchronize(b->best_ev));
+    HIPOK(b, hipMemcpy(h, b->best_dev.p, sizeof(h), hipMemcpyDeviceToHost));
+    b->best_id = h[0];
+    b->best_score = (int32_t)(int64_t)h[1];
+    b->best_index = h[2];
+    b->best_kind = 1;
+  }
+  if (b->best_kind != 1)
+    return fail(b, SW_ERR_STATE, "no best hit recorded (empty batch, or a device call without ids)");
+  if (best_id) *best_id = b->best_id;
+  if (best_score) *best_score = b->best_score;
+  if (best_index) *best_index = b->best_index;
+  return SW_OK;
 }
 
 // ---- host-buffer batches: a pipelined feeder ----------------------------------------------
@@ -1000,8 +1296,12 @@ size_t chunk_target(size_t total) {
 }
 }  // namespace
 
+static unsigned host_threads_total() { return host_threads(); }
+
 static sw_status feeder_init(sw_bank* b) {
-  if (!b->pool) b->pool.reset(new (std::nothrow) HostPool(host_threads()));
+  HIPOK(b, hipSetDevice(b->device));
+  if (!b->pool) b->pool.reset(new (std::nothrow) HostPool(b->pool_threads ? b->pool_threads
+                                                                          : host_threads()));
   if (!b->pool) return fail(b, SW_ERR_NOMEM, "host worker pool");
   if (b->copy_stream) return SW_OK;
   HIPOK(b, hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
@@ -1020,9 +1320,13 @@ struct Chunk {
 // Runs the feeder: gather(slot, chunk) fills the host slot and returns how many leading bytes
 // of it to copy (0: bad input, message set); they go to the device on the copy stream, score(dslot, chunk, d_scores) launches the
 // kernel on the bank stream; the scores come back to the pinned hscores in input order.
+// to_host: scores back to the pinned hscores (and the batch best hit {id = index, score,
+// index} after them, at best_at(n)) with the stream synchronised; else they stay in b->scores
+// on the device, enqueued on b->stream (a multi-device bank gathers them).
+static inline size_t best_at(size_t n) { return (n * 4 + 7) / 8 * 8; }
 template <class GatherF, class ScoreF>
 static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, GatherF gather,
-                      ScoreF score) {
+                      ScoreF score, bool to_host) {
   sw_status st = feeder_init(b);
   if (st != SW_OK) return st;
   size_t slot_bytes = 0;
@@ -1032,7 +1336,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     HIPOK(b, b->dslot[i].reserve(slot_bytes));
   }
   HIPOK(b, b->scores.reserve(n));
-  HIPOK(b, b->hscores.reserve(n * 4));
+  if (to_host) HIPOK(b, b->hscores.reserve(best_at(n) + 24));
   for (size_t i = 0; i < chunks.size(); ++i) {
     const int s = (int)(i % sw_bank::NSLOT);
     const Chunk& c = chunks[i];
@@ -1056,9 +1360,26 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     }
     HIPOK(b, hipEventRecord(b->kern_done[s], b->stream));
   }
+  if (!to_host) return SW_OK;
+  HIPOK(b, b->best_key.reserve(1));
+  HIPOK(b, b->best_dev.reserve(3));
+  HIPOK(b, swk_best_hit(b->scores.p, nullptr, n, b->best_key.p, b->best_dev.p, b->best_dev.p + 2,
+                        b->stream));
   HIPOK(b, hipMemcpyAsync(b->hscores.p, b->scores.p, n * 4, hipMemcpyDeviceToHost, b->stream));
+  HIPOK(b, hipMemcpyAsync(b->hscores.p + best_at(n), b->best_dev.p, 24, hipMemcpyDeviceToHost,
+                          b->stream));
   HIPOK(b, hipStreamSynchronize(b->stream));
   return SW_OK;
+}
+
+// The host best hit after a to_host feed: index and score from the pinned tail (id = index).
+static void take_best(sw_bank* b, size_t n) {
+  uint64_t h[3];
+  std::memcpy(h, b->hscores.p + best_at(n), sizeof(h));
+  b->best_index = h[2];
+  b->best_id = h[2];
+  b->best_score = (int32_t)(int64_t)h[1];
+  b->best_kind = 1;
 }
 
 static inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -1133,13 +1454,9 @@ static inline uint32_t pack_4bit(const uint8_t* src, uint32_t l, uint8_t* dst) {
   return mx;
 }
 
-extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const uint64_t* offsets,
-                                    const uint32_t* lens, size_t n, int32_t* scores_out) {
-  if (!b) return SW_ERR_ARG;
-  if (n == 0) return SW_OK;
-  if (!offsets || !lens || !scores_out) return fail(b, SW_ERR_ARG, "null host buffer");
-  if (n > 0xFFFFFFFFull)
-    return fail(b, SW_ERR_ARG, "host batches hold < 2^32 targets (sw_score_batch_device does not)");
+// The host-buffer batch through the feeder (n >= 1, buffers checked by the caller).
+static sw_status batch_feed(sw_bank* b, const uint8_t* residues, const uint64_t* offsets,
+                            const uint32_t* lens, size_t n, bool to_host) {
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
   if ((st = feeder_init(b)) != SW_OK) return st;
@@ -1171,7 +1488,6 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const u
   const size_t total = psum[P];
   const uint32_t max_len = *std::max_element(pmax.begin(), pmax.end());
   if (max_len && !residues) return fail(b, SW_ERR_ARG, "null residues");
-  if ((st = range_check(b, max_len)) != SW_OK) return st;
   // slot: offsets u64 | lens | perm | count (SlotTail) | codes at codes_at(cnt): one byte per
   // residue, or, for a DNA chunk without N, the 2-bit stream (a quarter of the PCIe bytes;
   // SWBANK_PACK2=0 disables), each target from a byte boundary, 16 zero bytes after the last
@@ -1339,12 +1655,7 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const u
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.perm_at) : nullptr,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr);
   };
-  if ((st = feed(b, n, chunks, gather, score)) != SW_OK) return st;
-  const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
-  parallel_for(pool, n, [&](size_t lo, size_t hi) {
-    std::memcpy(scores_out + lo, hs + lo, (hi - lo) * 4);
-  });
-  return SW_OK;
+  return feed(b, n, chunks, gather, score, to_host);
 }
 
 // ---- CAPI record path (row f2): sequence_t arrays as the reference host builds them ------
@@ -1370,39 +1681,28 @@ extern "C" sw_status sw_load_query_record(sw_bank* b, const void* record) {
 extern "C" sw_status sw_score_records_device(sw_bank* b, const void* d_records, size_t n,
                                              int32_t* d_scores, void* stream) {
   if (!b) return SW_ERR_ARG;
+  if (b->is_multi())
+    return fail(b, SW_ERR_UNSUPPORTED, "device buffers need a single-device bank");
+  b->best_kind = 0;
   if (n == 0) return SW_OK;
   if (!d_records || !d_scores) return fail(b, SW_ERR_ARG, "null device buffer");
   if (b->alpha != SW_DNA_ALPHA) return fail(b, SW_ERR_UNSUPPORTED, "records carry DNA only");
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
-  // lengths live on the device: bound them by the record capacity
-  if ((st = range_check(b, SWB_RECORD_MAX)) != SW_OK) return st;
+  // lengths live on the device: the kernels clamp them to the record capacity
   HIPOK(b, hipSetDevice(b->device));
   return launch(b, static_cast<const uint8_t*>(d_records), nullptr, nullptr, n, SWB_RECORD_MAX,
                 d_scores, stream ? reinterpret_cast<hipStream_t>(stream) : b->stream,
                 SWK_PACK_RECORDS);
 }
 
-extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
-                                      int32_t* scores_out) {
-  if (!b) return SW_ERR_ARG;
-  if (n == 0) return SW_OK;
-  if (!records || !scores_out) return fail(b, SW_ERR_ARG, "null host buffer");
-  if (b->alpha != SW_DNA_ALPHA) return fail(b, SW_ERR_UNSUPPORTED, "records carry DNA only");
-  if (n > 0xFFFFFFFFull)
-    return fail(b, SW_ERR_ARG, "host batches hold < 2^32 records (sw_score_records_device does not)");
+// Host records through the feeder (n >= 1, buffers checked by the caller); lengths are
+// checked while gathering.
+static sw_status records_feed(sw_bank* b, const uint8_t* recs, size_t n, bool to_host) {
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
   if ((st = feeder_init(b)) != SW_OK) return st;
-  const uint8_t* recs = static_cast<const uint8_t*>(records);
   const auto rlen = [&](size_t k) { return record_len(recs + k * SWB_RECORD); };
-  // lengths are checked while gathering; the range check takes the record capacity unless
-  // that is too long for the 16-bit lanes, then the batch's true maximum
-  if (range_check(b, SWB_RECORD_MAX) != SW_OK) {
-    uint32_t max_len = 0;
-    for (size_t k = 0; k < n; ++k) max_len = std::max(max_len, std::min(rlen(k), SWB_RECORD_MAX));
-    if ((st = range_check(b, max_len)) != SW_OK) return st;
-  }
   // chunks in input order: records | lens | perm | count (longest-first order per chunk)
   const size_t per = std::max<size_t>(1, chunk_target(n * SWB_RECORD) / SWB_RECORD);
   std::vector<Chunk> chunks;
@@ -1461,16 +1761,218 @@ extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.perm_at) : nullptr,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr);
   };
-  if ((st = feed(b, n, chunks, gather, score)) != SW_OK) return st;
+  return feed(b, n, chunks, gather, score, to_host);
+}
+
+// ---- multi-device banks (≙ MODULES ScoringModules behind the PrioEncoder,
+//      ScoreBank_v2.v:76-148; SURVEY §8 e) ---------------------------------------------------
+// A batch is dealt over the child banks (phase 1: every device scores its share, scores stay on
+// the device), then gathered on the first device (phase 2: one ncclGather of equal, padded
+// counts over RCCL/xGMI, or device copies), copied back once and scattered to input order on
+// the host.  The collective is issued only after every share was accepted, so a bad input on
+// one device cannot leave the others blocked inside the gather.
+template <class FeedF>
+static sw_status multi_gather(sw_bank* b, const std::vector<size_t>& cnt, FeedF feed_kid) {
+  const size_t D = b->kids.size();
+  const size_t cmax = *std::max_element(cnt.begin(), cnt.end());
+  for (size_t d = 0; d < D; ++d) {  // padded send buffers, sized before any score lands
+    sw_bank* k = b->kids[d];
+    HIPOK(b, hipSetDevice(k->device));
+    HIPOK(b, k->scores.reserve(std::max<size_t>(cmax, 1)));
+  }
+  std::vector<sw_status> st(D, SW_OK);
+  b->dpool->run([&](unsigned d) {
+    sw_bank* k = b->kids[d];
+    if (hipSetDevice(k->device) != hipSuccess) st[d] = SW_ERR_HIP;
+    else if (cnt[d]) st[d] = feed_kid(d);
+  });
+  for (size_t d = 0; d < D; ++d)
+    if (st[d] != SW_OK) {
+      for (sw_bank* k : b->kids) {
+        (void)hipSetDevice(k->device);
+        (void)hipStreamSynchronize(k->stream);
+      }
+      (void)hipSetDevice(b->device);
+      return fail(b, st[d], "device %d: %s", b->kids[d]->device, b->kids[d]->err);
+    }
+  sw_bank* root = b->kids[0];
+  HIPOK(b, hipSetDevice(root->device));
+  HIPOK(b, b->grecv.reserve(D * cmax));
+  HIPOK(b, b->hrecv.reserve(D * cmax * 4));
+  if (!b->comms.empty()) {
+    const Rccl& r = rccl();
+    std::vector<int> nst(D, 0);
+    b->dpool->run([&](unsigned d) {
+      sw_bank* k = b->kids[d];
+      if (hipSetDevice(k->device) != hipSuccess) { nst[d] = -1; return; }
+      const ncclResult_t e = r.gather(k->scores.p, d == 0 ? b->grecv.p : nullptr, cmax, ncclInt32, 0,
+                                      static_cast<ncclComm_t>(b->comms[d]), k->stream);
+      nst[d] = e != ncclSuccess ? (int)e : hipStreamSynchronize(k->stream) != hipSuccess ? -1 : 0;
+    });
+    for (size_t d = 0; d < D; ++d)
+      if (nst[d] != 0)
+        return fail(b, SW_ERR_HIP, "ncclGather on device %d failed (%s)", b->kids[d]->device,
+                    nst[d] > 0 ? r.errorString((ncclResult_t)nst[d]) : "HIP");
+    HIPOK(b, hipSetDevice(root->device));
+  } else {
+    for (size_t d = 0; d < D; ++d) {
+      sw_bank* k = b->kids[d];
+      if (!cnt[d]) continue;
+      HIPOK(b, hipSetDevice(k->device));
+      HIPOK(b, hipMemcpyPeerAsync(b->grecv.p + d * cmax, root->device, k->scores.p, k->device,
+                                  cnt[d] * 4, k->stream));
+      HIPOK(b, hipStreamSynchronize(k->stream));
+    }
+    HIPOK(b, hipSetDevice(root->device));
+  }
+  HIPOK(b, hipMemcpyAsync(b->hrecv.p, b->grecv.p, D * cmax * 4, hipMemcpyDeviceToHost,
+                          root->stream));
+  HIPOK(b, hipStreamSynchronize(root->stream));
+  copy_kernel_name(b, b->comms.empty() ? "copy" : "rccl");
+  return SW_OK;
+}
+
+// The lowest index with the maximum score over scores[0, n), in parallel on the pool.
+static void host_best(sw_bank* b, const int32_t* scores, size_t n) {
+  const unsigned T = b->pool->size();
+  std::vector<size_t> pi(T, SIZE_MAX);
+  const size_t step = (n + T - 1) / T;
+  b->pool->run([&](unsigned p) {
+    const size_t lo = std::min(n, p * step), hi = std::min(n, lo + step);
+    size_t bi = lo;
+    for (size_t k = lo + 1; k < hi; ++k)
+      if (scores[k] > scores[bi]) bi = k;
+    if (lo < hi) pi[p] = bi;
+  });
+  size_t bi = SIZE_MAX;
+  for (size_t x : pi)
+    if (x != SIZE_MAX && (bi == SIZE_MAX || scores[x] > scores[bi])) bi = x;
+  b->best_index = bi;
+  b->best_id = bi;
+  b->best_score = scores[bi];
+  b->best_kind = 1;
+}
+
+static sw_status multi_batch(sw_bank* b, const uint8_t* residues, const uint64_t* offsets,
+                             const uint32_t* lens, size_t n, int32_t* scores_out) {
+  const size_t D = b->kids.size();
+  // length-balanced deal (SURVEY §8 e): longest first, round robin -> each device gets every
+  // D-th target of the sorted order, itself already longest first (its feeder skips the sort)
+  std::vector<uint32_t> order(n);
+  if (!chunk_perm(*b->pool, lens, n, order.data())) std::iota(order.begin(), order.end(), 0u);
+  std::vector<size_t> cnt(D);
+  for (size_t d = 0; d < D; ++d) cnt[d] = n > d ? (n - d + D - 1) / D : 0;
+  std::vector<std::vector<uint64_t>> offs(D);
+  std::vector<std::vector<uint32_t>> lns(D), idx(D);
+  for (size_t d = 0; d < D; ++d) {
+    offs[d].resize(cnt[d]);
+    lns[d].resize(cnt[d]);
+    idx[d].resize(cnt[d]);
+  }
+  parallel_for(*b->pool, n, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      const uint32_t t = order[k];
+      const size_t d = k % D, i = k / D;
+      idx[d][i] = t;
+      offs[d][i] = offsets[t];
+      lns[d][i] = lens[t];
+    }
+  });
+  sw_status st = multi_gather(b, cnt, [&](unsigned d) {
+    return batch_feed(b->kids[d], residues, offs[d].data(), lns[d].data(), cnt[d], false);
+  });
+  if (st != SW_OK) return st;
+  const size_t cmax = cnt[0];
+  const int32_t* hr = reinterpret_cast<const int32_t*>(b->hrecv.p);
+  parallel_for(*b->pool, n, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      const size_t d = k % D, i = k / D;
+      scores_out[idx[d][i]] = hr[d * cmax + i];
+    }
+  });
+  host_best(b, scores_out, n);
+  return SW_OK;
+}
+
+static sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_t* scores_out) {
+  // records are at most 232 bases: contiguous ranges (no copy of the 64-byte records)
+  const size_t D = b->kids.size();
+  std::vector<size_t> cnt(D), first(D);
+  for (size_t d = 0; d < D; ++d) {
+    first[d] = n * d / D;
+    cnt[d] = n * (d + 1) / D - first[d];
+  }
+  sw_status st = multi_gather(b, cnt, [&](unsigned d) {
+    return records_feed(b->kids[d], recs + first[d] * SWB_RECORD, cnt[d], false);
+  });
+  if (st != SW_OK) return st;
+  const size_t cmax = *std::max_element(cnt.begin(), cnt.end());
+  const int32_t* hr = reinterpret_cast<const int32_t*>(b->hrecv.p);
+  for (size_t d = 0; d < D; ++d)
+    std::memcpy(scores_out + first[d], hr + d * cmax, cnt[d] * 4);
+  host_best(b, scores_out, n);
+  return SW_OK;
+}
+
+extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const uint64_t* offsets,
+                                    const uint32_t* lens, const uint64_t* ids, size_t n,
+                                    int32_t* scores_out) {
+  if (!b) return SW_ERR_ARG;
+  b->best_kind = 0;
+  if (n == 0) return SW_OK;
+  if (!offsets || !lens || !scores_out) return fail(b, SW_ERR_ARG, "null host buffer");
+  if (n > 0xFFFFFFFFull)
+    return fail(b, SW_ERR_ARG, "host batches hold < 2^32 targets (sw_score_batch_device does not)");
+  if (b->is_multi()) {
+    const sw_status st = multi_batch(b, residues, offsets, lens, n, scores_out);
+    if (st == SW_OK && ids) b->best_id = ids[b->best_index];
+    return st;
+  }
+  const sw_status st = batch_feed(b, residues, offsets, lens, n, true);
+  if (st != SW_OK) return st;
   const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
-  parallel_for(pool, n, [&](size_t lo, size_t hi) {
+  parallel_for(*b->pool, n, [&](size_t lo, size_t hi) {
     std::memcpy(scores_out + lo, hs + lo, (hi - lo) * 4);
   });
+  take_best(b, n);
+  if (ids) b->best_id = ids[b->best_index];
   return SW_OK;
+}
+
+extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
+                                      int32_t* scores_out) {
+  if (!b) return SW_ERR_ARG;
+  b->best_kind = 0;
+  if (n == 0) return SW_OK;
+  if (!records || !scores_out) return fail(b, SW_ERR_ARG, "null host buffer");
+  if (b->alpha != SW_DNA_ALPHA) return fail(b, SW_ERR_UNSUPPORTED, "records carry DNA only");
+  if (n > 0xFFFFFFFFull)
+    return fail(b, SW_ERR_ARG, "host batches hold < 2^32 records (sw_score_records_device does not)");
+  const uint8_t* recs = static_cast<const uint8_t*>(records);
+  sw_status st;
+  if (b->is_multi()) {
+    st = multi_records(b, recs, n, scores_out);
+  } else {
+    st = records_feed(b, recs, n, true);
+    if (st == SW_OK) {
+      const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
+      parallel_for(*b->pool, n, [&](size_t lo, size_t hi) {
+        std::memcpy(scores_out + lo, hs + lo, (hi - lo) * 4);
+      });
+      take_best(b, n);
+    }
+  }
+  if (st == SW_OK) {  // the record's own ID (sequence_t.ID, aligner_Header.h:20)
+    uint32_t id;
+    std::memcpy(&id, recs + b->best_index * SWB_RECORD, 4);
+    b->best_id = id;
+  }
+  return st;
 }
 
 extern "C" sw_status sw_bank_set_timing(sw_bank* b, int32_t enable) {
   if (!b) return SW_ERR_ARG;
+  if (b->is_multi()) return each_kid(b, [&](sw_bank* k) { return sw_bank_set_timing(k, enable); });
   b->timing = enable != 0;
   return SW_OK;
 }
@@ -1481,6 +1983,21 @@ extern "C" sw_status sw_bank_timing(sw_bank* b, uint64_t* launches, double* pack
   double p = 0, s = 0;
   uint64_t n = 0;
   sw_status st = SW_OK;
+  if (b->is_multi()) {  // summed over the devices
+    for (sw_bank* k : b->kids) {
+      uint64_t kn = 0;
+      double kp = 0, ks = 0;
+      if ((st = sw_bank_timing(k, &kn, &kp, &ks)) != SW_OK)
+        return fail(b, st, "device %d: %s", k->device, k->err);
+      n += kn;
+      p += kp;
+      s += ks;
+    }
+    if (launches) *launches = n;
+    if (pack_ms) *pack_ms = p;
+    if (score_ms) *score_ms = s;
+    return SW_OK;
+  }
   for (auto& ev : b->events) {
     float t1 = 0, t2 = 0;
     if (st == SW_OK && hipEventSynchronize(ev.c) == hipSuccess &&
@@ -1506,11 +2023,13 @@ extern "C" sw_status sw_bank_timing(sw_bank* b, uint64_t* launches, double* pack
 extern "C" sw_status sw_best_hit_device(sw_bank* b, const int32_t* d_scores, const uint64_t* d_ids,
                                         size_t n, uint64_t* d_out, void* stream) {
   if (!b) return SW_ERR_ARG;
+  if (b->is_multi())
+    return fail(b, SW_ERR_UNSUPPORTED, "device buffers need a single-device bank");
   if (!d_scores || !d_out || n == 0 || n > 0xFFFFFFFFull)
     return fail(b, SW_ERR_ARG, "sw_best_hit_device: empty, null or > 2^32 scores");
   HIPOK(b, hipSetDevice(b->device));
   HIPOK(b, b->best_key.reserve(1));
-  HIPOK(b, swk_best_hit(d_scores, d_ids, n, b->best_key.p, d_out,
+  HIPOK(b, swk_best_hit(d_scores, d_ids, n, b->best_key.p, d_out, nullptr,
                         stream ? reinterpret_cast<hipStream_t>(stream) : b->stream));
   return SW_OK;
 }

@@ -19,7 +19,7 @@ const char *sw_status_string(sw_status s) {
     case SW_ERR_ARG: return "invalid argument";
     case SW_ERR_NO_DEVICE: return "no usable gfx950 HIP device";
     case SW_ERR_HIP: return "HIP runtime error";
-    case SW_ERR_RANGE: return "score range exceeds the 16-bit lanes";
+    case SW_ERR_RANGE: return "substitution or gap range outside the kernels";
     case SW_ERR_STATE: return "penalties or query not loaded";
     case SW_ERR_NOMEM: return "out of memory";
     case SW_ERR_IO: return "I/O or parse error";

@@ -4,7 +4,7 @@
 
 /* Longest query a bank accepts; past 512 rows it runs as segments of SWBANK_SEG rows whose
  * bottom rows are handed on through HBM. */
-#define SWB_MAX_QUERY 8192u
+#define SWB_MAX_QUERY 65536u
 /* Targets per workgroup tile: 64 lanes x 2 packed u16 halves (the PE "toggle" pair). */
 #define SWB_TILE 128
 /* Selector byte that reads 0xFF from v_perm_b32 (padding: substitution = S - 255 < 0). */

@@ -381,14 +381,29 @@ __device__ __forceinline__ uint2 pad_tail(uint2 w, uint32_t j0, uint32_t len, ui
   return make_uint2((uint32_t)(v | p), (uint32_t)((v | p) >> 32));
 }
 
+// Loads at arbitrary byte offsets (target starts in the packed streams and records are not
+// aligned): memcpy tells the compiler the alignment is 1; gfx950 global loads accept any
+// alignment, so they stay single dword / dwordx2 loads.
+template <class T>
+__device__ __forceinline__ T load_u(const uint8_t* p) {
+  T v;
+  __builtin_memcpy(&v, p, sizeof(T));
+  return v;
+}
+// CAPI record length, clamped to the record capacity (a corrupt length cannot send a lane past
+// the 58-byte data field)
+__device__ __forceinline__ uint32_t record_len(const uint8_t* rec) {
+  return min((uint32_t)load_u<uint16_t>(rec + 4), SWB_RECORD_MAX);
+}
+
 __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint32_t pad,
                                          uint32_t packed, uint2& lo, uint2& hi) {
   const uint32_t j0 = (uint32_t)c * 8;
   if (packed == SWK_PACK_NIBBLE) {  // 4-bit stream, 4 bytes per 8 codes, clamped like below
     const uint32_t cl = min((uint32_t)c, max((t.llo + 7) / 8, 1u) - 1);
     const uint32_t ch = min((uint32_t)c, max((t.lhi + 7) / 8, 1u) - 1);
-    lo = unpack8n(*reinterpret_cast<const uint32_t*>(t.plo + 4 * cl));
-    hi = unpack8n(*reinterpret_cast<const uint32_t*>(t.phi + 4 * ch));
+    lo = unpack8n(load_u<uint32_t>(t.plo + 4 * cl));
+    hi = unpack8n(load_u<uint32_t>(t.phi + 4 * ch));
     if (!full) {
       lo = pad_tail(lo, j0, t.llo, pad);
       hi = pad_tail(hi, j0, t.lhi, pad);
@@ -402,8 +417,8 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint3
       cl = min(cl, max((t.llo + 7) / 8, 1u) - 1);
       ch = min(ch, max((t.lhi + 7) / 8, 1u) - 1);
     }
-    const uint32_t x = *reinterpret_cast<const uint16_t*>(t.plo + 2 * cl);
-    const uint32_t y = *reinterpret_cast<const uint16_t*>(t.phi + 2 * ch);
+    const uint32_t x = load_u<uint16_t>(t.plo + 2 * cl);
+    const uint32_t y = load_u<uint16_t>(t.phi + 2 * ch);
     lo = unpack8(x);
     hi = unpack8(y);
     if (!full) {
@@ -411,8 +426,8 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint3
       hi = pad_tail(hi, j0, t.lhi, pad);
     }
   } else if (full) {
-    lo = *reinterpret_cast<const uint2*>(t.plo + j0);
-    hi = *reinterpret_cast<const uint2*>(t.phi + j0);
+    lo = load_u<uint2>(t.plo + j0);
+    hi = load_u<uint2>(t.phi + j0);
   } else {
     uint32_t b[2][8];
 #pragma unroll
@@ -458,8 +473,8 @@ __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t
     b = idx[b];
   }
   if (packed == SWK_PACK_RECORDS) {
-    t.llo = va ? *reinterpret_cast<const uint16_t*>(res + a * SWB_RECORD + 4) : 0u;
-    t.lhi = vb ? *reinterpret_cast<const uint16_t*>(res + b * SWB_RECORD + 4) : 0u;
+    t.llo = va ? record_len(res + a * SWB_RECORD) : 0u;
+    t.lhi = vb ? record_len(res + b * SWB_RECORD) : 0u;
     t.plo = res + a * SWB_RECORD + 6;
     t.phi = res + b * SWB_RECORD + 6;
     return t;
@@ -539,8 +554,7 @@ __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens
   auto len = [&](size_t k) -> uint32_t {
     if (k >= n) return 0u;
     if (idx) k = idx[k];
-    return packed == SWK_PACK_RECORDS ? *reinterpret_cast<const uint16_t*>(res + k * SWB_RECORD + 4)
-                                      : lens[k];
+    return packed == SWK_PACK_RECORDS ? record_len(res + k * SWB_RECORD) : lens[k];
   };
   uint32_t L = max(len(a), len(b));
 #pragma unroll
@@ -1143,11 +1157,8 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
   if (tA >= n) return;  // whole wave
   const bool packed = a.packed != SWK_PACK_BYTES, rec = a.packed == SWK_PACK_RECORDS;
   const bool nib = a.packed == SWK_PACK_NIBBLE;
-  const uint32_t LA = rec ? *reinterpret_cast<const uint16_t*>(a.res + tA * SWB_RECORD + 4)
-                          : a.lens[tA];
-  const uint32_t LB = tB >= n ? 0u
-                      : rec ? *reinterpret_cast<const uint16_t*>(a.res + tB * SWB_RECORD + 4)
-                            : a.lens[tB];
+  const uint32_t LA = rec ? record_len(a.res + tA * SWB_RECORD) : a.lens[tA];
+  const uint32_t LB = tB >= n ? 0u : rec ? record_len(a.res + tB * SWB_RECORD) : a.lens[tB];
   const uint8_t* pA = rec ? a.res + tA * SWB_RECORD + 6 : a.res + (LA ? a.offs[tA] : 0);
   const uint8_t* pB = rec ? a.res + (tB < n ? tB : tA) * SWB_RECORD + 6
                           : a.res + (LB ? a.offs[tB] : 0);
@@ -1461,23 +1472,27 @@ __global__ void __launch_bounds__(256) best_kernel(const int32_t* scores, size_t
   }
   if (threadIdx.x == 0) atomicMax(key, red[0]);
 }
-__global__ void best_finalize(const unsigned long long* key, const uint64_t* ids, uint64_t* out) {
+__global__ void best_finalize(const unsigned long long* key, const uint64_t* ids, uint64_t* out,
+                              uint64_t* out_index) {
   const unsigned long long v = *key;
   const uint64_t idx = 0xFFFFFFFFull - (v & 0xFFFFFFFFull);
   out[0] = ids ? ids[idx] : idx;
   out[1] = (uint64_t)(int64_t)(int32_t)((uint32_t)(v >> 32) ^ 0x80000000u);
+  if (out_index) *out_index = idx;
 }
 }  // namespace swk
 
-// out[0] = best id, out[1] = best score (sign-extended); key: 8 bytes of device scratch.
+// out[0] = best id, out[1] = best score (sign-extended), *out_index (optional) = its index;
+// key: 8 bytes of device scratch.
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
-                                   unsigned long long* key, uint64_t* out, hipStream_t st) {
+                                   unsigned long long* key, uint64_t* out, uint64_t* out_index,
+                                   hipStream_t st) {
   hipError_t e = hipMemsetAsync(key, 0, sizeof(*key), st);
   if (e != hipSuccess) return e;
   const size_t blocks = std::min<size_t>((n + 255) / 256, 2048);
   hipLaunchKernelGGL(swk::best_kernel, dim3((unsigned)std::max<size_t>(blocks, 1)), dim3(256), 0,
                      st, scores, n, key);
-  hipLaunchKernelGGL(swk::best_finalize, dim3(1), dim3(1), 0, st, key, ids, out);
+  hipLaunchKernelGGL(swk::best_finalize, dim3(1), dim3(1), 0, st, key, ids, out, out_index);
   return hipGetLastError();
 }
 
@@ -1517,4 +1532,287 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
   SWK_WAVE_VARIANTS(SWK_WCASE)
 #undef SWK_WCASE
   return hipErrorInvalidValue;
+}
+
+// ========================================================================================
+// int32 kernel: exact scores past the 16-bit lanes (no bound on the score).  The u16 and f16
+// passes are exact for every pair whose computed score stays <= 65535 - max(s) (resp. 2048 -
+// max(s)): the first cell that would leave the lane range has an exact diagonal M above that
+// threshold (a gap value is at most an earlier, exact H minus a penalty), and the running max
+// keeps it.  So a batch past the 16-bit bound is scored by the 16-bit kernels as usual and the
+// pairs above 65535 - max(s) are re-scored here (an index list, like the f16 -> u16 re-score).
+//
+// One wave per pair; strips of 256 query rows, lane l owns rows [4l, 4l+4) of a strip (the
+// wave kernel's anti-diagonal walk: step t, lane l computes column t - l).  The strip's bottom
+// row {H, T|F} goes to the next strip through a per-wave HBM scratch row (ping-pong, 64
+// columns per coalesced load / store, readlane + a lane select per step).  Substitution scores come
+// from a per-strip profile: for every letter, lane l's 4 rows as int16 (uint2), staged in the
+// wave's own LDS slice (each lane reads only its own entries: no barrier).  Merged gaps apply
+// the HDL's first-column rule always (it changes nothing unless max(s) > o + e), in the
+// clamped form of the f16 kernels:
+//   M = max(0, Hdiag + s)   I = j ? max(Tup, Tleft) : 0   H = max(M, I)   T = max(0, M-o-e, I-e)
+// Gotoh (E, F one step ahead, floored at 0):
+//   H = max(0, Hdiag + s, E, F)   HN = H - o - e   E' = max(0, HN, E - e)   F' = max(0, HN, F - e)
+namespace swk {
+constexpr int I32_K = 4, I32_LETTERS = 25;  // rows per lane; profile letters incl. padding
+
+struct I32Args {
+  const uint8_t* res;
+  const uint64_t* offs;
+  const uint32_t* lens;
+  size_t n;
+  uint32_t packed;
+  const uint32_t* idx;   // optional: positions [0, min(n, *nidx - idx_base)) score idx[k]
+  const uint32_t* nidx;
+  uint32_t idx_base;
+  const uint2* prof;     // [strip][letter 0..pad][lane] 4 x int16 (rows 4l..4l+3)
+  uint32_t nstrips, qlen, pad, O, E;
+  int32_t* scores;
+  uint2* scratch;        // per wave: 2 x scols uint2
+  uint32_t scols;
+};
+
+__device__ __forceinline__ uint32_t i32_code(const uint8_t* p, uint32_t c, uint32_t packed) {
+  if (packed == SWK_PACK_BYTES) return p[c];
+  if (packed == SWK_PACK_NIBBLE) return (p[c >> 1] >> (4 * (c & 1))) & 15u;
+  return (p[c >> 2] >> (2 * (c & 3))) & 3u;  // records, 2-bit stream
+}
+
+__device__ __forceinline__ int32_t i32_lane0(int32_t inj, int32_t v) {  // wave_shr:1
+  return __builtin_amdgcn_update_dpp(inj, v, 0x138, 0xF, 0xF, false);
+}
+
+template <bool GOTOH>
+__global__ void __launch_bounds__(256) score_i32(const I32Args a) {
+  __shared__ uint2 lp[4][I32_LETTERS][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t gw = (size_t)blockIdx.x * 4 + wave, GW = (size_t)gridDim.x * 4;
+  size_t n = a.n;
+  if (a.idx) {
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(*a.nidx);
+    n = cnt > a.idx_base ? min(a.n, (size_t)(cnt - a.idx_base)) : 0;
+  }
+  uint2* const scr[2] = {a.scratch + gw * 2 * a.scols, a.scratch + gw * 2 * a.scols + a.scols};
+  const int32_t oe = (int32_t)(a.O + a.E), e = (int32_t)a.E;
+  const uint32_t pad = a.pad;
+  uint2 (&mine)[I32_LETTERS][64] = lp[wave];
+  for (size_t p = gw; p < n; p += GW) {
+    const size_t t = a.idx ? a.idx[p] : p;
+    const uint8_t* tp;
+    uint32_t L;
+    if (a.packed == SWK_PACK_RECORDS) {
+      tp = a.res + t * SWB_RECORD + 6;
+      L = record_len(a.res + t * SWB_RECORD);
+    } else {
+      L = a.lens[t];
+      tp = a.res + (L ? a.offs[t] : 0);
+    }
+    L = __builtin_amdgcn_readfirstlane(L);
+    int32_t best = 0;
+    for (uint32_t s = 0; s < a.nstrips && L; ++s) {
+      for (uint32_t c = 0; c <= pad; ++c) mine[c][lane] = a.prof[((size_t)s * (pad + 1) + c) * 64 + lane];
+      int32_t vmask[I32_K];
+#pragma unroll
+      for (int k = 0; k < I32_K; ++k)
+        vmask[k] = s * 256u + (uint32_t)lane * I32_K + k < a.qlen ? -1 : 0;
+      const bool seg_in = s > 0, seg_out = s + 1 < a.nstrips;
+      const uint2* ein = scr[(s + 1) & 1];
+      uint2* eout = scr[s & 1];
+      int32_t H[I32_K], X[I32_K];
+#pragma unroll
+      for (int k = 0; k < I32_K; ++k) H[k] = X[k] = 0;
+      int32_t botH = 0, botX = 0, prevUpH = 0;
+      uint32_t code = pad, buf = pad;
+      uint2 ebuf = make_uint2(0u, 0u), obuf = make_uint2(0u, 0u);
+      const uint32_t nsteps = L + 63;
+      for (uint32_t st = 0; st < nsteps; ++st) {
+        if ((st & 63) == 0) {  // the next 64 columns: codes (and the previous strip's row)
+          const uint32_t c = st + lane;
+          buf = c < L ? min(i32_code(tp, c, a.packed), pad) : pad;
+          if (seg_in) ebuf = c < L ? ein[c] : make_uint2(0u, 0u);
+        }
+        const uint32_t j = st - (uint32_t)lane;  // this lane's column (wraps when not started)
+        code = (uint32_t)i32_lane0((int32_t)__builtin_amdgcn_readlane(buf, st & 63), (int32_t)code);
+        const int32_t upH = i32_lane0(seg_in ? (int32_t)__builtin_amdgcn_readlane(ebuf.x, st & 63) : 0, botH);
+        const int32_t upX = i32_lane0(seg_in ? (int32_t)__builtin_amdgcn_readlane(ebuf.y, st & 63) : 0, botX);
+        const uint2 w = mine[code][lane];
+        const int32_t sc[I32_K] = {(int32_t)(w.x << 16) >> 16, (int32_t)w.x >> 16,
+                                   (int32_t)(w.y << 16) >> 16, (int32_t)w.y >> 16};
+        if (j < L) {  // active: column j of the lane's 4 rows
+          int32_t diag = prevUpH, up = upH, ux = upX;
+#pragma unroll
+          for (int k = 0; k < I32_K; ++k) {
+            const int32_t D = diag + sc[k];
+            diag = H[k];
+            if constexpr (GOTOH) {
+              const int32_t h = max(max(D, 0), max(X[k], ux));
+              const int32_t hn = h - oe;
+              X[k] = max(max(hn, 0), X[k] - e);  // E of (row, j+1)
+              ux = max(max(hn, 0), ux - e);      // F of (row+1, j)
+              H[k] = h;
+              best = max(best, h & vmask[k]);
+            } else {
+              const int32_t M = max(D, 0);
+              const int32_t I = j == 0 ? 0 : max(ux, X[k]);
+              const int32_t h = max(M, I);
+              ux = max(max(M - oe, I - e), 0);   // T: what the right and lower cells read
+              X[k] = ux;
+              H[k] = h;
+              best = max(best, h & vmask[k]);
+            }
+            (void)up;
+          }
+          botH = H[I32_K - 1];
+          botX = ux;
+        }
+        prevUpH = upH;
+        if (seg_out) {  // lane 63's bottom row of column st - 63 -> eout
+          const uint32_t c = st - 63;
+          if (st >= 63) {
+            const int32_t vh = __builtin_amdgcn_readlane(botH, 63);
+            const int32_t vx = __builtin_amdgcn_readlane(botX, 63);
+            const bool here = (uint32_t)lane == (c & 63);
+            obuf.x = here ? (uint32_t)vh : obuf.x;
+            obuf.y = here ? (uint32_t)vx : obuf.y;
+            if ((c & 63) == 63 || c + 1 == L) {
+              const uint32_t col = (c & ~63u) + lane;
+              if (col < L) eout[col] = obuf;
+            }
+          }
+        }
+      }
+      if (seg_out) __atomic_thread_fence(__ATOMIC_SEQ_CST);  // stores visible to the next strip
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
+    if (lane == 0) a.scores[t] = best;
+  }
+}
+}  // namespace swk
+
+// Waves to launch for n pairs of at most scols columns: one pair per wave at a time, up to
+// 16 waves per CU, within the scratch budget (2 x scols x 8 B per wave).
+extern "C" size_t swk_i32_waves(size_t n, uint32_t scols, size_t budget_bytes) {
+  const size_t per = (size_t)std::max(scols, 1u) * 2 * sizeof(uint2);
+  size_t w = std::min<size_t>(n, 256 * 16);
+  w = std::min(w, std::max<size_t>(4, budget_bytes / per));
+  return (w + 3) / 4 * 4;
+}
+
+extern "C" hipError_t swk_launch_i32(int gotoh, const uint8_t* res, const uint64_t* offs,
+                                     const uint32_t* lens, size_t n, int packed,
+                                     const uint32_t* idx, const uint32_t* nidx, uint32_t idx_base,
+                                     const void* prof, uint32_t nstrips, uint32_t qlen,
+                                     uint32_t pad, uint32_t O, uint32_t E, int32_t* scores,
+                                     void* scratch, uint32_t scols, size_t waves, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (pad + 1 > (uint32_t)swk::I32_LETTERS || waves == 0 || waves % 4) return hipErrorInvalidValue;
+  const swk::I32Args a{res, offs, lens, n, (uint32_t)packed, idx, nidx, idx_base,
+                       static_cast<const uint2*>(prof), nstrips, qlen, pad, O, E, scores,
+                       static_cast<uint2*>(scratch), scols};
+  if (gotoh)
+    hipLaunchKernelGGL(swk::score_i32<true>, dim3((unsigned)(waves / 4)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(swk::score_i32<false>, dim3((unsigned)(waves / 4)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ========================================================================================
+// Longest-first visiting order of a device batch (sw_score_batch_device with ragged lengths):
+// the PrioEncoder's feed order (ScoreBank_v2.v:142-148) so that each 128-target tile holds
+// similar lengths.  A counting sort over length bins (bin = (max_len - len) >> shift, at most
+// 2048 bins; targets within a bin differ by < 2^shift codes, and the order inside a bin is
+// free: scores are written at input positions).  hist: global bin counts; scan: exclusive
+// offsets in place + perm_n = n; scatter: per block, LDS bin counts, one global atomic per
+// non-empty bin reserves the block's range, LDS atomics place the elements.
+namespace swk {
+constexpr int SORT_BINS = 2048, SORT_BLOCK = 1024, SORT_ITEMS = 8;
+
+__device__ __forceinline__ uint32_t sort_bin(uint32_t len, uint32_t max_len, uint32_t shift) {
+  return (max_len - min(len, max_len)) >> shift;
+}
+
+__global__ void __launch_bounds__(SORT_BLOCK) sort_hist(const uint32_t* lens, size_t n,
+                                                        uint32_t max_len, uint32_t shift,
+                                                        uint32_t nb, uint32_t* hist) {
+  __shared__ uint32_t h[SORT_BINS];
+  for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK) h[i] = 0;
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * SORT_BLOCK * SORT_ITEMS;
+#pragma unroll
+  for (int it = 0; it < SORT_ITEMS; ++it) {
+    const size_t k = base + (size_t)it * SORT_BLOCK + threadIdx.x;
+    if (k < n) atomicAdd(&h[sort_bin(lens[k], max_len, shift)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+__global__ void __launch_bounds__(SORT_BLOCK) sort_scan(uint32_t* hist, uint32_t nb, size_t n,
+                                                        uint32_t* perm_n) {
+  __shared__ uint32_t part[SORT_BLOCK];
+  // each thread owns 2 consecutive bins (nb <= 2048)
+  const uint32_t i0 = threadIdx.x * 2;
+  const uint32_t a = i0 < nb ? hist[i0] : 0u, c = i0 + 1 < nb ? hist[i0 + 1] : 0u;
+  part[threadIdx.x] = a + c;
+  __syncthreads();
+  for (uint32_t off = 1; off < SORT_BLOCK; off <<= 1) {  // inclusive Hillis-Steele scan
+    const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const uint32_t ex = part[threadIdx.x] - (a + c);
+  if (i0 < nb) hist[i0] = ex;
+  if (i0 + 1 < nb) hist[i0 + 1] = ex + a;
+  if (threadIdx.x == 0) *perm_n = (uint32_t)n;
+}
+
+__global__ void __launch_bounds__(SORT_BLOCK) sort_scatter(const uint32_t* lens, size_t n,
+                                                           uint32_t max_len, uint32_t shift,
+                                                           uint32_t nb, uint32_t* offs,
+                                                           uint32_t* perm) {
+  __shared__ uint32_t h[SORT_BINS];
+  for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK) h[i] = 0;
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * SORT_BLOCK * SORT_ITEMS;
+  uint32_t bin[SORT_ITEMS];
+#pragma unroll
+  for (int it = 0; it < SORT_ITEMS; ++it) {
+    const size_t k = base + (size_t)it * SORT_BLOCK + threadIdx.x;
+    bin[it] = k < n ? sort_bin(lens[k], max_len, shift) : 0u;
+    if (k < n) atomicAdd(&h[bin[it]], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK)  // reserve this block's ranges
+    if (h[i]) h[i] = atomicAdd(&offs[i], h[i]);
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < SORT_ITEMS; ++it) {
+    const size_t k = base + (size_t)it * SORT_BLOCK + threadIdx.x;
+    if (k < n) perm[atomicAdd(&h[bin[it]], 1u)] = (uint32_t)k;
+  }
+}
+}  // namespace swk
+
+// perm[0, n) <- target numbers longest first, *perm_n <- n; scratch: SORT_BINS words.
+extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max_len,
+                                    uint32_t* perm, uint32_t* perm_n, uint32_t* scratch,
+                                    hipStream_t st) {
+  if (n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  uint32_t shift = 0;
+  while ((max_len >> shift) >= (uint32_t)swk::SORT_BINS) ++shift;
+  const uint32_t nb = (max_len >> shift) + 1;
+  hipError_t e = hipMemsetAsync(scratch, 0, nb * sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  const unsigned blocks =
+      (unsigned)((n + swk::SORT_BLOCK * swk::SORT_ITEMS - 1) / (swk::SORT_BLOCK * swk::SORT_ITEMS));
+  hipLaunchKernelGGL(swk::sort_hist, dim3(blocks), dim3(swk::SORT_BLOCK), 0, st, lens, n, max_len,
+                     shift, nb, scratch);
+  hipLaunchKernelGGL(swk::sort_scan, dim3(1), dim3(swk::SORT_BLOCK), 0, st, scratch, nb, n, perm_n);
+  hipLaunchKernelGGL(swk::sort_scatter, dim3(blocks), dim3(swk::SORT_BLOCK), 0, st, lens, n,
+                     max_len, shift, nb, scratch, perm);
+  return hipGetLastError();
 }

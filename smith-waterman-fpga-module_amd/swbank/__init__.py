@@ -40,8 +40,10 @@ EXPORTS = (
     "sw_score_batch_device", "sw_best_hit", "sw_encode_ascii", "sw_pack_2bit",
     "sw_unpack_2bit", "sw_fill_matrix", "sw_bank_set_timing", "sw_bank_timing",
     "sw_last_kernel", "sw_load_query_record", "sw_score_records", "sw_score_records_device",
-    "sw_best_hit_device",
+    "sw_best_hit_device", "sw_batch_best", "sw_bank_devices",
 )
+ABI_VERSION = 2
+MAX_DEVICES = 16
 RECORD_BYTES, RECORD_MAX_BASES = 64, 232
 
 
@@ -54,7 +56,8 @@ class SwbankError(RuntimeError):
 class _Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("alphabet", ctypes.c_int32),
                 ("gap_model", ctypes.c_int32), ("max_query_len", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("n_devices", ctypes.c_int32),
+                ("devices", ctypes.c_int32 * 16)]
 
 
 _LIB: Optional[ctypes.CDLL] = None
@@ -77,6 +80,8 @@ def lib() -> ctypes.CDLL:
         except ImportError:
             pass
     L = ctypes.CDLL(LIB_PATH)
+    if L.sw_abi_version() != ABI_VERSION:
+        raise SwbankError(ERR_UNSUPPORTED, f"{LIB_PATH}: ABI {L.sw_abi_version()}, want {ABI_VERSION}")
     P, i32, u32, u64, sz = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64,
                             ctypes.c_size_t)
     sig = {
@@ -91,8 +96,10 @@ def lib() -> ctypes.CDLL:
         "sw_set_penalties": (i32, [P, i32, i32, i32, i32]),
         "sw_set_matrix": (i32, [P, P, i32, i32, i32]),
         "sw_load_query": (i32, [P, u64, P, u32]),
-        "sw_score_batch": (i32, [P, P, P, P, sz, P]),
-        "sw_score_batch_device": (i32, [P, P, P, P, sz, u32, P, P]),
+        "sw_score_batch": (i32, [P, P, P, P, P, sz, P]),
+        "sw_score_batch_device": (i32, [P, P, P, P, P, sz, u32, P, P]),
+        "sw_batch_best": (i32, [P, P, P, P]),
+        "sw_bank_devices": (i32, [P, P, i32]),
         "sw_best_hit": (i32, [P, P, P, sz, P, P]),
         "sw_encode_ascii": (sz, [i32, ctypes.c_char_p, sz, P]),
         "sw_pack_2bit": (sz, [ctypes.c_char_p, sz, P]),
@@ -200,17 +207,50 @@ def pack_targets(seqs: Sequence[np.ndarray]) -> Tuple[np.ndarray, np.ndarray, np
     return res, offs, lens
 
 
+def validate_batch(residues, offsets, lens, ids=None):
+    """Host batch -> contiguous (residues u8, offsets u64, lens u32, ids u64 | None), or
+    ValueError when the arrays disagree: the C feeder reads residues[offsets[k] :
+    offsets[k] + lens[k]] for every k < len(lens), so a short or out-of-range array would be a
+    host over-read inside the library rather than a Python error."""
+    res = np.ascontiguousarray(residues, dtype=np.uint8).reshape(-1)
+    ln = np.ascontiguousarray(lens, dtype=np.uint32).reshape(-1)
+    off_in = np.asarray(offsets).reshape(-1)
+    if off_in.size != ln.size:
+        raise ValueError(f"{off_in.size} offsets for {ln.size} lengths")
+    if off_in.size and np.issubdtype(off_in.dtype, np.signedinteger) and off_in.min() < 0:
+        raise ValueError("negative offset")
+    offs = np.ascontiguousarray(off_in, dtype=np.uint64)
+    if ln.size and int((offs + ln.astype(np.uint64)).max()) > res.size:
+        raise ValueError("a target runs past the end of residues")
+    idv = None
+    if ids is not None:
+        idv = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1)
+        if idv.size != ln.size:
+            raise ValueError(f"{idv.size} ids for {ln.size} targets")
+    return res, offs, ln, idv
+
+
 # ---- the bank ----------------------------------------------------------------------------
 class ScoreBank:
-    """One ScoreBank_v2 instance on one GPU (sw_bank_create)."""
+    """One ScoreBank_v2 instance (sw_bank_create): on one GPU, or with ``devices=[...]`` a
+    multi-device bank that deals every host batch over those GPUs (the RTL's MODULES,
+    ScoreBank_v2.v:76-148) and gathers the scores back with RCCL."""
 
     def __init__(self, device: int = -1, alphabet: int = ALPHABET_DNA,
-                 gap_model: int = GAP_MERGED, max_query_len: int = 0):
+                 gap_model: int = GAP_MERGED, max_query_len: int = 0,
+                 devices: Optional[Sequence[int]] = None):
         L = lib()
         cfg = _Config()
         L.sw_config_default(ctypes.byref(cfg))
         cfg.device, cfg.alphabet, cfg.gap_model, cfg.max_query_len = (
             device, alphabet, gap_model, max_query_len)
+        if devices is not None:
+            devices = list(devices)
+            if not 1 <= len(devices) <= MAX_DEVICES:
+                raise ValueError(f"devices: 1..{MAX_DEVICES} ordinals")
+            cfg.n_devices = len(devices)
+            for i, d in enumerate(devices):
+                cfg.devices[i] = d
         h = ctypes.c_void_p()
         st = L.sw_bank_create(ctypes.byref(h), ctypes.byref(cfg))
         if st != OK:
@@ -256,24 +296,40 @@ class ScoreBank:
         self._check(lib().sw_load_query(self._h, qid, _p(buf), len(c)))
 
     # target stream
-    def score_batch(self, residues: np.ndarray, offsets: np.ndarray, lens: np.ndarray) -> np.ndarray:
-        res = np.ascontiguousarray(residues, dtype=np.uint8)
-        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
-        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+    def score_batch(self, residues: np.ndarray, offsets: np.ndarray, lens: np.ndarray,
+                    ids: Optional[np.ndarray] = None) -> np.ndarray:
+        """Scores of targets residues[offsets[k] : offsets[k] + lens[k]] in input order; ids
+        (optional, one per target) tag the batch best hit (best())."""
+        res, offs, ln, idv = validate_batch(residues, offsets, lens, ids)
         out = np.empty(len(ln), dtype=np.int32)  # every entry written by the library
         if len(ln) == 0:
             return out
-        self._check(lib().sw_score_batch(self._h, _p(res), _p(offs), _p(ln), len(ln), _p(out)))
+        self._check(lib().sw_score_batch(self._h, _p(res), _p(offs), _p(ln),
+                                         _p(idv) if idv is not None else None, len(ln), _p(out)))
         return out
+
+    def best(self) -> Tuple[int, int, int]:
+        """Best hit of the last batch call (sw_batch_best, ≙ max / vld_max):
+        (id, score, index) — lowest index among equal maxima."""
+        bid, bsc, bix = ctypes.c_uint64(), ctypes.c_int32(), ctypes.c_uint64()
+        self._check(lib().sw_batch_best(self._h, ctypes.byref(bid), ctypes.byref(bsc),
+                                        ctypes.byref(bix)))
+        return int(bid.value), int(bsc.value), int(bix.value)
+
+    def devices(self) -> list:
+        arr = (ctypes.c_int32 * MAX_DEVICES)()
+        n = lib().sw_bank_devices(self._h, arr, MAX_DEVICES)
+        return [int(arr[i]) for i in range(n)]
 
     def score_targets(self, seqs: Iterable[np.ndarray]) -> np.ndarray:
         return self.score_batch(*pack_targets(list(seqs)))
 
     def score_batch_device(self, d_res: int, d_offs: int, d_lens: int, n: int, max_len: int,
-                           d_scores: int, stream: int = 0):
-        """Device pointers (ints, e.g. torch.Tensor.data_ptr()); async on `stream`."""
-        self._check(lib().sw_score_batch_device(self._h, d_res, d_offs, d_lens, n, max_len,
-                                                d_scores, stream or None))
+                           d_scores: int, stream: int = 0, d_ids: int = 0):
+        """Device pointers (ints, e.g. torch.Tensor.data_ptr()); async on `stream`.  With d_ids
+        the call also records the batch best hit on the device (best())."""
+        self._check(lib().sw_score_batch_device(self._h, d_res, d_offs, d_lens, d_ids or None,
+                                                n, max_len, d_scores, stream or None))
 
     # CAPI record path (sequence_t arrays, 2-bit codes)
     def load_query_record(self, record: np.ndarray):

@@ -93,7 +93,7 @@ static int score(const char *qpath, const char *lpath) {
   uint64_t off0 = 0;
   uint32_t len0 = 1;
   uint8_t c0 = 0;
-  CHECK(sw_score_batch(bank, &c0, &off0, &len0, 1, &dummy) == SW_ERR_STATE, "state error");
+  CHECK(sw_score_batch(bank, &c0, &off0, &len0, NULL, 1, &dummy) == SW_ERR_STATE, "state error");
   CHECK(strlen(sw_last_error(bank)) > 0, "error text");
 
   CHECK(sw_set_penalties(bank, 5, -4, -12, -4) == SW_OK, "penalties");
@@ -108,6 +108,8 @@ static int score(const char *qpath, const char *lpath) {
   uint64_t *offs = malloc(n * sizeof *offs);
   uint32_t *lens = malloc(n * sizeof *lens);
   int32_t *s1 = malloc(n * sizeof *s1), *s2 = malloc(n * sizeof *s2);
+  uint64_t *ids = malloc(n * sizeof *ids);
+  for (int k = 0; k < n; ++k) ids[k] = 1000000007ull * (uint64_t)(k + 1);  /* 48-bit-style tags */
   size_t pos = 0;
   for (int k = 0; k < n; ++k) {
     const size_t l = strlen(ls[k]);
@@ -116,8 +118,15 @@ static int score(const char *qpath, const char *lpath) {
     lens[k] = (uint32_t)l;
     pos += l;
   }
-  CHECK(sw_score_batch(bank, res, offs, lens, (size_t)n, s1) == SW_OK, sw_last_error(bank));
+  CHECK(sw_score_batch(bank, res, offs, lens, ids, (size_t)n, s1) == SW_OK, sw_last_error(bank));
   printf("kernel %s\n", sw_last_kernel(bank));
+  /* the batch best hit (≙ max / vld_max) carries the caller's id */
+  uint64_t bb_id = 0, bb_ix = 0;
+  int32_t bb_sc = 0;
+  CHECK(sw_batch_best(bank, &bb_id, &bb_sc, &bb_ix) == SW_OK, sw_last_error(bank));
+  CHECK(bb_ix < (uint64_t)n && bb_id == ids[bb_ix] && bb_sc == s1[bb_ix], "batch best");
+  for (uint64_t k = 0; k < (uint64_t)n; ++k)
+    CHECK(s1[k] < bb_sc || (s1[k] == bb_sc && k >= bb_ix), "batch best = lowest max index");
 
   /* the same library as CAPI sequence_t records (64 B each), query from a record */
   unsigned char (*recs)[SW_RECORD_BYTES] = calloc((size_t)n + 1, SW_RECORD_BYTES);
@@ -138,6 +147,13 @@ static int score(const char *qpath, const char *lpath) {
   sw_pack_2bit(qs[0], qlen, qrec + 6);
   CHECK(sw_load_query_record(bank, qrec) == SW_OK, "query record");
   CHECK(sw_score_records(bank, recs, (size_t)nrec, s2) == SW_OK, sw_last_error(bank));
+  CHECK(sw_batch_best(bank, &bb_id, &bb_sc, &bb_ix) == SW_OK, "records best");
+  CHECK(bb_sc == s2[bb_ix], "records best score");
+  {
+    uint32_t rid;
+    memcpy(&rid, recs[bb_ix], 4);
+    CHECK(bb_id == rid, "records best carries the record ID");
+  }
   for (int k = 0, r = 0; k < n; ++k) {
     if (strlen(ls[k]) > SW_RECORD_MAX_BASES) continue;
     CHECK(s2[r] == s1[k], "records path == byte path");
@@ -151,11 +167,11 @@ static int score(const char *qpath, const char *lpath) {
   printf("best %s %d\n", ln[best_id], best);
 
   /* argument errors */
-  CHECK(sw_score_batch(bank, res, NULL, lens, (size_t)n, s1) == SW_ERR_ARG, "null offsets");
+  CHECK(sw_score_batch(bank, res, NULL, lens, NULL, (size_t)n, s1) == SW_ERR_ARG, "null offsets");
   uint8_t bad = 9;
   CHECK(sw_load_query(bank, 0, &bad, 1) == SW_ERR_ARG, "code outside alphabet");
   sw_bank_destroy(bank);
-  free(q); free(res); free(offs); free(lens); free(s1); free(s2); free(recs);
+  free(q); free(res); free(offs); free(lens); free(s1); free(s2); free(recs); free(ids);
   printf("score ok\n");
   return 0;
 }

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_status_strings():
-    assert S.lib().sw_abi_version() == 1
+    assert S.lib().sw_abi_version() == S.ABI_VERSION == 2
     assert S.status_string(0) == "ok"
     assert "gfx950" in S.status_string(S.ERR_NO_DEVICE)
     assert S.lib().sw_max_query_len() >= 128
@@ -122,3 +122,38 @@ def test_no_cpu_fallback_without_gpu():
 def test_cli_usage_and_missing_inputs():
     r = subprocess.run([S.CLI_PATH], capture_output=True, text=True)
     assert r.returncode == 1 and "Input files missing" in r.stderr
+
+
+def test_batch_validation_rejects_mismatched_arrays():
+    """ScoreBank.score_batch validates on the host before the C feeder reads anything
+    (a short offsets array or an out-of-range target would otherwise be a host over-read)."""
+    res = np.zeros(10, np.uint8)
+    r, o, l, i = S.validate_batch(res, [0, 4], [4, 6], ids=[7, 8])
+    assert o.dtype == np.uint64 and l.dtype == np.uint32 and i.tolist() == [7, 8]
+    with pytest.raises(ValueError):
+        S.validate_batch(res, [0], [4, 6])            # fewer offsets than lengths
+    with pytest.raises(ValueError):
+        S.validate_batch(res, [0, -1], [4, 6])        # negative offset
+    with pytest.raises(ValueError):
+        S.validate_batch(res, [0, 5], [4, 6])         # runs past the residues
+    with pytest.raises(ValueError):
+        S.validate_batch(res, [0, 4], [4, 6], ids=[1])  # ids count
+    assert S.validate_batch(np.zeros(0, np.uint8), [], [])[2].size == 0
+
+
+def test_multi_device_config_without_gpu():
+    """A multi-device bank needs every listed device: none here, so it fails like a single
+    bank (no CPU fallback), and more than SW_MAX_DEVICES ordinals is an argument error."""
+    with pytest.raises(ValueError):
+        S.ScoreBank(devices=[0] * (S.MAX_DEVICES + 1))
+    if S.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(S.SwbankError) as ei:
+        S.ScoreBank(devices=[0, 0])
+    assert ei.value.status == S.ERR_NO_DEVICE
+
+
+def test_cli_rejects_bad_device_list():
+    r = subprocess.run([S.CLI_PATH, "-q", "x", "-l", "y", "-d", "0,a"], capture_output=True,
+                       text=True)
+    assert r.returncode == 1

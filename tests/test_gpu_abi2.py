@@ -1,0 +1,292 @@
+"""GPU: the ABI-2 surface — scores past the 16-bit lanes (int32 re-score), the batch best hit
+with caller ids (≙ ScoreBank_v2.v:39-43 results/IDs/max), the on-device length sort of ragged
+device batches, device records with corrupt lengths, and multi-device banks (the RTL's
+MODULES, ScoreBank_v2.v:76-148) with their RCCL / copy score gather.
+
+Every score is checked bit-exact against the oracle (test infrastructure only)."""
+import os
+
+import numpy as np
+import pytest
+
+import swbank as S
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+REF = (5, -4, -12, -4)
+
+
+def _codes(rng, n, alpha=4):
+    return rng.integers(0, alpha, n, dtype=np.uint8)
+
+
+def _mutate(rng, s, p, alpha=4):
+    t = s.copy()
+    m = rng.random(len(t)) < p
+    t[m] = rng.integers(0, alpha, int(m.sum()), dtype=np.uint8)
+    return t
+
+
+# ---- int32: scores past 65535 -------------------------------------------------------------
+@pytest.mark.parametrize("kernel", ["tile", "wave"])
+def test_scores_past_16_bits_dna(kernel, monkeypatch):
+    """A 14,000-bp query against near-copies of itself: self score 70,000 > 65,535.  The
+    16-bit pass flags those pairs and the int32 kernel re-scores them exactly."""
+    monkeypatch.setenv("SWBANK_KERNEL", kernel)
+    rng = np.random.default_rng(11)
+    q = _codes(rng, 14000)
+    seqs = [q.copy(), _mutate(rng, q, 0.01), _mutate(rng, q, 0.2), q[:9000].copy(),
+            _codes(rng, 300), np.zeros(0, np.uint8), q[5000:].copy()]
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+        kern = bank.last_kernel()
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)
+    assert want[0] == 70000 and want.max() > 65535
+    assert (got == want).all(), (kern, got.tolist(), want.tolist())
+    assert "+i32-rescore" in kern
+
+
+def test_scores_past_16_bits_protein_gotoh():
+    """BLOSUM62 / Gotoh: a 13,000-aa query (SWB_MAX_QUERY is 65,536 now) against itself and
+    mutants; the self score is above the 16-bit bound."""
+    rng = np.random.default_rng(12)
+    q = rng.integers(0, 20, 13000, dtype=np.uint8)
+    seqs = [q.copy(), _mutate(rng, q, 0.05, 20), rng.integers(0, 20, 700, dtype=np.uint8)]
+    with S.ScoreBank(alphabet=S.ALPHABET_PROTEIN, gap_model=S.GAP_GOTOH) as bank:
+        bank.set_matrix(O.BLOSUM62, -11, -1)
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+        kern = bank.last_kernel()
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.BLOSUM62, -11, -1, O.GAP_GOTOH)
+    assert want[0] > 65535
+    assert (got == want).all(), (kern, got.tolist(), want.tolist())
+
+
+@pytest.mark.parametrize("case", ["dna-ref", "dna-col0", "dna-gotoh", "prot-merged",
+                                  "prot-gotoh", "dna-N"])
+@pytest.mark.parametrize("qlen", [1, 5, 63, 64, 255, 256, 257, 700])
+def test_int32_kernel_everywhere(case, qlen, monkeypatch):
+    """SWBANK_I32=1 routes every pair through the int32 kernel (after the 16-bit pass), so the
+    kernel itself is checked on random shapes, both gap models, the HDL column-0 rule, protein
+    and N codes, across strip boundaries (256 rows)."""
+    monkeypatch.setenv("SWBANK_I32", "1")
+    rng = np.random.default_rng(hash((case, qlen)) % 2**32)
+    prot = case.startswith("prot")
+    alpha = 20 if prot else 4
+    model = S.GAP_GOTOH if case.endswith("gotoh") else S.GAP_MERGED
+    q = rng.integers(0, alpha, qlen, dtype=np.uint8)
+    seqs = [rng.integers(0, alpha, int(rng.integers(0, 400)), dtype=np.uint8) for _ in range(150)]
+    seqs += [_mutate(rng, q, 0.1, alpha), q[: qlen // 2].copy()]
+    if case == "dna-N":
+        for t in seqs[:40]:
+            t[rng.random(len(t)) < 0.1] = 4
+    with S.ScoreBank(alphabet=S.ALPHABET_PROTEIN if prot else S.ALPHABET_DNA,
+                     gap_model=model) as bank:
+        if prot:
+            sub, go, ge = O.BLOSUM62, -11, -1
+            bank.set_matrix(sub, go, ge)
+        else:
+            pen = {"dna-col0": (9, -3, -2, -1)}.get(case, REF)
+            sub, go, ge = O.dna_matrix(pen[0], pen[1]), pen[2], pen[3]
+            bank.set_penalties(*pen)
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+        assert "+i32-rescore" in bank.last_kernel()
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, sub.astype(np.int8), go, ge, model)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), int(lens[i]), int(got[i]), int(want[i])) for i in bad[:6]]
+
+
+def test_int32_kernel_on_records(monkeypatch):
+    monkeypatch.setenv("SWBANK_I32", "1")
+    rng = np.random.default_rng(5)
+    q = _codes(rng, 300)
+    seqs = [_codes(rng, int(rng.integers(0, 233))) for _ in range(300)]
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        got = bank.score_records(S.make_records(seqs))
+    res, offs, lens = O.pack_residues(seqs)
+    assert (got == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
+
+
+# ---- batch best hit with ids ---------------------------------------------------------------
+def test_batch_best_host_device_and_records():
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(21)
+    q = _codes(rng, 128)
+    seqs = [_codes(rng, int(rng.integers(1, 200))) for _ in range(3000)]
+    seqs[1234] = q.copy()                      # the unique best
+    seqs[2345] = q.copy()                      # a tie: the lower index wins
+    ids = (np.arange(len(seqs), dtype=np.uint64) * 7919 + (1 << 40))
+    res, offs, lens = O.pack_residues(seqs)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        sc = bank.score_batch(res, offs, lens, ids=ids)
+        assert bank.best() == (int(ids[1234]), 640, 1234)
+        bank.score_batch(res, offs, lens)      # no ids: the id is the index
+        assert bank.best() == (1234, 640, 1234)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        d_res = torch.from_numpy(res).to(dev)
+        d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+        d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+        d_ids = torch.from_numpy(ids.view(np.int64)).to(dev)
+        d_sc = torch.zeros(len(seqs), dtype=torch.int32, device=dev)
+        st = torch.cuda.current_stream().cuda_stream
+        bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(),
+                                len(seqs), int(lens.max()), d_sc.data_ptr(), st,
+                                d_ids=d_ids.data_ptr())
+        assert bank.best() == (int(ids[1234]), 640, 1234)
+        assert (d_sc.cpu().numpy() == sc).all()
+        bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(),
+                                len(seqs), int(lens.max()), d_sc.data_ptr(), st)
+        with pytest.raises(S.SwbankError) as e:  # a device call without ids records nothing
+            bank.best()
+        assert e.value.status == S.ERR_STATE
+        short = [s[:232] for s in seqs]
+        rec = S.make_records(short, ids=[int(i) & 0xFFFFFFFF for i in ids])
+        rs = bank.score_records(rec)
+        b = int(np.argmax(rs))
+        assert bank.best() == (int(ids[b]) & 0xFFFFFFFF, int(rs[b]), b)
+
+
+# ---- ragged device batches: on-device length sort -------------------------------------------
+@pytest.mark.parametrize("lo,hi", [(64, 128), (1, 150), (0, 1000), (100, 101)])
+def test_device_sort_ragged(lo, hi, monkeypatch):
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(lo * 1000 + hi)
+    q = _codes(rng, 150)
+    n = 20000
+    lens0 = rng.integers(lo, hi + 1, n)
+    seqs = [_codes(rng, int(l)) for l in lens0]
+    for t in seqs[::97]:
+        t[rng.random(len(t)) < 0.05] = 4
+    res, offs, lens = O.pack_residues(seqs)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out = {}
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        for dsort in ("1", "0"):
+            monkeypatch.setenv("SWBANK_DSORT", dsort)
+            d_sc = torch.full((n,), -1, dtype=torch.int32, device=dev)
+            bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n,
+                                    max(int(lens.max()), 1), d_sc.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            out[dsort] = d_sc.cpu().numpy()
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)
+    assert (out["1"] == want).all() and (out["0"] == want).all()
+
+
+# ---- device records with a corrupt length field --------------------------------------------
+def test_device_records_clamp_corrupt_lengths():
+    """A device record whose length field exceeds 232 is read as 232 bases (the kernels clamp
+    it): no read past the data field or the buffer, same score as the 232-base
+    record, with a query of several segments too (edge rows sized for 232 columns)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(3)
+    seqs = [_codes(rng, 232) for _ in range(300)]
+    rec = S.make_records(seqs)
+    bad = rec.copy()
+    bad[::3, 4:6] = np.frombuffer(np.uint16(60000).tobytes(), np.uint8)
+    bad[1::3, 4:6] = np.frombuffer(np.uint16(233).tobytes(), np.uint8)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    for qlen in (100, 1500):
+        q = _codes(rng, qlen)
+        with S.ScoreBank() as bank:
+            bank.set_penalties(*REF)
+            bank.load_query(q)
+            good = bank.score_records(rec)
+            d_rec = torch.from_numpy(bad.reshape(-1)).to(dev)
+            d_sc = torch.full((len(seqs),), -1, dtype=torch.int32, device=dev)
+            bank.score_records_device(d_rec.data_ptr(), len(seqs), d_sc.data_ptr(),
+                                      torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            assert (d_sc.cpu().numpy() == good).all()
+
+
+# ---- multi-device banks ---------------------------------------------------------------------
+def _ragged_batch(seed, n=5000):
+    rng = np.random.default_rng(seed)
+    q = _codes(rng, 150)
+    seqs = [_codes(rng, int(l)) for l in rng.integers(0, 1200, n)]
+    seqs[n // 2] = q.copy()
+    return q, seqs
+
+
+@pytest.mark.parametrize("devices,gather", [([0, 0], "copy"), ([0, 0, 0], "copy"),
+                                            ([0], "rccl"), ([0], "copy")])
+def test_multi_device_bank_equals_single(devices, gather, monkeypatch):
+    """A multi-device bank on the one GPU of the box: [0, 0] deals the batch over two child
+    banks and gathers with device copies (RCCL refuses two ranks on one device); [0] with
+    SWBANK_GATHER=rccl runs the real ncclCommInitAll + ncclGather path on a 1-rank comm.
+    Scores must equal the single bank's bit for bit, in input order, with the best hit."""
+    monkeypatch.setenv("SWBANK_GATHER", gather)
+    q, seqs = _ragged_batch(len(devices) * 10 + len(gather))
+    res, offs, lens = O.pack_residues(seqs)
+    ids = np.arange(len(seqs), dtype=np.uint64) + 500
+    with S.ScoreBank() as one:
+        one.set_penalties(*REF)
+        one.load_query(q)
+        want = one.score_batch(res, offs, lens)
+    with S.ScoreBank(devices=devices) as multi:
+        assert multi.devices() == devices
+        multi.set_penalties(*REF)
+        multi.load_query(q)
+        got = multi.score_batch(res, offs, lens, ids=ids)
+        kern = multi.last_kernel()
+        assert kern.startswith(f"multi[{len(devices)}] gather={gather}"), kern
+        assert (got == want).all()
+        b = int(np.argmax(want))
+        assert multi.best() == (int(ids[b]), int(want[b]), b)
+        # records through the same bank
+        short = [s[:232] for s in seqs]
+        r_multi = multi.score_records(S.make_records(short))
+        with pytest.raises(S.SwbankError) as e:  # device buffers need a single-device bank
+            multi.score_batch_device(0, 0, 0, 1, 1, 0)
+        assert e.value.status == S.ERR_UNSUPPORTED
+    res2, offs2, lens2 = O.pack_residues(short)
+    assert (r_multi == O.score_batch(q, res2, offs2, lens2, O.dna_matrix(), -12, -4)).all()
+    assert (want == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
+
+
+def test_multi_device_bank_bad_input_leaves_bank_usable(monkeypatch):
+    """A code outside the alphabet on one device's share fails the call before any gather is
+    issued (no rank is left waiting in the collective) and the bank stays usable."""
+    monkeypatch.setenv("SWBANK_GATHER", "copy")
+    q, seqs = _ragged_batch(3, 2000)
+    bad = [s.copy() for s in seqs]
+    bad[1500] = np.array([9, 9, 9], np.uint8)
+    with S.ScoreBank(devices=[0, 0]) as multi:
+        multi.set_penalties(*REF)
+        multi.load_query(q)
+        with pytest.raises(S.SwbankError) as e:
+            multi.score_targets(bad)
+        assert e.value.status == S.ERR_ARG
+        got = multi.score_targets(seqs)
+    res, offs, lens = O.pack_residues(seqs)
+    assert (got == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
+
+
+def test_cli_device_list(tmp_path, monkeypatch):
+    """swbank -d 0,0: the CLI's multi-device bank reproduces the single-device transcript."""
+    import subprocess
+    monkeypatch.setenv("SWBANK_GATHER", "copy")
+    q, lib = O.golden_fasta("query100.fa"), O.golden_fasta("data500.fa")
+    one = subprocess.run([S.CLI_PATH, "-q", q, "-l", lib], capture_output=True, text=True)
+    two = subprocess.run([S.CLI_PATH, "-q", q, "-l", lib, "-d", "0,0", "-b"], capture_output=True,
+                         text=True)
+    assert one.returncode == 0 and two.returncode == 0, two.stderr
+    assert one.stdout == two.stdout and one.stdout.count("score:") == 499
+    assert two.stderr.startswith("best: >")

@@ -1,0 +1,61 @@
+"""GPU: bench.py's own flows, end to end, as the driver runs them.
+
+* N = 2 ranks under ``torch.distributed.run`` on the box's one GPU (SWBENCH_SHARE_GPU=1 puts both
+  ranks on device 0; SWBENCH_BACKEND=gloo because RCCL refuses two ranks on one device): one
+  JSON line with n_gpus 2, and rank 0's parity check covers the slice it GATHERED from rank 1
+  (regenerated from rank 1's seed and re-scored by the oracle).
+* the ragged and literal-data500 workloads at reduced size (parity sample 0 mismatches).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _json_line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("workload", ["q100xdata500", "ragged"])
+def test_bench_two_ranks_gathered_parity(workload):
+    env = dict(os.environ, SWBENCH_BACKEND="gloo", SWBENCH_SHARE_GPU="1",
+               MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--reps", "64", "--cpu-seconds", "0", "--workload", workload]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["scaling"] == "weak"
+    ps = d["parity_sample"]
+    assert ps["ranks"] == 2 and ps["mismatches"] == 0 and ps["targets"] >= 2 * 256
+
+
+@pytest.mark.parametrize("workload", ["ragged", "data500"])
+def test_bench_workloads_one_gpu(workload):
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
+           "--reps", "64", "--cpu-seconds", "0", "--workload", workload]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 1 and d["parity_sample"]["mismatches"] == 0
+    assert d["pcie_inclusive"]["matches_device_api"] is True
+    assert 0 < d["roofline"]["frac"] <= 1.0
