@@ -119,16 +119,17 @@ sw_status sw_set_matrix(sw_bank *bank, const int8_t *matrix, int32_t alpha, int3
 sw_status sw_load_query(sw_bank *bank, uint64_t id, const uint8_t *codes, uint32_t len);
 
 /* ---- target stream -> scores ----------------------------------------------------------- */
-/* Host buffers, blocking.  Target k = residues[offsets[k] .. offsets[k]+lens[k]) (codes),
+/* Host buffers, blocking.  Target k = residues[offsets[k] .. offsets[k]+lens[k]) (codes) of
+ * the residues_len-byte buffer (a target outside it is SW_ERR_ARG, nothing past it is read),
  * tagged ids[k] (the RTL's 48-bit record ID, ScoreBank_v2.v:26-28,39-41; NULL = the index k).
  * scores_out[k] = max local-alignment score of (query, target k).  The bank feeds the batch in
  * chunks through pinned staging on its own worker threads and a copy stream (gather, PCIe and
  * scoring overlap), so host buffers need no pinning or layout; n < 2^32.  The call also records
  * the batch's best hit for sw_batch_best.  A multi-device bank deals the batch over its
  * devices and gathers the scores back in input order. */
-sw_status sw_score_batch(sw_bank *bank, const uint8_t *residues, const uint64_t *offsets,
-                         const uint32_t *lens, const uint64_t *ids, size_t n,
-                         int32_t *scores_out);
+sw_status sw_score_batch(sw_bank *bank, const uint8_t *residues, size_t residues_len,
+                         const uint64_t *offsets, const uint32_t *lens, const uint64_t *ids,
+                         size_t n, int32_t *scores_out);
 
 /* Device buffers, asynchronous on `stream` (a hipStream_t; NULL = the bank's stream).
  * max_len must be >= every lens[k]; targets are visited in the caller's order unless their

@@ -205,7 +205,7 @@ int main(int argc, char **argv) {
     lens[k] = (uint32_t)l;
     pos += l;
   }
-  if (st == SW_OK) st = sw_score_batch(bank, res, offs, lens, NULL, lib.n, scores);
+  if (st == SW_OK) st = sw_score_batch(bank, res, total, offs, lens, NULL, lib.n, scores);
   if (st != SW_OK) {
     fprintf(stderr, "swbank: %s: %s\n", sw_status_string(st), sw_last_error(bank));
     sw_bank_destroy(bank);

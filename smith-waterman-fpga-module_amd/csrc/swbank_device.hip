@@ -44,14 +44,15 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                        const void* edge_in, void* edge_out, uint32_t ecols,
                                        int accum, int packed, const uint32_t* idx,
-                                       const uint32_t* nidx, uint32_t idx_base, int pair,
-                                       uint32_t pS1, uint32_t pS2, hipStream_t st);
+                                       const uint32_t* nidx, uint32_t idx_base,
+                                       const uint32_t* ident, int pair, uint32_t pS1,
+                                       uint32_t pS2, hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
                                    hipStream_t st);
 extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max_len,
-                                    uint32_t* perm, uint32_t* perm_n, uint32_t* scratch,
-                                    hipStream_t st);
+                                    uint32_t* perm, uint32_t* perm_n, uint32_t* ident,
+                                    uint32_t* scratch, hipStream_t st);
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
                                     uint32_t* idx, uint32_t* count, hipStream_t st);
 extern "C" size_t swk_i32_waves(size_t n, uint32_t scols, size_t budget_bytes);
@@ -1047,13 +1048,16 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   }
   // A device batch (dsort) visits its targets longest first, sorted on the device, so every
   // tile holds similar lengths (a tile runs to its longest lane); SWBANK_DSORT=0 disables.
+  const uint32_t* ident = nullptr;  // device sort: 1 when the lengths share one bin
   if (dsort && !use_wave && !perm && packed == SWK_PACK_BYTES && ntiles > 1 &&
       n <= 0xFFFFFFFFull && env_int("SWBANK_DSORT", 1) != 0) {
-    HIPOK(b, b->dperm.reserve(n + 1));
+    HIPOK(b, b->dperm.reserve(n + 2));
     HIPOK(b, b->dsort.reserve(2048));
-    HIPOK(b, swk_sort_lens(d_lens, n, max_len, b->dperm.p, b->dperm.p + n, b->dsort.p, st));
+    HIPOK(b, swk_sort_lens(d_lens, n, max_len, b->dperm.p, b->dperm.p + n, b->dperm.p + n + 1,
+                           b->dsort.p, st));
     perm = b->dperm.p;
     perm_n = b->dperm.p + n;
+    ident = b->dperm.p + n + 1;
   }
   // Segmented queries hand each segment's bottom row to the next through HBM: ntiles x ecols
   // x 512 B per edge buffer.  Past SWBANK_EDGE_MB (default 2048) the batch runs as
@@ -1115,8 +1119,8 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                                   f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
                                   pair ? b->pair_bytes : f16 && b->prof ? b->PS16 : b->PS,
                                   b->pad, b->segs[s].W, scores, ein, eout, ecols, s > 0 ? 1 : 0,
-                                  (int)packed, idx, nidx, (uint32_t)p0, pair ? 1 : 0, b->pS1,
-                                  b->pS2, st));
+                                  (int)packed, idx, nidx, (uint32_t)p0,
+                                  pass == 0 ? ident : nullptr, pair ? 1 : 0, b->pS1, b->pS2, st));
       }
     }
   }
@@ -1455,8 +1459,9 @@ static inline uint32_t pack_4bit(const uint8_t* src, uint32_t l, uint8_t* dst) {
 }
 
 // The host-buffer batch through the feeder (n >= 1, buffers checked by the caller).
-static sw_status batch_feed(sw_bank* b, const uint8_t* residues, const uint64_t* offsets,
-                            const uint32_t* lens, size_t n, bool to_host) {
+static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
+                            const uint64_t* offsets, const uint32_t* lens, size_t n,
+                            bool to_host) {
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
   if ((st = feeder_init(b)) != SW_OK) return st;
@@ -1523,7 +1528,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, const uint64_t*
   std::vector<uint32_t> chunk_mode(chunks.size(), SWK_PACK_BYTES);
   std::vector<size_t> part(T + 1), part2(T + 1), part4(T + 1);
   std::vector<uint32_t> partmax(T);
-  std::atomic<size_t> bad{SIZE_MAX};
+  std::atomic<size_t> bad{SIZE_MAX}, oob{SIZE_MAX};
   std::atomic<uint32_t> wide{0};
   size_t gi = 0, si = 0;
   const auto gather = [&](uint8_t* slot, const Chunk& c) -> size_t {
@@ -1538,21 +1543,41 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, const uint64_t*
     std::fill(part.begin(), part.end(), 0);
     std::fill(part2.begin(), part2.end(), 0);
     std::fill(part4.begin(), part4.end(), 0);
+    oob = SIZE_MAX;
     pool.run([&](unsigned p) {
       size_t acc = 0, acc2 = 0, acc4 = 0;
       uint32_t m = 0;
+      bool out = false;
       for (size_t k = c.c0 + std::min(cnt, p * step); k < c.c0 + std::min(cnt, (p + 1) * step);
            ++k) {
         acc += lens[k];
         acc2 += (lens[k] + 3) / 4;
         acc4 += (lens[k] + 1) / 2;
         m = std::max(m, lens[k]);
+        // the target must lie inside the caller's residues (checked before any byte is read;
+        // the pack passes below re-read this part's offsets from cache)
+        out |= offsets[k] > nres || lens[k] > nres - offsets[k];
       }
+      if (out)
+        for (size_t k = c.c0 + std::min(cnt, p * step); k < c.c0 + std::min(cnt, (p + 1) * step);
+             ++k)
+          if (offsets[k] > nres || lens[k] > nres - offsets[k]) {
+            size_t cur = oob.load();
+            while (k < cur && !oob.compare_exchange_weak(cur, k)) {
+            }
+            break;
+          }
       part[p + 1] = acc;
       part2[p + 1] = acc2;
       part4[p + 1] = acc4;
       partmax[p] = m;
     });
+    if (oob.load() != SIZE_MAX) {
+      const size_t k = oob.load();
+      fail(b, SW_ERR_ARG, "target %zu [%llu, +%u) outside the %zu residues", k,
+           (unsigned long long)offsets[k], lens[k], nres);
+      return 0;
+    }
     chunk_max[gi] = *std::max_element(partmax.begin(), partmax.end());
     for (unsigned p = 0; p < T; ++p) {
       part[p + 1] += part[p];
@@ -1853,8 +1878,9 @@ static void host_best(sw_bank* b, const int32_t* scores, size_t n) {
   b->best_kind = 1;
 }
 
-static sw_status multi_batch(sw_bank* b, const uint8_t* residues, const uint64_t* offsets,
-                             const uint32_t* lens, size_t n, int32_t* scores_out) {
+static sw_status multi_batch(sw_bank* b, const uint8_t* residues, size_t nres,
+                             const uint64_t* offsets, const uint32_t* lens, size_t n,
+                             int32_t* scores_out) {
   const size_t D = b->kids.size();
   // length-balanced deal (SURVEY §8 e): longest first, round robin -> each device gets every
   // D-th target of the sorted order, itself already longest first (its feeder skips the sort)
@@ -1879,7 +1905,7 @@ static sw_status multi_batch(sw_bank* b, const uint8_t* residues, const uint64_t
     }
   });
   sw_status st = multi_gather(b, cnt, [&](unsigned d) {
-    return batch_feed(b->kids[d], residues, offs[d].data(), lns[d].data(), cnt[d], false);
+    return batch_feed(b->kids[d], residues, nres, offs[d].data(), lns[d].data(), cnt[d], false);
   });
   if (st != SW_OK) return st;
   const size_t cmax = cnt[0];
@@ -1914,9 +1940,9 @@ static sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_
   return SW_OK;
 }
 
-extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const uint64_t* offsets,
-                                    const uint32_t* lens, const uint64_t* ids, size_t n,
-                                    int32_t* scores_out) {
+extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, size_t residues_len,
+                                    const uint64_t* offsets, const uint32_t* lens,
+                                    const uint64_t* ids, size_t n, int32_t* scores_out) {
   if (!b) return SW_ERR_ARG;
   b->best_kind = 0;
   if (n == 0) return SW_OK;
@@ -1924,11 +1950,11 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, const u
   if (n > 0xFFFFFFFFull)
     return fail(b, SW_ERR_ARG, "host batches hold < 2^32 targets (sw_score_batch_device does not)");
   if (b->is_multi()) {
-    const sw_status st = multi_batch(b, residues, offsets, lens, n, scores_out);
+    const sw_status st = multi_batch(b, residues, residues_len, offsets, lens, n, scores_out);
     if (st == SW_OK && ids) b->best_id = ids[b->best_index];
     return st;
   }
-  const sw_status st = batch_feed(b, residues, offsets, lens, n, true);
+  const sw_status st = batch_feed(b, residues, residues_len, offsets, lens, n, true);
   if (st != SW_OK) return st;
   const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
   parallel_for(*b->pool, n, [&](size_t lo, size_t hi) {

@@ -529,6 +529,7 @@ struct ScoreArgs {
   const uint32_t* idx;
   const uint32_t* nidx;   // with idx: positions [0, min(n, *nidx - idx_base)) are valid
   uint32_t idx_base;
+  const uint32_t* ident;  // optional: *ident != 0 -> idx is the identity (ignore it)
   // PAIR (f16 DNA merged): letter-pair table strides; slot (a, b) at 16 + a*pS1 + b*pS2
   uint32_t pS1, pS2;
   // f16 kernels: f16_pair(-(o+e)), f16_pair(-e), f16_pair(-o)
@@ -597,7 +598,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   uint8_t* prof = reinterpret_cast<uint8_t*>(ring + (size_t)(W > 1 ? W - 1 : 0) * 2 * C * 64);
 
   size_t n = a.n;
-  if (a.idx) {
+  const uint32_t* idx = a.idx;
+  if (idx && a.ident && __builtin_amdgcn_readfirstlane(*a.ident)) idx = nullptr;
+  if (idx) {
     const uint32_t cnt = __builtin_amdgcn_readfirstlane(*a.nidx);
     n = cnt > a.idx_base ? min(a.n, (size_t)(cnt - a.idx_base)) : 0;
   }
@@ -606,10 +609,10 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   int total = 0;  // chunks of all this workgroup's tiles: every wave runs total + W - 1 phases
   const uint32_t packed = a.packed;
   for (int t = blockIdx.x; t < ntiles; t += G)
-    total += tile_nch(a.res, a.lens, n, t, lane, packed, a.idx);
+    total += tile_nch(a.res, a.lens, n, t, lane, packed, idx);
 
   int tile = blockIdx.x;
-  Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, a.idx);
+  Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, idx);
   int nch, nfull;
   tile_chunks(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
               nfull);
@@ -722,7 +725,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       if (!last) {
         load_raw(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
       } else if (ntile < ntiles) {  // first chunk of the next tile
-        cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed, a.idx);
+        cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed, idx);
         tile_chunks(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
                     n, nch_n, nfull_n);
         load_raw(cur, 0, nfull_n > 0, a.pad, packed, rlo, rhi);
@@ -889,8 +892,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
             blo = f16_unscore((uint32_t)blo);
             bhi = f16_unscore((uint32_t)bhi);
           }
-          const size_t slo = a.idx && tlo < n ? a.idx[tlo] : tlo;
-          const size_t shi = a.idx && thi < n ? a.idx[thi] : thi;
+          const size_t slo = idx && tlo < n ? idx[tlo] : tlo;
+          const size_t shi = idx && thi < n ? idx[thi] : thi;
           if (a.accum) {  // best over the previous query segments
             if (tlo < n) blo = max(blo, a.scores[slo]);
             if (thi < n) bhi = max(bhi, a.scores[shi]);
@@ -1416,13 +1419,14 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                        const void* edge_in, void* edge_out, uint32_t ecols,
                                        int accum, int packed, const uint32_t* idx,
-                                       const uint32_t* nidx, uint32_t idx_base, int pair,
-                                       uint32_t pS1, uint32_t pS2, hipStream_t st) {
+                                       const uint32_t* nidx, uint32_t idx_base,
+                                       const uint32_t* ident, int pair, uint32_t pS1,
+                                       uint32_t pS2, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                          O,    E,    PS,   pad, scores, static_cast<const uint2*>(edge_in),
                          static_cast<uint2*>(edge_out), ecols, (uint32_t)accum, (uint32_t)packed,
-                         idx, nidx, idx_base, pS1, pS2,
+                         idx, nidx, idx_base, ident, pS1, pS2,
                          swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
                          swk::f16_pair(-(int)O)};
   const uint32_t prof_bytes = (pad + 1) * PS;
@@ -1521,7 +1525,7 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
                          static_cast<const uint2*>(edge_in), static_cast<uint2*>(edge_out), ecols,
-                         (uint32_t)accum, (uint32_t)packed, nullptr, nullptr, 0u, 0u, 0u,
+                         (uint32_t)accum, (uint32_t)packed, nullptr, nullptr, 0u, nullptr, 0u, 0u,
                          swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
                          swk::f16_pair(-(int)O)};
   const uint32_t prof_bytes = (pad + 1) * PS;
@@ -1733,6 +1737,26 @@ __device__ __forceinline__ uint32_t sort_bin(uint32_t len, uint32_t max_len, uin
   return (max_len - min(len, max_len)) >> shift;
 }
 
+// h[bin] += 1 for the active lanes; returns the lane's slot (the old value + its rank among
+// the lanes of its bin).  A wave whose lanes share one bin (uniform or already sorted lengths)
+// adds once from its first lane; otherwise every lane adds its own (distinct bins rarely
+// collide, and 64 serialised atomics on one address were the cost this avoids).
+__device__ __forceinline__ uint32_t wave_bin_add(uint32_t* h, uint32_t bin, bool active) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t act = __ballot(active);
+  if (!act) return 0;
+  const int leader = __builtin_ctzll(act);
+  const uint32_t lb = __builtin_amdgcn_readlane(bin, leader);
+  const uint64_t m = __ballot(active && bin == lb);
+  if (m == act) {
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&h[lb], (uint32_t)__builtin_popcountll(m));
+    base = __builtin_amdgcn_readlane(base, leader);
+    return base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1));
+  }
+  return active ? atomicAdd(&h[bin], 1u) : 0u;
+}
+
 __global__ void __launch_bounds__(SORT_BLOCK) sort_hist(const uint32_t* lens, size_t n,
                                                         uint32_t max_len, uint32_t shift,
                                                         uint32_t nb, uint32_t* hist) {
@@ -1743,19 +1767,23 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_hist(const uint32_t* lens, si
 #pragma unroll
   for (int it = 0; it < SORT_ITEMS; ++it) {
     const size_t k = base + (size_t)it * SORT_BLOCK + threadIdx.x;
-    if (k < n) atomicAdd(&h[sort_bin(lens[k], max_len, shift)], 1u);
+    (void)wave_bin_add(h, k < n ? sort_bin(lens[k], max_len, shift) : 0u, k < n);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK)
     if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
+// Exclusive offsets in place, *perm_n = n, ident[0] = 1 when at most one bin is non-empty (the
+// caller's order is already fine: the scatter and the score kernel's indirection are skipped).
 __global__ void __launch_bounds__(SORT_BLOCK) sort_scan(uint32_t* hist, uint32_t nb, size_t n,
-                                                        uint32_t* perm_n) {
+                                                        uint32_t* perm_n, uint32_t* ident) {
   __shared__ uint32_t part[SORT_BLOCK];
   // each thread owns 2 consecutive bins (nb <= 2048)
   const uint32_t i0 = threadIdx.x * 2;
   const uint32_t a = i0 < nb ? hist[i0] : 0u, c = i0 + 1 < nb ? hist[i0 + 1] : 0u;
+  const int used = __syncthreads_count((a != 0) + (c != 0) > 0 ? 1 : 0) +
+                   __syncthreads_count(a != 0 && c != 0 ? 1 : 0);
   part[threadIdx.x] = a + c;
   __syncthreads();
   for (uint32_t off = 1; off < SORT_BLOCK; off <<= 1) {  // inclusive Hillis-Steele scan
@@ -1767,23 +1795,27 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_scan(uint32_t* hist, uint32_t
   const uint32_t ex = part[threadIdx.x] - (a + c);
   if (i0 < nb) hist[i0] = ex;
   if (i0 + 1 < nb) hist[i0 + 1] = ex + a;
-  if (threadIdx.x == 0) *perm_n = (uint32_t)n;
+  if (threadIdx.x == 0) {
+    *perm_n = (uint32_t)n;
+    *ident = used <= 1 ? 1u : 0u;
+  }
 }
 
 __global__ void __launch_bounds__(SORT_BLOCK) sort_scatter(const uint32_t* lens, size_t n,
                                                            uint32_t max_len, uint32_t shift,
                                                            uint32_t nb, uint32_t* offs,
-                                                           uint32_t* perm) {
+                                                           uint32_t* perm, const uint32_t* ident) {
+  if (__builtin_amdgcn_readfirstlane(*ident)) return;  // one length bin: order unchanged
   __shared__ uint32_t h[SORT_BINS];
   for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK) h[i] = 0;
   __syncthreads();
   const size_t base = (size_t)blockIdx.x * SORT_BLOCK * SORT_ITEMS;
-  uint32_t bin[SORT_ITEMS];
+  uint32_t bin[SORT_ITEMS], slot[SORT_ITEMS];
 #pragma unroll
   for (int it = 0; it < SORT_ITEMS; ++it) {
     const size_t k = base + (size_t)it * SORT_BLOCK + threadIdx.x;
     bin[it] = k < n ? sort_bin(lens[k], max_len, shift) : 0u;
-    if (k < n) atomicAdd(&h[bin[it]], 1u);
+    slot[it] = wave_bin_add(h, bin[it], k < n);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK)  // reserve this block's ranges
@@ -1792,15 +1824,16 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_scatter(const uint32_t* lens,
 #pragma unroll
   for (int it = 0; it < SORT_ITEMS; ++it) {
     const size_t k = base + (size_t)it * SORT_BLOCK + threadIdx.x;
-    if (k < n) perm[atomicAdd(&h[bin[it]], 1u)] = (uint32_t)k;
+    if (k < n) perm[h[bin[it]] + slot[it]] = (uint32_t)k;
   }
 }
 }  // namespace swk
 
-// perm[0, n) <- target numbers longest first, *perm_n <- n; scratch: SORT_BINS words.
+// perm[0, n) <- target numbers longest first, *perm_n <- n, *ident <- 1 when the lengths
+// share one bin (perm then left unwritten: visit in input order); scratch: SORT_BINS words.
 extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max_len,
-                                    uint32_t* perm, uint32_t* perm_n, uint32_t* scratch,
-                                    hipStream_t st) {
+                                    uint32_t* perm, uint32_t* perm_n, uint32_t* ident,
+                                    uint32_t* scratch, hipStream_t st) {
   if (n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
   uint32_t shift = 0;
   while ((max_len >> shift) >= (uint32_t)swk::SORT_BINS) ++shift;
@@ -1811,8 +1844,9 @@ extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max
       (unsigned)((n + swk::SORT_BLOCK * swk::SORT_ITEMS - 1) / (swk::SORT_BLOCK * swk::SORT_ITEMS));
   hipLaunchKernelGGL(swk::sort_hist, dim3(blocks), dim3(swk::SORT_BLOCK), 0, st, lens, n, max_len,
                      shift, nb, scratch);
-  hipLaunchKernelGGL(swk::sort_scan, dim3(1), dim3(swk::SORT_BLOCK), 0, st, scratch, nb, n, perm_n);
+  hipLaunchKernelGGL(swk::sort_scan, dim3(1), dim3(swk::SORT_BLOCK), 0, st, scratch, nb, n, perm_n,
+                     ident);
   hipLaunchKernelGGL(swk::sort_scatter, dim3(blocks), dim3(swk::SORT_BLOCK), 0, st, lens, n,
-                     max_len, shift, nb, scratch, perm);
+                     max_len, shift, nb, scratch, perm, ident);
   return hipGetLastError();
 }

@@ -96,7 +96,7 @@ def lib() -> ctypes.CDLL:
         "sw_set_penalties": (i32, [P, i32, i32, i32, i32]),
         "sw_set_matrix": (i32, [P, P, i32, i32, i32]),
         "sw_load_query": (i32, [P, u64, P, u32]),
-        "sw_score_batch": (i32, [P, P, P, P, P, sz, P]),
+        "sw_score_batch": (i32, [P, P, sz, P, P, P, sz, P]),
         "sw_score_batch_device": (i32, [P, P, P, P, P, sz, u32, P, P]),
         "sw_batch_best": (i32, [P, P, P, P]),
         "sw_bank_devices": (i32, [P, P, i32]),
@@ -209,9 +209,11 @@ def pack_targets(seqs: Sequence[np.ndarray]) -> Tuple[np.ndarray, np.ndarray, np
 
 def validate_batch(residues, offsets, lens, ids=None):
     """Host batch -> contiguous (residues u8, offsets u64, lens u32, ids u64 | None), or
-    ValueError when the arrays disagree: the C feeder reads residues[offsets[k] :
-    offsets[k] + lens[k]] for every k < len(lens), so a short or out-of-range array would be a
-    host over-read inside the library rather than a Python error."""
+    ValueError when the arrays disagree: the C feeder reads offsets[k], lens[k] (and ids[k])
+    for every k < len(lens), so a short array would be a host over-read inside the library
+    rather than a Python error.  Each target's range against the residues is checked by the
+    library itself (sw_score_batch takes the residue count; SW_ERR_ARG, nothing read past it),
+    inside the feeder pass that reads the offsets anyway."""
     res = np.ascontiguousarray(residues, dtype=np.uint8).reshape(-1)
     ln = np.ascontiguousarray(lens, dtype=np.uint32).reshape(-1)
     off_in = np.asarray(offsets).reshape(-1)
@@ -220,8 +222,6 @@ def validate_batch(residues, offsets, lens, ids=None):
     if off_in.size and np.issubdtype(off_in.dtype, np.signedinteger) and off_in.min() < 0:
         raise ValueError("negative offset")
     offs = np.ascontiguousarray(off_in, dtype=np.uint64)
-    if ln.size and int((offs + ln.astype(np.uint64)).max()) > res.size:
-        raise ValueError("a target runs past the end of residues")
     idv = None
     if ids is not None:
         idv = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1)
@@ -304,7 +304,7 @@ class ScoreBank:
         out = np.empty(len(ln), dtype=np.int32)  # every entry written by the library
         if len(ln) == 0:
             return out
-        self._check(lib().sw_score_batch(self._h, _p(res), _p(offs), _p(ln),
+        self._check(lib().sw_score_batch(self._h, _p(res), res.size, _p(offs), _p(ln),
                                          _p(idv) if idv is not None else None, len(ln), _p(out)))
         return out
 

@@ -93,7 +93,7 @@ static int score(const char *qpath, const char *lpath) {
   uint64_t off0 = 0;
   uint32_t len0 = 1;
   uint8_t c0 = 0;
-  CHECK(sw_score_batch(bank, &c0, &off0, &len0, NULL, 1, &dummy) == SW_ERR_STATE, "state error");
+  CHECK(sw_score_batch(bank, &c0, 1, &off0, &len0, NULL, 1, &dummy) == SW_ERR_STATE, "state error");
   CHECK(strlen(sw_last_error(bank)) > 0, "error text");
 
   CHECK(sw_set_penalties(bank, 5, -4, -12, -4) == SW_OK, "penalties");
@@ -118,7 +118,7 @@ static int score(const char *qpath, const char *lpath) {
     lens[k] = (uint32_t)l;
     pos += l;
   }
-  CHECK(sw_score_batch(bank, res, offs, lens, ids, (size_t)n, s1) == SW_OK, sw_last_error(bank));
+  CHECK(sw_score_batch(bank, res, total, offs, lens, ids, (size_t)n, s1) == SW_OK, sw_last_error(bank));
   printf("kernel %s\n", sw_last_kernel(bank));
   /* the batch best hit (≙ max / vld_max) carries the caller's id */
   uint64_t bb_id = 0, bb_ix = 0;
@@ -167,7 +167,11 @@ static int score(const char *qpath, const char *lpath) {
   printf("best %s %d\n", ln[best_id], best);
 
   /* argument errors */
-  CHECK(sw_score_batch(bank, res, NULL, lens, NULL, (size_t)n, s1) == SW_ERR_ARG, "null offsets");
+  CHECK(sw_score_batch(bank, res, total, NULL, lens, NULL, (size_t)n, s1) == SW_ERR_ARG, "null offsets");
+  /* a target past the residues is refused before anything is read */
+  CHECK(sw_score_batch(bank, res, total - 1, offs, lens, NULL, (size_t)n, s1) == SW_ERR_ARG,
+        "target outside residues");
+  CHECK(strstr(sw_last_error(bank), "outside") != NULL, "range error text");
   uint8_t bad = 9;
   CHECK(sw_load_query(bank, 0, &bad, 1) == SW_ERR_ARG, "code outside alphabet");
   sw_bank_destroy(bank);

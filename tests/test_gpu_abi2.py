@@ -290,3 +290,23 @@ def test_cli_device_list(tmp_path, monkeypatch):
     assert one.returncode == 0 and two.returncode == 0, two.stderr
     assert one.stdout == two.stdout and one.stdout.count("score:") == 499
     assert two.stderr.startswith("best: >")
+
+
+def test_host_batch_target_outside_residues():
+    """sw_score_batch checks every target against the residue count before reading it."""
+    rng = np.random.default_rng(8)
+    q = _codes(rng, 64)
+    seqs = [_codes(rng, 100) for _ in range(5000)]
+    res, offs, lens = O.pack_residues(seqs)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        with pytest.raises(S.SwbankError) as e:
+            bank.score_batch(res[:-1], offs, lens)
+        assert e.value.status == S.ERR_ARG and "outside" in str(e.value)
+        bad = offs.copy()
+        bad[4000] = np.uint64(2**63)  # huge offset: no overflow into a small address
+        with pytest.raises(S.SwbankError):
+            bank.score_batch(res, bad, lens)
+        got = bank.score_batch(res, offs, lens)  # still usable
+    assert (got == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
