@@ -53,6 +53,7 @@ extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, s
 extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max_len,
                                     uint32_t* perm, uint32_t* perm_n, uint32_t* ident,
                                     uint32_t* scratch, hipStream_t st);
+extern "C" size_t swk_sort_scratch_bytes(void);
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
                                     uint32_t* idx, uint32_t* count, hipStream_t st);
 extern "C" size_t swk_i32_waves(size_t n, uint32_t scols, size_t budget_bytes);
@@ -1052,7 +1053,11 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   if (dsort && !use_wave && !perm && packed == SWK_PACK_BYTES && ntiles > 1 &&
       n <= 0xFFFFFFFFull && env_int("SWBANK_DSORT", 1) != 0) {
     HIPOK(b, b->dperm.reserve(n + 2));
-    HIPOK(b, b->dsort.reserve(2048));
+    const size_t sw = swk_sort_scratch_bytes() / 4;
+    if (b->dsort.cap < sw) {  // zeroed once; the sort kernels leave it zeroed
+      HIPOK(b, b->dsort.reserve(sw));
+      HIPOK(b, hipMemsetAsync(b->dsort.p, 0, sw * 4, st));
+    }
     HIPOK(b, swk_sort_lens(d_lens, n, max_len, b->dperm.p, b->dperm.p + n, b->dperm.p + n + 1,
                            b->dsort.p, st));
     perm = b->dperm.p;

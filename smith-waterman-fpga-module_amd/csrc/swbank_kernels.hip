@@ -1686,7 +1686,9 @@ __global__ void __launch_bounds__(256) score_i32(const I32Args a) {
           }
         }
       }
-      if (seg_out) __atomic_thread_fence(__ATOMIC_SEQ_CST);  // stores visible to the next strip
+      // the next strip's lane 0 reads these columns (same wave, same CU and L1): a
+      // workgroup-scope fence orders the stores before those loads (no L2 write-back)
+      if (seg_out) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
@@ -1757,10 +1759,22 @@ __device__ __forceinline__ uint32_t wave_bin_add(uint32_t* h, uint32_t bin, bool
   return active ? atomicAdd(&h[bin], 1u) : 0u;
 }
 
-__global__ void __launch_bounds__(SORT_BLOCK) sort_hist(const uint32_t* lens, size_t n,
-                                                        uint32_t max_len, uint32_t shift,
-                                                        uint32_t nb, uint32_t* hist) {
+// scratch: hist[SORT_BINS] | done[2] (block counters), zero between calls: the last block of
+// a call's last kernel zeroes them again, so no memset per call.
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Histogram of the bins, then (the last block to finish) exclusive offsets in place,
+// *perm_n = n, and *ident = 1 when at most one bin is non-empty (the caller's order is kept:
+// the scatter and the score kernel's indirection are skipped, and the hist is zeroed here).
+__global__ void __launch_bounds__(SORT_BLOCK) sort_hist_scan(const uint32_t* lens, size_t n,
+                                                             uint32_t max_len, uint32_t shift,
+                                                             uint32_t nb, uint32_t* hist,
+                                                             uint32_t* perm_n, uint32_t* ident) {
   __shared__ uint32_t h[SORT_BINS];
+  __shared__ uint32_t part[SORT_BLOCK];
+  __shared__ int last;
   for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK) h[i] = 0;
   __syncthreads();
   const size_t base = (size_t)blockIdx.x * SORT_BLOCK * SORT_ITEMS;
@@ -1770,18 +1784,22 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_hist(const uint32_t* lens, si
     (void)wave_bin_add(h, k < n ? sort_bin(lens[k], max_len, shift) : 0u, k < n);
   }
   __syncthreads();
+  // hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the bins are written by
+  // device-scope atomics, each wave waits for its own, the last block (told by the counter's
+  // returned value) reads them with sc1 loads; no L2 write-back fence (__threadfence() here
+  // cost ~35 us per call)
   for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK)
     if (h[i]) atomicAdd(&hist[i], h[i]);
-}
-
-// Exclusive offsets in place, *perm_n = n, ident[0] = 1 when at most one bin is non-empty (the
-// caller's order is already fine: the scatter and the score kernel's indirection are skipped).
-__global__ void __launch_bounds__(SORT_BLOCK) sort_scan(uint32_t* hist, uint32_t nb, size_t n,
-                                                        uint32_t* perm_n, uint32_t* ident) {
-  __shared__ uint32_t part[SORT_BLOCK];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  uint32_t* done = hist + SORT_BINS;
+  if (threadIdx.x == 0) last = atomicAdd(&done[0], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
   // each thread owns 2 consecutive bins (nb <= 2048)
   const uint32_t i0 = threadIdx.x * 2;
-  const uint32_t a = i0 < nb ? hist[i0] : 0u, c = i0 + 1 < nb ? hist[i0 + 1] : 0u;
+  const uint32_t a = i0 < nb ? ld_agent(&hist[i0]) : 0u;
+  const uint32_t c = i0 + 1 < nb ? ld_agent(&hist[i0 + 1]) : 0u;
   const int used = __syncthreads_count((a != 0) + (c != 0) > 0 ? 1 : 0) +
                    __syncthreads_count(a != 0 && c != 0 ? 1 : 0);
   part[threadIdx.x] = a + c;
@@ -1793,11 +1811,13 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_scan(uint32_t* hist, uint32_t
     __syncthreads();
   }
   const uint32_t ex = part[threadIdx.x] - (a + c);
-  if (i0 < nb) hist[i0] = ex;
-  if (i0 + 1 < nb) hist[i0 + 1] = ex + a;
+  const bool one = used <= 1;
+  if (i0 < nb) hist[i0] = one ? 0u : ex;
+  if (i0 + 1 < nb) hist[i0 + 1] = one ? 0u : ex + a;
   if (threadIdx.x == 0) {
     *perm_n = (uint32_t)n;
-    *ident = used <= 1 ? 1u : 0u;
+    *ident = one ? 1u : 0u;
+    done[0] = 0;
   }
 }
 
@@ -1807,6 +1827,7 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_scatter(const uint32_t* lens,
                                                            uint32_t* perm, const uint32_t* ident) {
   if (__builtin_amdgcn_readfirstlane(*ident)) return;  // one length bin: order unchanged
   __shared__ uint32_t h[SORT_BINS];
+  __shared__ int last;
   for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK) h[i] = 0;
   __syncthreads();
   const size_t base = (size_t)blockIdx.x * SORT_BLOCK * SORT_ITEMS;
@@ -1824,13 +1845,25 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_scatter(const uint32_t* lens,
 #pragma unroll
   for (int it = 0; it < SORT_ITEMS; ++it) {
     const size_t k = base + (size_t)it * SORT_BLOCK + threadIdx.x;
-    if (k < n) perm[h[bin[it]] + slot[it]] = (uint32_t)k;
+    const uint32_t pos = h[bin[it]] + slot[it];
+    if (k < n && pos < n) perm[pos] = (uint32_t)k;
   }
+  // the last block zeroes the offsets and the counters for the next call (every block's
+  // offset atomics returned before its counter add; the zeros reach the next call's kernels
+  // through the kernel boundary)
+  __syncthreads();
+  uint32_t* done = offs + SORT_BINS;
+  if (threadIdx.x == 0) last = atomicAdd(&done[1], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK) offs[i] = 0;
+  if (threadIdx.x == 0) done[1] = 0;
 }
 }  // namespace swk
 
 // perm[0, n) <- target numbers longest first, *perm_n <- n, *ident <- 1 when the lengths
-// share one bin (perm then left unwritten: visit in input order); scratch: SORT_BINS words.
+// share one bin (perm then left unwritten: visit in input order); scratch:
+// swk_sort_scratch_bytes(), zero on entry and on return.
 extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max_len,
                                     uint32_t* perm, uint32_t* perm_n, uint32_t* ident,
                                     uint32_t* scratch, hipStream_t st) {
@@ -1838,15 +1871,14 @@ extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max
   uint32_t shift = 0;
   while ((max_len >> shift) >= (uint32_t)swk::SORT_BINS) ++shift;
   const uint32_t nb = (max_len >> shift) + 1;
-  hipError_t e = hipMemsetAsync(scratch, 0, nb * sizeof(uint32_t), st);
-  if (e != hipSuccess) return e;
   const unsigned blocks =
       (unsigned)((n + swk::SORT_BLOCK * swk::SORT_ITEMS - 1) / (swk::SORT_BLOCK * swk::SORT_ITEMS));
-  hipLaunchKernelGGL(swk::sort_hist, dim3(blocks), dim3(swk::SORT_BLOCK), 0, st, lens, n, max_len,
-                     shift, nb, scratch);
-  hipLaunchKernelGGL(swk::sort_scan, dim3(1), dim3(swk::SORT_BLOCK), 0, st, scratch, nb, n, perm_n,
-                     ident);
+  hipLaunchKernelGGL(swk::sort_hist_scan, dim3(blocks), dim3(swk::SORT_BLOCK), 0, st, lens, n,
+                     max_len, shift, nb, scratch, perm_n, ident);
   hipLaunchKernelGGL(swk::sort_scatter, dim3(blocks), dim3(swk::SORT_BLOCK), 0, st, lens, n,
                      max_len, shift, nb, scratch, perm, ident);
   return hipGetLastError();
 }
+
+// Bytes of sort scratch (zeroed once at allocation; the kernels leave it zeroed).
+extern "C" size_t swk_sort_scratch_bytes(void) { return (swk::SORT_BINS + 2) * sizeof(uint32_t); }

@@ -158,7 +158,7 @@ def test_batch_best_host_device_and_records():
 
 
 # ---- ragged device batches: on-device length sort -------------------------------------------
-@pytest.mark.parametrize("lo,hi", [(64, 128), (1, 150), (0, 1000), (100, 101)])
+@pytest.mark.parametrize("lo,hi", [(64, 128), (1, 150), (0, 1000), (100, 101), (128, 128)])
 def test_device_sort_ragged(lo, hi, monkeypatch):
     torch = pytest.importorskip("torch")
     rng = np.random.default_rng(lo * 1000 + hi)
