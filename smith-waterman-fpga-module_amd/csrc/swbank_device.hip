@@ -36,7 +36,8 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
                                       const uint64_t* offs, const uint32_t* lens, size_t n,
                                       const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
-                                      int packed, hipStream_t st);
+                                      int packed, const uint32_t* fb_qtab, uint32_t fb_nv,
+                                      uint32_t fb_PS, int32_t fb_thresh, hipStream_t st);
 extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh, int f16,
                                        const uint8_t* res, const uint64_t* offs,
                                        const uint32_t* lens, size_t n, const uint32_t* qtab,
@@ -1015,6 +1016,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   const char* arith = opt16 ? "f16+u16-rescore" : use_f16 ? "f16" : "u16";
   // the f16 pass of the tile kernel reads the letter-pair table when the query has one
   const bool use_pair = use_f16 && b->pair_bytes != 0 && env_int("SWBANK_PAIR", 1) != 0;
+  bool wave_fb = false;  // the wave kernel re-scores its own flagged pairs
   if (use_wave) {
     snprintf(b->last_kernel, sizeof(b->last_kernel), "wave %s%s K=%d segs=%d", arith,
              b->prof ? "-profile" : "", b->wK, b->wsegs);
@@ -1028,6 +1030,9 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
       HIPOK(b, b->edge[0].reserve(words));
       HIPOK(b, b->edge[1].reserve(words));
     }
+    // optimistic f16 with one query segment: the wave re-scores a flagged pair in u16 itself
+    // (no flag kernel, no re-score launches)
+    wave_fb = opt16 && b->wsegs == 1 && env_int("SWBANK_WAVE_FB", 1) != 0;
     for (size_t p0 = 0; p0 < n; p0 += wspan) {
       const size_t np = std::min(wspan, n - p0);
       for (int sg = 0; sg < b->wsegs; ++sg) {
@@ -1040,7 +1045,8 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                      use_f16 ? b->wtab16.p + sg * b->wseg_words16 : b->wtab.p + sg * b->wseg_words,
                      use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
                      use_f16 && b->prof ? b->wPS16 : b->wPS, b->pad, d_scores + p0,
-                     (int)packed, st));
+                     (int)packed, wave_fb ? b->wtab.p : nullptr, b->nv, b->wPS,
+                     2048 - std::max(0, b->smax), st));
       }
     }
   } else {
@@ -1081,7 +1087,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   }
   // pass 0: every pair with the tile kernel (unless the wave kernel ran); pass 1 (optimistic
   // f16 only): the pairs scoring above 2048 - max(s), re-scored in u16 by the tile kernel
-  for (int pass = use_wave ? 1 : 0; pass < (opt16 ? 2 : 1); ++pass) {
+  for (int pass = use_wave ? 1 : 0; pass < (opt16 && !wave_fb ? 2 : 1); ++pass) {
     const bool f16 = use_f16 && pass == 0;
     if (pass == 1) {
       HIPOK(b, b->fb_idx.reserve(n));

@@ -534,6 +534,12 @@ struct ScoreArgs {
   uint32_t pS1, pS2;
   // f16 kernels: f16_pair(-(o+e)), f16_pair(-e), f16_pair(-o)
   uint32_t f16_noe, f16_ne, f16_no;
+  // wave kernel, optimistic f16 (single query segment): a pair scoring above fb_thresh is
+  // re-scored at once in u16 by the same wave, from the u16 table fb_qtab in HBM (LUT words
+  // or the profile, row stride fb_PS) with fb_nv; fb_qtab == nullptr: no fallback
+  const uint32_t* fb_qtab;
+  uint32_t fb_nv, fb_PS;
+  int32_t fb_thresh;
 };
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -1140,24 +1146,17 @@ __device__ __forceinline__ uint32_t dpp_shr1_zero(uint32_t v) {  // lane 0 reads
   return __builtin_amdgcn_mov_dpp(v, 0x138 /* wave_shr:1 */, 0xF, 0xF, true);
 }
 
-// qtab (wave layout): LUT: 64*K row words | PROF: (pad+1) x PS bytes, PS = 64*K.
+// One pair (targets 2*pair, 2*pair+1; tA < n) against the query (segment): returns the two
+// best scores (every lane), and writes the segment's bottom row when a.edge_out is set.
+// qtab (wave layout): LUT: 64*K row words | PROF: (pad+1) x PS bytes, PS = 64*K (u16) or
+// 128*K (f16).  prof: the profile (PROF), in LDS for the main pass or in HBM for the u16
+// re-score of an optimistic f16 pass (the compiler emits ds_ or flat loads per call site).
 template <int K, bool COL0, bool PROF, bool GOTOH, bool F16>
-__global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
-  const int lane = threadIdx.x & 63;
-  if constexpr (PROF) {
-    const uint32_t words = (a.pad + 1) * a.PS / 16;
-    const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
-    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
-      reinterpret_cast<uint4*>(prof)[i] = src[i];
-    __syncthreads();
-  }
-  const size_t pair = (size_t)blockIdx.x * (blockDim.x >> 6) +
-                      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* prof,
+                                           const uint32_t* qtab, uint32_t nv, uint32_t PSb,
+                                           size_t pair, int lane) {
   const size_t tA = 2 * pair, tB = tA + 1;
   const size_t n = a.n;
-  if (tA >= n) return;  // whole wave
   const bool packed = a.packed != SWK_PACK_BYTES, rec = a.packed == SWK_PACK_RECORDS;
   const bool nib = a.packed == SWK_PACK_NIBBLE;
   const uint32_t LA = rec ? record_len(a.res + tA * SWB_RECORD) : a.lens[tA];
@@ -1177,7 +1176,6 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
   // f16 profile: the code word carries the LDS byte offsets of both letters' profile rows
   // plus the lane's own row offset (2K bytes per lane, added per DPP hop), so the lane's two
   // addresses are one mask / shift each; the host keeps (pad + 1) x PS <= 64 KiB
-  const uint32_t PSb = a.PS;
   const uint32_t hop = (2u * K) | (2u * K) << 16;
   const auto code_word = [&](uint32_t x, uint32_t y) -> uint32_t {
     if constexpr (F16 && PROF) return x * PSb | (y * PSb) << 16;
@@ -1196,9 +1194,8 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
   uint32_t lut[PROF ? 1 : K];
   if constexpr (!PROF) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) lut[k] = a.qtab[lane * K + k];
+    for (int k = 0; k < K; ++k) lut[k] = qtab[lane * K + k];
   }
-  const uint32_t nv = a.nv;
   const uint8_t* prow = prof + lane * K;       // this lane's rows in every profile letter row
 
   u16x2 Hl[K], Xl[K];
@@ -1264,7 +1261,7 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
       const bool z = COL0 && t == lane;
       if constexpr (PROF) {
         ProfLookupK16<K> lk;
-        const uint8_t* lds = reinterpret_cast<const uint8_t*>(smem);
+        const uint8_t* lds = prof;
         const uint32_t olo = let & 0xFFFFu, ohi = let >> 16;
         if constexpr (K == 4) {
           const uint2 x = *reinterpret_cast<const uint2*>(lds + olo);
@@ -1296,15 +1293,15 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
       ProfLookupK<K> lk;
       const uint32_t blo = let & 0xFFu, bhi = (let >> 16) & 0xFFu;
       if constexpr (K == 4) {
-        lk.lo[0] = *reinterpret_cast<const uint32_t*>(prow + __umul24(blo, a.PS));
-        lk.hi[0] = *reinterpret_cast<const uint32_t*>(prow + __umul24(bhi, a.PS));
+        lk.lo[0] = *reinterpret_cast<const uint32_t*>(prow + __umul24(blo, PSb));
+        lk.hi[0] = *reinterpret_cast<const uint32_t*>(prow + __umul24(bhi, PSb));
       } else if constexpr (K == 8) {
-        const uint2 x = *reinterpret_cast<const uint2*>(prow + __umul24(blo, a.PS));
-        const uint2 y = *reinterpret_cast<const uint2*>(prow + __umul24(bhi, a.PS));
+        const uint2 x = *reinterpret_cast<const uint2*>(prow + __umul24(blo, PSb));
+        const uint2 y = *reinterpret_cast<const uint2*>(prow + __umul24(bhi, PSb));
         lk.lo[0] = x.x; lk.lo[1] = x.y; lk.hi[0] = y.x; lk.hi[1] = y.y;
       } else {
-        const uint4 x = *reinterpret_cast<const uint4*>(prow + __umul24(blo, a.PS));
-        const uint4 y = *reinterpret_cast<const uint4*>(prow + __umul24(bhi, a.PS));
+        const uint4 x = *reinterpret_cast<const uint4*>(prow + __umul24(blo, PSb));
+        const uint4 y = *reinterpret_cast<const uint4*>(prow + __umul24(bhi, PSb));
         lk.lo[0] = x.x; lk.lo[1] = x.y; lk.lo[2] = x.z; lk.lo[3] = x.w;
         lk.hi[0] = y.x; lk.hi[1] = y.y; lk.hi[2] = y.z; lk.hi[3] = y.w;
       }
@@ -1356,8 +1353,36 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
     bx = max(bx, (uint32_t)__shfl_xor((int)bx, off));
     by = max(by, (uint32_t)__shfl_xor((int)by, off));
   }
+  return make_uint2(bx, by);
+}
+
+template <int K, bool COL0, bool PROF, bool GOTOH, bool F16>
+__global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
+  const int lane = threadIdx.x & 63;
+  if constexpr (PROF) {
+    const uint32_t words = (a.pad + 1) * a.PS / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+      reinterpret_cast<uint4*>(prof)[i] = src[i];
+    __syncthreads();
+  }
+  const size_t pair = (size_t)blockIdx.x * (blockDim.x >> 6) +
+                      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t tA = 2 * pair, tB = tA + 1;
+  const size_t n = a.n;
+  if (tA >= n) return;  // whole wave
+  uint2 b = wave_pair<K, COL0, PROF, GOTOH, F16>(a, prof, a.qtab, a.nv, a.PS, pair, lane);
+  if constexpr (F16) {
+    // optimistic f16: a pair above 2048 - max(s) may have rounded; re-score it in u16 now
+    // (the profile from HBM: rare, and no LDS for a second table)
+    if (a.fb_qtab && (int32_t)max(b.x, b.y) > a.fb_thresh)
+      b = wave_pair<K, COL0, PROF, GOTOH, false>(a, reinterpret_cast<const uint8_t*>(a.fb_qtab),
+                                                 a.fb_qtab, a.fb_nv, a.fb_PS, pair, lane);
+  }
   if (lane == 0) {
-    int32_t sa = (int32_t)bx, sb = (int32_t)by;
+    int32_t sa = (int32_t)b.x, sb = (int32_t)b.y;
     if (a.accum) {  // best over the previous query segments
       sa = max(sa, a.scores[tA]);
       if (tB < n) sb = max(sb, a.scores[tB]);
@@ -1428,7 +1453,7 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                          static_cast<uint2*>(edge_out), ecols, (uint32_t)accum, (uint32_t)packed,
                          idx, nidx, idx_base, ident, pS1, pS2,
                          swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
-                         swk::f16_pair(-(int)O)};
+                         swk::f16_pair(-(int)O), nullptr, 0u, 0u, 0};
   const uint32_t prof_bytes = (pad + 1) * PS;
   if (pair) {  // PS = pair-table bytes
     if (R == 32 && f16 && !prof && !gotoh && !col0)
@@ -1521,13 +1546,14 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
                                       const uint64_t* offs, const uint32_t* lens, size_t n,
                                       const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
-                                      int packed, hipStream_t st) {
+                                      int packed, const uint32_t* fb_qtab, uint32_t fb_nv,
+                                      uint32_t fb_PS, int32_t fb_thresh, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
                          static_cast<const uint2*>(edge_in), static_cast<uint2*>(edge_out), ecols,
                          (uint32_t)accum, (uint32_t)packed, nullptr, nullptr, 0u, nullptr, 0u, 0u,
                          swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
-                         swk::f16_pair(-(int)O)};
+                         swk::f16_pair(-(int)O), fb_qtab, fb_nv, fb_PS, fb_thresh};
   const uint32_t prof_bytes = (pad + 1) * PS;
 #define SWK_WCASE(KK, C0, PF, GT)                                                         \
   if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                                 \
