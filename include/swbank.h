@@ -183,8 +183,9 @@ sw_status sw_best_hit_device(sw_bank *bank, const int32_t *d_scores, const uint6
  *      _DEBUGGING_ "calculation #N completed, runtime: C cycles") ------------------------- */
 /* When enabled, every launch is bracketed by hipEvents on the stream it runs on. */
 sw_status sw_bank_set_timing(sw_bank *bank, int32_t enable);
-/* Synchronises on the recorded events and returns the launches and the summed device
- * milliseconds of the feeder (pack) and score kernels since the previous call. */
+/* Synchronises on the recorded events and returns the launches and the summed milliseconds of
+ * the feeder (pack: host gather / packing time of the host-buffer calls) and of the score
+ * kernels (device time) since the previous call. */
 sw_status sw_bank_timing(sw_bank *bank, uint64_t *launches, double *pack_ms, double *score_ms);
 /* Which kernel the last score call ran, e.g. "tile f16 R=32 W=4 segs=1 grid=998" or
  * "wave u16 K=4" (empty before the first call).  No reference counterpart: the RTL has one

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--qlen", type=int, default=128)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--ragged", action="store_true", help="lengths uniform in [L/2, L]")
+    ap.add_argument("--no-records", action="store_true")
     ap.add_argument("--n-frac", type=float, default=0.0,
                     help="fraction of residues set to N (the feeder then sends 4-bit chunks)")
     args = ap.parse_args()
@@ -44,15 +45,23 @@ def main():
         bank.load_query(q)
         ref = bank.score_batch(res, offs, lens)  # warm-up (allocations, pinned staging)
         ts = []
+        bank.timing()
+        bank.set_timing(True)
         for _ in range(args.iters):
             t0 = time.perf_counter()
             got = bank.score_batch(res, offs, lens)
             ts.append(time.perf_counter() - t0)
+        bank.set_timing(False)
+        launches, pack_ms, score_ms = bank.timing()
         assert np.array_equal(got, ref)
         out["host_api_ms"] = round(min(ts) * 1e3, 2)
+        out["host_api_mean_ms"] = round(sum(ts) / len(ts) * 1e3, 2)
+        out["feeder_gather_ms_per_call"] = round(pack_ms / args.iters, 3)
+        out["score_kernel_ms_per_call"] = round(score_ms / args.iters, 3)
+        out["launches_per_call"] = launches / args.iters
         out["host_api_gcups"] = round(cells / min(ts) / 1e9, 1)
         out["kernel"] = bank.last_kernel()
-        if not args.ragged and not args.n_frac and L <= S.RECORD_MAX_BASES:
+        if not args.no_records and not args.ragged and not args.n_frac and L <= S.RECORD_MAX_BASES:
             recs = S.make_records(res.reshape(n, L))
             bank.score_records(recs)
             ts = []

@@ -51,6 +51,10 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
                                    hipStream_t st);
+extern "C" hipError_t swk_best_part(const int32_t* scores, size_t n, size_t base,
+                                    unsigned long long* key, hipStream_t st);
+extern "C" hipError_t swk_best_finalize(const unsigned long long* key, const uint64_t* ids,
+                                        uint64_t* out, uint64_t* out_index, hipStream_t st);
 extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max_len,
                                     uint32_t* perm, uint32_t* perm_n, uint32_t* ident,
                                     uint32_t* scratch, hipStream_t st);
@@ -245,6 +249,8 @@ struct sw_bank {
   hipStream_t copy_stream = nullptr;
   hipEvent_t h2d_done[NSLOT] = {}, kern_done[NSLOT] = {};
   PinBuf hslot[NSLOT], hscores;
+  std::vector<hipEvent_t> out_ev;  // per chunk: its scores are back in hscores
+  double host_pack_ms = 0;         // feeder gather time of host calls (with timing on)
   DevBuf<uint8_t> dslot[NSLOT];
   std::unique_ptr<HostPool> pool;
 
@@ -505,6 +511,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->edge[0].release();
   b->edge[1].release();
   if (b->copy_stream) (void)hipStreamSynchronize(b->copy_stream);
+  for (hipEvent_t e : b->out_ev) (void)hipEventDestroy(e);
   for (int i = 0; i < sw_bank::NSLOT; ++i) {
     b->hslot[i].release();
     b->dslot[i].release();
@@ -1221,10 +1228,14 @@ extern "C" sw_status sw_batch_best(sw_bank* b, uint64_t* best_id, int32_t* best_
 // (code validation fused into the copy) while chunk i-1 crosses PCIe on the copy stream and
 // chunk i-2 is scored on the bank stream.
 namespace {
+// Feeder threads: SWBANK_HOST_THREADS, else the process's CPU share when OMP_NUM_THREADS
+// states it (capped at 16), else 8 (and never more than the machine has).
 unsigned host_threads() {
   const int t = env_int("SWBANK_HOST_THREADS", 0);
   if (t > 0) return (unsigned)std::min(t, 64);
-  return std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int omp = env_int("OMP_NUM_THREADS", 0);
+  return std::min(hw, omp > 0 ? (unsigned)std::min(omp, 16) : 8u);
 }
 
 // f(lo, hi) over [0, n) split into the pool's parts (inline below 2048 items)
@@ -1335,13 +1346,15 @@ struct Chunk {
 // Runs the feeder: gather(slot, chunk) fills the host slot and returns how many leading bytes
 // of it to copy (0: bad input, message set); they go to the device on the copy stream, score(dslot, chunk, d_scores) launches the
 // kernel on the bank stream; the scores come back to the pinned hscores in input order.
-// to_host: scores back to the pinned hscores (and the batch best hit {id = index, score,
-// index} after them, at best_at(n)) with the stream synchronised; else they stay in b->scores
-// on the device, enqueued on b->stream (a multi-device bank gathers them).
+// out != nullptr: every chunk's scores go back to the pinned hscores right after its kernel
+// (and the batch best hit {id = index, score, index} after them, at best_at(n), folded chunk
+// by chunk), and are copied into out in input order as they land, while later chunks still
+// score; out == nullptr: they stay in b->scores on the device, enqueued on b->stream (a
+// multi-device bank gathers them).
 static inline size_t best_at(size_t n) { return (n * 4 + 7) / 8 * 8; }
 template <class GatherF, class ScoreF>
 static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, GatherF gather,
-                      ScoreF score, bool to_host) {
+                      ScoreF score, int32_t* out) {
   sw_status st = feeder_init(b);
   if (st != SW_OK) return st;
   size_t slot_bytes = 0;
@@ -1351,38 +1364,59 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     HIPOK(b, b->dslot[i].reserve(slot_bytes));
   }
   HIPOK(b, b->scores.reserve(n));
-  if (to_host) HIPOK(b, b->hscores.reserve(best_at(n) + 24));
+  if (out) {
+    HIPOK(b, b->hscores.reserve(best_at(n) + 24));
+    HIPOK(b, b->best_key.reserve(1));
+    HIPOK(b, b->best_dev.reserve(3));
+    HIPOK(b, hipMemsetAsync(b->best_key.p, 0, sizeof(unsigned long long), b->stream));
+    while (b->out_ev.size() < chunks.size()) {
+      hipEvent_t e;
+      HIPOK(b, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      b->out_ev.push_back(e);
+    }
+  }
+  const auto fail_sync = [&](sw_status s) {
+    (void)hipStreamSynchronize(b->stream);
+    (void)hipStreamSynchronize(b->copy_stream);
+    return s;
+  };
   for (size_t i = 0; i < chunks.size(); ++i) {
     const int s = (int)(i % sw_bank::NSLOT);
     const Chunk& c = chunks[i];
     if (i >= (size_t)sw_bank::NSLOT) HIPOK(b, hipEventSynchronize(b->h2d_done[s]));
+    const auto t0 = std::chrono::steady_clock::now();
     const size_t bytes = gather(b->hslot[s].p, c);
-    if (bytes == 0) {
-      (void)hipStreamSynchronize(b->stream);
-      (void)hipStreamSynchronize(b->copy_stream);
-      return SW_ERR_ARG;
-    }
+    if (b->timing)
+      b->host_pack_ms +=
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (bytes == 0) return fail_sync(SW_ERR_ARG);
     if (i >= (size_t)sw_bank::NSLOT)
       HIPOK(b, hipStreamWaitEvent(b->copy_stream, b->kern_done[s], 0));
     HIPOK(b, hipMemcpyAsync(b->dslot[s].p, b->hslot[s].p, bytes, hipMemcpyHostToDevice,
                             b->copy_stream));
     HIPOK(b, hipEventRecord(b->h2d_done[s], b->copy_stream));
     HIPOK(b, hipStreamWaitEvent(b->stream, b->h2d_done[s], 0));
-    if ((st = score(b->dslot[s].p, c, b->scores.p + c.c0)) != SW_OK) {
-      (void)hipStreamSynchronize(b->stream);
-      (void)hipStreamSynchronize(b->copy_stream);
-      return st;
-    }
+    if ((st = score(b->dslot[s].p, c, b->scores.p + c.c0)) != SW_OK) return fail_sync(st);
     HIPOK(b, hipEventRecord(b->kern_done[s], b->stream));
+    if (out) {
+      HIPOK(b, swk_best_part(b->scores.p + c.c0, c.c1 - c.c0, c.c0, b->best_key.p, b->stream));
+      HIPOK(b, hipMemcpyAsync(b->hscores.p + c.c0 * 4, b->scores.p + c.c0, (c.c1 - c.c0) * 4,
+                              hipMemcpyDeviceToHost, b->stream));
+      HIPOK(b, hipEventRecord(b->out_ev[i], b->stream));
+    }
   }
-  if (!to_host) return SW_OK;
-  HIPOK(b, b->best_key.reserve(1));
-  HIPOK(b, b->best_dev.reserve(3));
-  HIPOK(b, swk_best_hit(b->scores.p, nullptr, n, b->best_key.p, b->best_dev.p, b->best_dev.p + 2,
-                        b->stream));
-  HIPOK(b, hipMemcpyAsync(b->hscores.p, b->scores.p, n * 4, hipMemcpyDeviceToHost, b->stream));
+  if (!out) return SW_OK;
+  HIPOK(b, swk_best_finalize(b->best_key.p, nullptr, b->best_dev.p, b->best_dev.p + 2, b->stream));
   HIPOK(b, hipMemcpyAsync(b->hscores.p + best_at(n), b->best_dev.p, 24, hipMemcpyDeviceToHost,
                           b->stream));
+  const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
+  for (size_t i = 0; i < chunks.size(); ++i) {  // scores into the caller's buffer as they land
+    const Chunk& c = chunks[i];
+    HIPOK(b, hipEventSynchronize(b->out_ev[i]));
+    parallel_for(*b->pool, c.c1 - c.c0, [&](size_t lo, size_t hi) {
+      std::memcpy(out + c.c0 + lo, hs + c.c0 + lo, (hi - lo) * 4);
+    });
+  }
   HIPOK(b, hipStreamSynchronize(b->stream));
   return SW_OK;
 }
@@ -1472,7 +1506,7 @@ static inline uint32_t pack_4bit(const uint8_t* src, uint32_t l, uint8_t* dst) {
 // The host-buffer batch through the feeder (n >= 1, buffers checked by the caller).
 static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                             const uint64_t* offsets, const uint32_t* lens, size_t n,
-                            bool to_host) {
+                            int32_t* out) {
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
   if ((st = feeder_init(b)) != SW_OK) return st;
@@ -1691,7 +1725,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.perm_at) : nullptr,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr);
   };
-  return feed(b, n, chunks, gather, score, to_host);
+  return feed(b, n, chunks, gather, score, out);
 }
 
 // ---- CAPI record path (row f2): sequence_t arrays as the reference host builds them ------
@@ -1734,7 +1768,7 @@ extern "C" sw_status sw_score_records_device(sw_bank* b, const void* d_records, 
 
 // Host records through the feeder (n >= 1, buffers checked by the caller); lengths are
 // checked while gathering.
-static sw_status records_feed(sw_bank* b, const uint8_t* recs, size_t n, bool to_host) {
+static sw_status records_feed(sw_bank* b, const uint8_t* recs, size_t n, int32_t* out) {
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
   if ((st = feeder_init(b)) != SW_OK) return st;
@@ -1797,7 +1831,7 @@ static sw_status records_feed(sw_bank* b, const uint8_t* recs, size_t n, bool to
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.perm_at) : nullptr,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr);
   };
-  return feed(b, n, chunks, gather, score, to_host);
+  return feed(b, n, chunks, gather, score, out);
 }
 
 // ---- multi-device banks (≙ MODULES ScoringModules behind the PrioEncoder,
@@ -1916,7 +1950,7 @@ static sw_status multi_batch(sw_bank* b, const uint8_t* residues, size_t nres,
     }
   });
   sw_status st = multi_gather(b, cnt, [&](unsigned d) {
-    return batch_feed(b->kids[d], residues, nres, offs[d].data(), lns[d].data(), cnt[d], false);
+    return batch_feed(b->kids[d], residues, nres, offs[d].data(), lns[d].data(), cnt[d], nullptr);
   });
   if (st != SW_OK) return st;
   const size_t cmax = cnt[0];
@@ -1940,7 +1974,7 @@ static sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_
     cnt[d] = n * (d + 1) / D - first[d];
   }
   sw_status st = multi_gather(b, cnt, [&](unsigned d) {
-    return records_feed(b->kids[d], recs + first[d] * SWB_RECORD, cnt[d], false);
+    return records_feed(b->kids[d], recs + first[d] * SWB_RECORD, cnt[d], nullptr);
   });
   if (st != SW_OK) return st;
   const size_t cmax = *std::max_element(cnt.begin(), cnt.end());
@@ -1965,12 +1999,8 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, size_t 
     if (st == SW_OK && ids) b->best_id = ids[b->best_index];
     return st;
   }
-  const sw_status st = batch_feed(b, residues, residues_len, offsets, lens, n, true);
+  const sw_status st = batch_feed(b, residues, residues_len, offsets, lens, n, scores_out);
   if (st != SW_OK) return st;
-  const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
-  parallel_for(*b->pool, n, [&](size_t lo, size_t hi) {
-    std::memcpy(scores_out + lo, hs + lo, (hi - lo) * 4);
-  });
   take_best(b, n);
   if (ids) b->best_id = ids[b->best_index];
   return SW_OK;
@@ -1990,14 +2020,8 @@ extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
   if (b->is_multi()) {
     st = multi_records(b, recs, n, scores_out);
   } else {
-    st = records_feed(b, recs, n, true);
-    if (st == SW_OK) {
-      const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
-      parallel_for(*b->pool, n, [&](size_t lo, size_t hi) {
-        std::memcpy(scores_out + lo, hs + lo, (hi - lo) * 4);
-      });
-      take_best(b, n);
-    }
+    st = records_feed(b, recs, n, scores_out);
+    if (st == SW_OK) take_best(b, n);
   }
   if (st == SW_OK) {  // the record's own ID (sequence_t.ID, aligner_Header.h:20)
     uint32_t id;
@@ -2051,6 +2075,8 @@ extern "C" sw_status sw_bank_timing(sw_bank* b, uint64_t* launches, double* pack
     (void)hipEventDestroy(ev.c);
   }
   b->events.clear();
+  p += b->host_pack_ms;  // host calls: the feeder's gather / pack time on the host
+  b->host_pack_ms = 0;
   if (launches) *launches = n;
   if (pack_ms) *pack_ms = p;
   if (score_ms) *score_ms = s;

@@ -1483,13 +1483,13 @@ namespace swk {
 // Bank best hit on the device (≙ ScoreBank_v2 max/vld_max): key = biased score << 32 |
 // (2^32 - 1 - index), so one 64-bit max picks the highest score and, among equals, the
 // lowest index.  Block-level max in LDS, one atomicMax per block.
-__global__ void __launch_bounds__(256) best_kernel(const int32_t* scores, size_t n,
+__global__ void __launch_bounds__(256) best_kernel(const int32_t* scores, size_t n, size_t base,
                                                    unsigned long long* key) {
   __shared__ unsigned long long red[256];
   unsigned long long m = 0;
   for (size_t k = (size_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (size_t)gridDim.x * 256) {
     const unsigned long long v = ((unsigned long long)((uint32_t)scores[k] ^ 0x80000000u) << 32) |
-                                 (0xFFFFFFFFull - (uint32_t)k);
+                                 (0xFFFFFFFFull - (uint32_t)(base + k));
     m = v > m ? v : m;
   }
   red[threadIdx.x] = m;
@@ -1511,18 +1511,35 @@ __global__ void best_finalize(const unsigned long long* key, const uint64_t* ids
 }
 }  // namespace swk
 
+// Fold scores[0, n) (batch positions base + k) into the 64-bit best key (zeroed by the caller
+// before the first part); few blocks, so the contended atomicMax stays cheap (2048 blocks cost
+// ~25 us on 1 M scores, 256 about 3).
+extern "C" hipError_t swk_best_part(const int32_t* scores, size_t n, size_t base,
+                                    unsigned long long* key, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>((n + 2047) / 2048, 256);
+  hipLaunchKernelGGL(swk::best_kernel, dim3((unsigned)blocks), dim3(256), 0, st, scores, n, base,
+                     key);
+  return hipGetLastError();
+}
+
+// out[0] = best id (ids ? ids[index] : index), out[1] = best score (sign-extended), *out_index
+// (optional) = its index, from the key.
+extern "C" hipError_t swk_best_finalize(const unsigned long long* key, const uint64_t* ids,
+                                        uint64_t* out, uint64_t* out_index, hipStream_t st) {
+  hipLaunchKernelGGL(swk::best_finalize, dim3(1), dim3(1), 0, st, key, ids, out, out_index);
+  return hipGetLastError();
+}
+
 // out[0] = best id, out[1] = best score (sign-extended), *out_index (optional) = its index;
 // key: 8 bytes of device scratch.
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
                                    hipStream_t st) {
   hipError_t e = hipMemsetAsync(key, 0, sizeof(*key), st);
-  if (e != hipSuccess) return e;
-  const size_t blocks = std::min<size_t>((n + 255) / 256, 2048);
-  hipLaunchKernelGGL(swk::best_kernel, dim3((unsigned)std::max<size_t>(blocks, 1)), dim3(256), 0,
-                     st, scores, n, key);
-  hipLaunchKernelGGL(swk::best_finalize, dim3(1), dim3(1), 0, st, key, ids, out, out_index);
-  return hipGetLastError();
+  if (e == hipSuccess) e = swk_best_part(scores, n, 0, key, st);
+  if (e == hipSuccess) e = swk_best_finalize(key, ids, out, out_index, st);
+  return e;
 }
 
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
