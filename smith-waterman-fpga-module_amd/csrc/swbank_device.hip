@@ -250,6 +250,7 @@ struct sw_bank {
   hipEvent_t h2d_done[NSLOT] = {}, kern_done[NSLOT] = {};
   PinBuf hslot[NSLOT], hscores;
   std::vector<hipEvent_t> out_ev;  // per chunk: its scores are back in hscores
+  hipStream_t out_stream = nullptr;  // scores back to the host, beside the next chunk's kernel
   double host_pack_ms = 0;         // feeder gather time of host calls (with timing on)
   DevBuf<uint8_t> dslot[NSLOT];
   std::unique_ptr<HostPool> pool;
@@ -511,6 +512,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->edge[0].release();
   b->edge[1].release();
   if (b->copy_stream) (void)hipStreamSynchronize(b->copy_stream);
+  if (b->out_stream) (void)hipStreamSynchronize(b->out_stream);
   for (hipEvent_t e : b->out_ev) (void)hipEventDestroy(e);
   for (int i = 0; i < sw_bank::NSLOT; ++i) {
     b->hslot[i].release();
@@ -521,6 +523,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->hscores.release();
   b->pool.reset();
   if (b->copy_stream) (void)hipStreamDestroy(b->copy_stream);
+  if (b->out_stream) (void)hipStreamDestroy(b->out_stream);
   b->res.release();
   b->offs.release();
   b->lens.release();
@@ -1331,6 +1334,7 @@ static sw_status feeder_init(sw_bank* b) {
   if (!b->pool) return fail(b, SW_ERR_NOMEM, "host worker pool");
   if (b->copy_stream) return SW_OK;
   HIPOK(b, hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
+  HIPOK(b, hipStreamCreateWithFlags(&b->out_stream, hipStreamNonBlocking));
   for (int i = 0; i < sw_bank::NSLOT; ++i) {
     HIPOK(b, hipEventCreateWithFlags(&b->h2d_done[i], hipEventDisableTiming));
     HIPOK(b, hipEventCreateWithFlags(&b->kern_done[i], hipEventDisableTiming));
@@ -1346,12 +1350,11 @@ struct Chunk {
 // Runs the feeder: gather(slot, chunk) fills the host slot and returns how many leading bytes
 // of it to copy (0: bad input, message set); they go to the device on the copy stream, score(dslot, chunk, d_scores) launches the
 // kernel on the bank stream; the scores come back to the pinned hscores in input order.
-// out != nullptr: every chunk's scores go back to the pinned hscores right after its kernel
-// (and the batch best hit {id = index, score, index} after them, at best_at(n), folded chunk
-// by chunk), and are copied into out in input order as they land, while later chunks still
-// score; out == nullptr: they stay in b->scores on the device, enqueued on b->stream (a
+// out != nullptr: every chunk's scores go back to the pinned hscores on out_stream right after
+// its kernel (beside the next chunk's kernel on the bank stream) and are copied into out in
+// input order as they land, the batch best hit (lowest index of the maximum) tracked in the same
+// pass; out == nullptr: they stay in b->scores on the device, enqueued on b->stream (a
 // multi-device bank gathers them).
-static inline size_t best_at(size_t n) { return (n * 4 + 7) / 8 * 8; }
 template <class GatherF, class ScoreF>
 static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, GatherF gather,
                       ScoreF score, int32_t* out) {
@@ -1365,10 +1368,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   }
   HIPOK(b, b->scores.reserve(n));
   if (out) {
-    HIPOK(b, b->hscores.reserve(best_at(n) + 24));
-    HIPOK(b, b->best_key.reserve(1));
-    HIPOK(b, b->best_dev.reserve(3));
-    HIPOK(b, hipMemsetAsync(b->best_key.p, 0, sizeof(unsigned long long), b->stream));
+    HIPOK(b, b->hscores.reserve(n * 4));
     while (b->out_ev.size() < chunks.size()) {
       hipEvent_t e;
       HIPOK(b, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1378,6 +1378,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   const auto fail_sync = [&](sw_status s) {
     (void)hipStreamSynchronize(b->stream);
     (void)hipStreamSynchronize(b->copy_stream);
+    (void)hipStreamSynchronize(b->out_stream);
     return s;
   };
   for (size_t i = 0; i < chunks.size(); ++i) {
@@ -1399,36 +1400,47 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     if ((st = score(b->dslot[s].p, c, b->scores.p + c.c0)) != SW_OK) return fail_sync(st);
     HIPOK(b, hipEventRecord(b->kern_done[s], b->stream));
     if (out) {
-      HIPOK(b, swk_best_part(b->scores.p + c.c0, c.c1 - c.c0, c.c0, b->best_key.p, b->stream));
+      HIPOK(b, hipStreamWaitEvent(b->out_stream, b->kern_done[s], 0));
       HIPOK(b, hipMemcpyAsync(b->hscores.p + c.c0 * 4, b->scores.p + c.c0, (c.c1 - c.c0) * 4,
-                              hipMemcpyDeviceToHost, b->stream));
-      HIPOK(b, hipEventRecord(b->out_ev[i], b->stream));
+                              hipMemcpyDeviceToHost, b->out_stream));
+      HIPOK(b, hipEventRecord(b->out_ev[i], b->out_stream));
     }
   }
   if (!out) return SW_OK;
-  HIPOK(b, swk_best_finalize(b->best_key.p, nullptr, b->best_dev.p, b->best_dev.p + 2, b->stream));
-  HIPOK(b, hipMemcpyAsync(b->hscores.p + best_at(n), b->best_dev.p, 24, hipMemcpyDeviceToHost,
-                          b->stream));
+  // scores into the caller's buffer as they land, with the best hit: per pool part the lowest
+  // index of its maximum, then the lowest index among the parts' maxima
   const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
-  for (size_t i = 0; i < chunks.size(); ++i) {  // scores into the caller's buffer as they land
+  const unsigned T = b->pool->size();
+  std::vector<size_t> pbest(T);
+  size_t best = 0;
+  for (size_t i = 0; i < chunks.size(); ++i) {
     const Chunk& c = chunks[i];
     HIPOK(b, hipEventSynchronize(b->out_ev[i]));
-    parallel_for(*b->pool, c.c1 - c.c0, [&](size_t lo, size_t hi) {
-      std::memcpy(out + c.c0 + lo, hs + c.c0 + lo, (hi - lo) * 4);
-    });
+    const size_t cnt = c.c1 - c.c0;
+    const unsigned parts = cnt >= 4096 ? T : 1;
+    const size_t step = (cnt + parts - 1) / parts;
+    std::fill(pbest.begin(), pbest.end(), SIZE_MAX);
+    const auto part = [&](unsigned p) {
+      const size_t lo = c.c0 + std::min(cnt, p * step), hi = c.c0 + std::min(cnt, (p + 1) * step);
+      size_t bi = lo;
+      for (size_t k = lo; k < hi; ++k) {
+        const int32_t v = hs[k];
+        out[k] = v;
+        if (v > hs[bi]) bi = k;
+      }
+      if (lo < hi) pbest[p] = bi;
+    };
+    if (parts > 1) b->pool->run(part);
+    else part(0);
+    for (size_t x : pbest)  // parts and chunks in index order: strictly greater keeps the lowest
+      if (x != SIZE_MAX && hs[x] > hs[best]) best = x;
   }
+  b->best_index = best;
+  b->best_id = best;
+  b->best_score = hs[best];
+  b->best_kind = 1;
   HIPOK(b, hipStreamSynchronize(b->stream));
   return SW_OK;
-}
-
-// The host best hit after a to_host feed: index and score from the pinned tail (id = index).
-static void take_best(sw_bank* b, size_t n) {
-  uint64_t h[3];
-  std::memcpy(h, b->hscores.p + best_at(n), sizeof(h));
-  b->best_index = h[2];
-  b->best_id = h[2];
-  b->best_score = (int32_t)(int64_t)h[1];
-  b->best_kind = 1;
 }
 
 static inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -2001,7 +2013,6 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, size_t 
   }
   const sw_status st = batch_feed(b, residues, residues_len, offsets, lens, n, scores_out);
   if (st != SW_OK) return st;
-  take_best(b, n);
   if (ids) b->best_id = ids[b->best_index];
   return SW_OK;
 }
@@ -2021,7 +2032,6 @@ extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
     st = multi_records(b, recs, n, scores_out);
   } else {
     st = records_feed(b, recs, n, scores_out);
-    if (st == SW_OK) take_best(b, n);
   }
   if (st == SW_OK) {  // the record's own ID (sequence_t.ID, aligner_Header.h:20)
     uint32_t id;

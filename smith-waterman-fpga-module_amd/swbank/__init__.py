@@ -297,11 +297,17 @@ class ScoreBank:
 
     # target stream
     def score_batch(self, residues: np.ndarray, offsets: np.ndarray, lens: np.ndarray,
-                    ids: Optional[np.ndarray] = None) -> np.ndarray:
+                    ids: Optional[np.ndarray] = None,
+                    out: Optional[np.ndarray] = None) -> np.ndarray:
         """Scores of targets residues[offsets[k] : offsets[k] + lens[k]] in input order; ids
-        (optional, one per target) tag the batch best hit (best())."""
+        (optional, one per target) tag the batch best hit (best()); out (optional, int32,
+        contiguous, one per target) is filled and returned instead of a new array."""
         res, offs, ln, idv = validate_batch(residues, offsets, lens, ids)
-        out = np.empty(len(ln), dtype=np.int32)  # every entry written by the library
+        if out is None:
+            out = np.empty(len(ln), dtype=np.int32)  # every entry written by the library
+        elif (out.dtype != np.int32 or out.shape != (len(ln),)
+              or not out.flags["C_CONTIGUOUS"] or not out.flags["WRITEABLE"]):
+            raise ValueError("out: a writable contiguous int32 array with one entry per target")
         if len(ln) == 0:
             return out
         self._check(lib().sw_score_batch(self._h, _p(res), res.size, _p(offs), _p(ln),
