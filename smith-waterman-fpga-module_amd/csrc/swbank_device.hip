@@ -251,6 +251,8 @@ struct sw_bank {
   PinBuf hslot[NSLOT], hscores;
   std::vector<hipEvent_t> out_ev;  // per chunk: its scores are back in hscores
   hipStream_t out_stream = nullptr;  // scores back to the host, beside the next chunk's kernel
+  hipStream_t stream2 = nullptr;     // odd chunks' kernels (scratch-free launches overlap)
+  hipEvent_t ev_s2 = nullptr;
   double host_pack_ms = 0;         // feeder gather time of host calls (with timing on)
   DevBuf<uint8_t> dslot[NSLOT];
   std::unique_ptr<HostPool> pool;
@@ -513,6 +515,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->edge[1].release();
   if (b->copy_stream) (void)hipStreamSynchronize(b->copy_stream);
   if (b->out_stream) (void)hipStreamSynchronize(b->out_stream);
+  if (b->stream2) (void)hipStreamSynchronize(b->stream2);
   for (hipEvent_t e : b->out_ev) (void)hipEventDestroy(e);
   for (int i = 0; i < sw_bank::NSLOT; ++i) {
     b->hslot[i].release();
@@ -524,6 +527,8 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->pool.reset();
   if (b->copy_stream) (void)hipStreamDestroy(b->copy_stream);
   if (b->out_stream) (void)hipStreamDestroy(b->out_stream);
+  if (b->stream2) (void)hipStreamDestroy(b->stream2);
+  if (b->ev_s2) (void)hipEventDestroy(b->ev_s2);
   b->res.release();
   b->offs.release();
   b->lens.release();
@@ -946,7 +951,8 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                         const uint32_t* d_lens, size_t n, uint32_t max_len, int32_t* d_scores,
                         hipStream_t st, uint32_t packed = SWK_PACK_BYTES,
                         const uint32_t* perm = nullptr,
-                        const uint32_t* perm_n = nullptr, bool dsort = false) {
+                        const uint32_t* perm_n = nullptr, bool dsort = false,
+                        bool wait_prev = true) {
   // Past the 16-bit lanes (min(|q|, max|t|) * max(s) + max(s) > 65535) the 16-bit passes are
   // still exact for every pair scoring <= 65535 - max(s); the pairs above are re-scored by the
   // int32 kernel through an index list (swk_launch_i32).
@@ -972,7 +978,8 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   HIPOK(b, hipStreamWaitEvent(st, b->ev_ready, 0));  // the query tables are uploaded
   // bank-owned scratch (edge rows, re-score lists, the device sort order, int32 scratch) is
   // reused by every call: a call on another stream waits for the previous call to finish
-  HIPOK(b, hipStreamWaitEvent(st, b->ev_used, 0));
+  // (the host feeder's scratch-free chunk launches on two streams skip it, wait_prev = false)
+  if (wait_prev) HIPOK(b, hipStreamWaitEvent(st, b->ev_used, 0));
   const size_t nseg = b->segs.size();
   const bool rec = packed == SWK_PACK_RECORDS;
   const uint32_t ecols = (max_len + 7) / 8 * 8;
@@ -1323,6 +1330,17 @@ size_t chunk_target(size_t total) {
   if (mb > 0) return (size_t)mb << 20;
   return std::min<size_t>((size_t)256 << 20, std::max<size_t>((size_t)8 << 20, total / 8));
 }
+
+// Cumulative chunk boundaries (in input bytes) of a host batch: the first chunk a quarter of
+// chunk_target() (at least 1 MiB) so the GPU starts early, then doubling up to chunk_target()
+// (SWBANK_CHUNK_MB: fixed size).  Boundaries strictly inside (0, total).
+std::vector<size_t> chunk_bounds(size_t total) {
+  std::vector<size_t> bounds;
+  const size_t cap = chunk_target(total);
+  size_t sz = env_int("SWBANK_CHUNK_MB", 0) > 0 ? cap : std::max<size_t>(1 << 20, cap / 4);
+  for (size_t at = sz; at < total; at += sz, sz = std::min(cap, sz * 2)) bounds.push_back(at);
+  return bounds;
+}
 }  // namespace
 
 static unsigned host_threads_total() { return host_threads(); }
@@ -1335,6 +1353,8 @@ static sw_status feeder_init(sw_bank* b) {
   if (b->copy_stream) return SW_OK;
   HIPOK(b, hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
   HIPOK(b, hipStreamCreateWithFlags(&b->out_stream, hipStreamNonBlocking));
+  HIPOK(b, hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
+  HIPOK(b, hipEventCreateWithFlags(&b->ev_s2, hipEventDisableTiming));
   for (int i = 0; i < sw_bank::NSLOT; ++i) {
     HIPOK(b, hipEventCreateWithFlags(&b->h2d_done[i], hipEventDisableTiming));
     HIPOK(b, hipEventCreateWithFlags(&b->kern_done[i], hipEventDisableTiming));
@@ -1355,9 +1375,11 @@ struct Chunk {
 // input order as they land, the batch best hit (lowest index of the maximum) tracked in the same
 // pass; out == nullptr: they stay in b->scores on the device, enqueued on b->stream (a
 // multi-device bank gathers them).
+// overlap: the chunks' launches use no bank scratch (scratch_free), so odd chunks run on
+// stream2 and one launch's drain overlaps the next one's start.
 template <class GatherF, class ScoreF>
 static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, GatherF gather,
-                      ScoreF score, int32_t* out) {
+                      ScoreF score, int32_t* out, bool overlap) {
   sw_status st = feeder_init(b);
   if (st != SW_OK) return st;
   size_t slot_bytes = 0;
@@ -1377,6 +1399,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   }
   const auto fail_sync = [&](sw_status s) {
     (void)hipStreamSynchronize(b->stream);
+    (void)hipStreamSynchronize(b->stream2);
     (void)hipStreamSynchronize(b->copy_stream);
     (void)hipStreamSynchronize(b->out_stream);
     return s;
@@ -1396,15 +1419,20 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     HIPOK(b, hipMemcpyAsync(b->dslot[s].p, b->hslot[s].p, bytes, hipMemcpyHostToDevice,
                             b->copy_stream));
     HIPOK(b, hipEventRecord(b->h2d_done[s], b->copy_stream));
-    HIPOK(b, hipStreamWaitEvent(b->stream, b->h2d_done[s], 0));
-    if ((st = score(b->dslot[s].p, c, b->scores.p + c.c0)) != SW_OK) return fail_sync(st);
-    HIPOK(b, hipEventRecord(b->kern_done[s], b->stream));
+    hipStream_t ks = overlap && (i & 1) ? b->stream2 : b->stream;
+    HIPOK(b, hipStreamWaitEvent(ks, b->h2d_done[s], 0));
+    if ((st = score(b->dslot[s].p, c, b->scores.p + c.c0, ks)) != SW_OK) return fail_sync(st);
+    HIPOK(b, hipEventRecord(b->kern_done[s], ks));
     if (out) {
       HIPOK(b, hipStreamWaitEvent(b->out_stream, b->kern_done[s], 0));
       HIPOK(b, hipMemcpyAsync(b->hscores.p + c.c0 * 4, b->scores.p + c.c0, (c.c1 - c.c0) * 4,
                               hipMemcpyDeviceToHost, b->out_stream));
       HIPOK(b, hipEventRecord(b->out_ev[i], b->out_stream));
     }
+  }
+  if (overlap) {  // the bank stream (the multi-device gather, the next call) after stream2
+    HIPOK(b, hipEventRecord(b->ev_s2, b->stream2));
+    HIPOK(b, hipStreamWaitEvent(b->stream, b->ev_s2, 0));
   }
   if (!out) return SW_OK;
   // scores into the caller's buffer as they land, with the best hit: per pool part the lowest
@@ -1515,6 +1543,19 @@ static inline uint32_t pack_4bit(const uint8_t* src, uint32_t l, uint8_t* dst) {
   return mx;
 }
 
+// True when launches for targets of at most max_len use no bank scratch (one query segment,
+// no optimistic f16 re-score list, no int32 re-score), so host-feeder chunks may run on two
+// streams (SWBANK_OVERLAP=0 disables).  Mirrors launch()'s choices.
+static bool scratch_free(const sw_bank* b, uint32_t max_len) {
+  if (env_int("SWBANK_OVERLAP", 1) == 0) return false;
+  const uint64_t s = (uint64_t)std::max(0, b->smax);
+  const uint64_t top = std::min<uint64_t>(b->query.size(), max_len) * s + s;
+  const bool need32 = top > 65535u || env_int("SWBANK_I32", 0) != 0;
+  const bool f16_ok = b->f16 && b->f16_neg >= -2048 && env_int("SWBANK_F16", 1) != 0;
+  const bool opt16 = f16_ok && top > 2048u && env_int("SWBANK_F16_OPT", 1) != 0;
+  return b->segs.size() == 1 && b->wsegs == 1 && !need32 && !opt16;
+}
+
 // The host-buffer batch through the feeder (n >= 1, buffers checked by the caller).
 static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                             const uint64_t* offsets, const uint32_t* lens, size_t n,
@@ -1554,14 +1595,17 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   // residue, or, for a DNA chunk without N, the 2-bit stream (a quarter of the PCIe bytes;
   // SWBANK_PACK2=0 disables), each target from a byte boundary, 16 zero bytes after the last
   const auto codes_at = [](size_t cnt) { return align16(cnt * 16 + 4); };
-  const size_t target = chunk_target(total);
+  const std::vector<size_t> bounds = chunk_bounds(total);
+  const auto nb = [&](size_t acc) {  // boundaries at or below acc
+    return std::upper_bound(bounds.begin(), bounds.end(), acc) - bounds.begin();
+  };
   std::vector<std::vector<std::pair<size_t, size_t>>> pcut(P);  // (end position, code prefix)
   run_parts([&](unsigned p) {
     size_t acc = psum[p];
     for (size_t k = std::min(n, p * pstep); k < std::min(n, (p + 1) * pstep); ++k) {
-      const size_t before = acc / target;
+      const auto before = nb(acc);
       acc += lens[k];
-      if (acc / target != before && k + 1 < n) pcut[p].push_back({k + 1, acc});
+      if (nb(acc) != before && k + 1 < n) pcut[p].push_back({k + 1, acc});
     }
   });
   std::vector<Chunk> chunks;
@@ -1725,7 +1769,9 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                  : mode == SWK_PACK_NIBBLE ? align16(part4[T] + 16)
                                            : align16(part[T]));
   };
-  const auto score = [&](uint8_t* dslot, const Chunk& c, int32_t* d_scores) -> sw_status {
+  const bool overlap = scratch_free(b, max_len);
+  const auto score = [&](uint8_t* dslot, const Chunk& c, int32_t* d_scores,
+                         hipStream_t ks) -> sw_status {
     const size_t cnt = c.c1 - c.c0;
     const SlotTail tl = slot_tail(cnt * 8, cnt);
     const bool pm = has_perm[si];
@@ -1733,11 +1779,12 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     const uint32_t ml = chunk_max[si++];
     return launch(b, dslot + codes_at(cnt), reinterpret_cast<const uint64_t*>(dslot),
                   reinterpret_cast<const uint32_t*>(dslot + tl.lens_at), cnt, ml, d_scores,
-                  b->stream, mode,
+                  ks, mode,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.perm_at) : nullptr,
-                  pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr);
+                  pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr, false,
+                  !overlap);
   };
-  return feed(b, n, chunks, gather, score, out);
+  return feed(b, n, chunks, gather, score, out, overlap);
 }
 
 // ---- CAPI record path (row f2): sequence_t arrays as the reference host builds them ------
@@ -1786,12 +1833,15 @@ static sw_status records_feed(sw_bank* b, const uint8_t* recs, size_t n, int32_t
   if ((st = feeder_init(b)) != SW_OK) return st;
   const auto rlen = [&](size_t k) { return record_len(recs + k * SWB_RECORD); };
   // chunks in input order: records | lens | perm | count (longest-first order per chunk)
-  const size_t per = std::max<size_t>(1, chunk_target(n * SWB_RECORD) / SWB_RECORD);
   std::vector<Chunk> chunks;
-  for (size_t c0 = 0; c0 < n; c0 += per) {
-    const size_t c1 = std::min(n, c0 + per);
+  size_t c0 = 0;
+  for (size_t at : chunk_bounds(n * SWB_RECORD)) {
+    const size_t c1 = std::min(n, std::max(c0 + 1, at / SWB_RECORD));
+    if (c1 >= n) break;
     chunks.push_back({c0, c1, align16((c1 - c0) * (SWB_RECORD + 8) + 4)});
+    c0 = c1;
   }
+  chunks.push_back({c0, n, align16((n - c0) * (SWB_RECORD + 8) + 4)});
   HostPool& pool = *b->pool;
   HIPOK(b, hipSetDevice(b->device));
   std::vector<char> has_perm(chunks.size(), 0);
@@ -1834,16 +1884,19 @@ static sw_status records_feed(sw_bank* b, const uint8_t* recs, size_t n, int32_t
     *reinterpret_cast<uint32_t*>(slot + tl.cnt_at) = (uint32_t)cnt;
     return c.bytes;
   };
-  const auto score = [&](uint8_t* dslot, const Chunk& c, int32_t* d_scores) -> sw_status {
+  const bool overlap = scratch_free(b, SWB_RECORD_MAX);
+  const auto score = [&](uint8_t* dslot, const Chunk& c, int32_t* d_scores,
+                         hipStream_t ks) -> sw_status {
     const size_t cnt = c.c1 - c.c0;
     const SlotTail tl = slot_tail(cnt * SWB_RECORD, cnt);
     const bool pm = has_perm[si];
     const uint32_t ml = chunk_max[si++];
-    return launch(b, dslot, nullptr, nullptr, cnt, ml, d_scores, b->stream, SWK_PACK_RECORDS,
+    return launch(b, dslot, nullptr, nullptr, cnt, ml, d_scores, ks, SWK_PACK_RECORDS,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.perm_at) : nullptr,
-                  pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr);
+                  pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr, false,
+                  !overlap);
   };
-  return feed(b, n, chunks, gather, score, out);
+  return feed(b, n, chunks, gather, score, out, overlap);
 }
 
 // ---- multi-device banks (≙ MODULES ScoringModules behind the PrioEncoder,
