@@ -61,6 +61,7 @@ extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max
 extern "C" size_t swk_sort_scratch_bytes(void);
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
                                     uint32_t* idx, uint32_t* count, hipStream_t st);
+extern "C" void swk_set_occ_cap(int per_cu);
 extern "C" size_t swk_i32_waves(size_t n, uint32_t scols, size_t budget_bytes);
 extern "C" hipError_t swk_launch_i32(int gotoh, const uint8_t* res, const uint64_t* offs,
                                      const uint32_t* lens, size_t n, int packed,
@@ -73,6 +74,32 @@ namespace {
 int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// Debug-only host phase trace (tuning aid): with SWBANK_TRACE_FILE set, host-buffer calls append
+// "phase microseconds-since-call-entry" lines to that file.  Off by default; the library never
+// prints otherwise.
+struct PhaseTrace {
+  const char* path = std::getenv("SWBANK_TRACE_FILE");
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  std::vector<std::pair<const char*, double>> marks;
+  void mark(const char* what) {
+    if (path)
+      marks.push_back({what, std::chrono::duration<double, std::micro>(
+                                 std::chrono::steady_clock::now() - t0).count()});
+  }
+  ~PhaseTrace() {
+    if (!path || marks.empty()) return;
+    if (FILE* f = std::fopen(path, "a")) {
+      for (auto& m : marks) std::fprintf(f, "%s %.1f\n", m.first, m.second);
+      std::fprintf(f, "--\n");
+      std::fclose(f);
+    }
+  }
+};
+thread_local PhaseTrace* g_trace = nullptr;
+inline void trace_mark(const char* what) {
+  if (g_trace) g_trace->mark(what);
 }
 
 template <typename T>
@@ -1337,7 +1364,9 @@ size_t chunk_target(size_t total) {
 std::vector<size_t> chunk_bounds(size_t total) {
   std::vector<size_t> bounds;
   const size_t cap = chunk_target(total);
-  size_t sz = env_int("SWBANK_CHUNK_MB", 0) > 0 ? cap : std::max<size_t>(1 << 20, cap / 4);
+  const int first_kb = env_int("SWBANK_CHUNK_FIRST_KB", 0);
+  size_t sz = first_kb > 0 ? (size_t)first_kb << 10
+              : env_int("SWBANK_CHUNK_MB", 0) > 0 ? cap : std::max<size_t>(1 << 20, cap / 4);
   for (size_t at = sz; at < total; at += sz, sz = std::min(cap, sz * 2)) bounds.push_back(at);
   return bounds;
 }
@@ -1397,6 +1426,13 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
       b->out_ev.push_back(e);
     }
   }
+  // overlapped chunk launches run two at a time: each takes at most SWBANK_CHUNK_OCC (2)
+  // workgroups per CU, so a chunk's tiles are several per workgroup (less pipeline fill and
+  // drain per tile) and the two streams share the chip
+  struct OccCap {
+    explicit OccCap(int c) { swk_set_occ_cap(c); }
+    ~OccCap() { swk_set_occ_cap(0); }
+  } occ_cap(overlap ? std::max(0, env_int("SWBANK_CHUNK_OCC", 2)) : 0);
   const auto fail_sync = [&](sw_status s) {
     (void)hipStreamSynchronize(b->stream);
     (void)hipStreamSynchronize(b->stream2);
@@ -1408,8 +1444,10 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     const int s = (int)(i % sw_bank::NSLOT);
     const Chunk& c = chunks[i];
     if (i >= (size_t)sw_bank::NSLOT) HIPOK(b, hipEventSynchronize(b->h2d_done[s]));
+    trace_mark("gather<");
     const auto t0 = std::chrono::steady_clock::now();
     const size_t bytes = gather(b->hslot[s].p, c);
+    trace_mark("gather>");
     if (b->timing)
       b->host_pack_ms +=
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1422,6 +1460,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     hipStream_t ks = overlap && (i & 1) ? b->stream2 : b->stream;
     HIPOK(b, hipStreamWaitEvent(ks, b->h2d_done[s], 0));
     if ((st = score(b->dslot[s].p, c, b->scores.p + c.c0, ks)) != SW_OK) return fail_sync(st);
+    trace_mark("launched");
     HIPOK(b, hipEventRecord(b->kern_done[s], ks));
     if (out) {
       HIPOK(b, hipStreamWaitEvent(b->out_stream, b->kern_done[s], 0));
@@ -1444,6 +1483,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   for (size_t i = 0; i < chunks.size(); ++i) {
     const Chunk& c = chunks[i];
     HIPOK(b, hipEventSynchronize(b->out_ev[i]));
+    trace_mark("landed");
     const size_t cnt = c.c1 - c.c0;
     const unsigned parts = cnt >= 4096 ? T : 1;
     const size_t step = (cnt + parts - 1) / parts;
@@ -1468,6 +1508,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   b->best_score = hs[best];
   b->best_kind = 1;
   HIPOK(b, hipStreamSynchronize(b->stream));
+  trace_mark("done");
   return SW_OK;
 }
 
@@ -1588,6 +1629,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     pmax[p] = m;
   });
   for (unsigned p = 0; p < P; ++p) psum[p + 1] += psum[p];
+  trace_mark("lens-pass");
   const size_t total = psum[P];
   const uint32_t max_len = *std::max_element(pmax.begin(), pmax.end());
   if (max_len && !residues) return fail(b, SW_ERR_ARG, "null residues");
@@ -1595,17 +1637,20 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   // residue, or, for a DNA chunk without N, the 2-bit stream (a quarter of the PCIe bytes;
   // SWBANK_PACK2=0 disables), each target from a byte boundary, 16 zero bytes after the last
   const auto codes_at = [](size_t cnt) { return align16(cnt * 16 + 4); };
-  const std::vector<size_t> bounds = chunk_bounds(total);
-  const auto nb = [&](size_t acc) {  // boundaries at or below acc
-    return std::upper_bound(bounds.begin(), bounds.end(), acc) - bounds.begin();
-  };
+  std::vector<size_t> bounds = chunk_bounds(total);
+  bounds.push_back(SIZE_MAX);  // sentinel
   std::vector<std::vector<std::pair<size_t, size_t>>> pcut(P);  // (end position, code prefix)
   run_parts([&](unsigned p) {
     size_t acc = psum[p];
+    // the next boundary above this part's start; a cut after target k when the running code
+    // count reaches it (several boundaries inside one target make one cut)
+    size_t j = std::upper_bound(bounds.begin(), bounds.end(), acc) - bounds.begin();
     for (size_t k = std::min(n, p * pstep); k < std::min(n, (p + 1) * pstep); ++k) {
-      const auto before = nb(acc);
       acc += lens[k];
-      if (nb(acc) != before && k + 1 < n) pcut[p].push_back({k + 1, acc});
+      if (acc >= bounds[j]) {
+        while (acc >= bounds[j]) ++j;
+        if (k + 1 < n) pcut[p].push_back({k + 1, acc});
+      }
     }
   });
   std::vector<Chunk> chunks;
@@ -1617,6 +1662,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   };
   for (const auto& cuts : pcut)
     for (const auto& ca : cuts) add_chunk(ca.first, ca.second);
+  trace_mark("cuts");
   add_chunk(n, total);
   std::vector<uint32_t> chunk_max(chunks.size(), 0);  // set by the chunk's gather
   const uint32_t alpha = (uint32_t)b->alpha;
@@ -2059,6 +2105,10 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, size_t 
   if (!offsets || !lens || !scores_out) return fail(b, SW_ERR_ARG, "null host buffer");
   if (n > 0xFFFFFFFFull)
     return fail(b, SW_ERR_ARG, "host batches hold < 2^32 targets (sw_score_batch_device does not)");
+  PhaseTrace trace;
+  g_trace = trace.path ? &trace : nullptr;
+  struct Reset { ~Reset() { g_trace = nullptr; } } reset_trace;
+  trace_mark("entry");
   if (b->is_multi()) {
     const sw_status st = multi_batch(b, residues, residues_len, offsets, lens, n, scores_out);
     if (st == SW_OK && ids) b->best_id = ids[b->best_index];

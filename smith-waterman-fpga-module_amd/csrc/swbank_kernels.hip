@@ -29,7 +29,9 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include "swbank_internal.h"
 
@@ -930,17 +932,41 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
 // Workgroups for a persistent launch: as many as fit on the device at once (occupancy x CUs),
 // then evened out so every workgroup gets the same number of tiles (+-1).  SWBANK_GRID=0 gives
 // one workgroup per tile; SWBANK_GRID=m caps the resident workgroups per CU at m (tuning).
+// Per-thread cap on resident workgroups per CU for the next score launches (0 = none): the host
+// feeder's overlapped chunk launches take half the chip each (swk_set_occ_cap).
+static thread_local int t_occ_cap = 0;
+
+// Occupancy per (kernel, block size, LDS bytes, device), queried once: the runtime query costs
+// microseconds, and the host feeder launches a kernel per chunk.
+static int cached_occupancy(const void* fn, int threads, size_t lds, int dev, int* cus) {
+  struct Entry { const void* fn; int threads; size_t lds; int dev, occ, cus; };
+  static std::mutex m;
+  static std::vector<Entry> cache;
+  std::lock_guard<std::mutex> g(m);
+  for (const Entry& e : cache)
+    if (e.fn == fn && e.threads == threads && e.lds == lds && e.dev == dev) {
+      *cus = e.cus;
+      return e.occ;
+    }
+  int occ = 0, c = 0;
+  if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, threads, lds) != hipSuccess)
+    return 0;
+  cache.push_back({fn, threads, lds, dev, occ, c});
+  *cus = c;
+  return occ;
+}
+
 static unsigned persistent_grid(const void* fn, size_t ntiles, int threads, size_t lds) {
-  int dev = 0, cus = 0, occ = 0;
+  int dev = 0, cus = 0;
   const char* env = std::getenv("SWBANK_GRID");
   const int cap = (env && *env) ? std::atoi(env) : -1;
   if (cap == 0) return (unsigned)ntiles;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, threads, lds) != hipSuccess ||
-      cus <= 0 || occ <= 0)
-    return (unsigned)ntiles;
+  if (hipGetDevice(&dev) != hipSuccess) return (unsigned)ntiles;
+  int occ = cached_occupancy(fn, threads, lds, dev, &cus);
+  if (cus <= 0 || occ <= 0) return (unsigned)ntiles;
   if (cap > 0) occ = std::min(occ, cap);
+  if (t_occ_cap > 0) occ = std::min(occ, t_occ_cap);
   const size_t slots = (size_t)cus * occ;
   const size_t rounds = (ntiles + slots - 1) / slots;
   return (unsigned)((ntiles + rounds - 1) / rounds);
@@ -1428,6 +1454,8 @@ static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream
   X(16, 4, 0, 0, 0, 1) X(16, 4, 1, 0, 0, 1) X(32, 4, 0, 0, 0, 1) X(64, 4, 0, 0, 0, 1)         \
   X(16, 4, 0, 0, 1, 1)                                                                        \
   X(16, 4, 0, 1, 0, 1) X(16, 4, 1, 1, 0, 1) X(16, 4, 0, 1, 1, 1)
+
+extern "C" void swk_set_occ_cap(int per_cu) { swk::t_occ_cap = per_cu; }
 
 extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh, int f16) {
 #define SWK_HAS(RR, BB, C0, PF, GT, FH) \
