@@ -589,26 +589,7 @@ __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens
 // 16 A/C/G/T slots on 16 different 4-bank groups (conflict-free ds_read_b128).  A column of
 // wave w reads its row words as 4 blocks of 8 (two ds_read_b128 each), one block ahead of
 // the asm block that consumes them: 6.5 VALU per 2 cells instead of 7.5.
-// Wave-to-wave hand-off without a workgroup barrier (FLAGS): prog[w] = phases wave w has
-// completed (release store after its ring writes and tile-slot atomics); wave w enters phase ph
-// once its producer w-1 and its consumer w+1 have completed phase ph-1 (acquire loads), so
-// neighbours drift by up to a phase instead of the whole workgroup stepping together.  A tile
-// slot k % W is reused for tile k only after the last wave has read and cleared it for tile
-// k - W: clr[s] = the next tile slot s may take.  Waits poll with s_sleep and are bounded (a
-// logic error must not hang the GPU: the scores would then be wrong, and the tests say so).
-__device__ __forceinline__ void wait_ge(const uint32_t* p, uint32_t v) {
-  for (uint32_t it = 0; __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v;
-       ++it) {
-    if (it > (1u << 24)) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-__device__ __forceinline__ void publish(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
-          bool FLAGS = false>
+template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
   constexpr int C = 8;
   static_assert(!PAIR || (R == 32 && F16 && !PROF && !GOTOH && !COL0), "PAIR: f16 merged R=32");
@@ -618,9 +599,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int W = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
   const bool seg_in = a.edge_in != nullptr, seg_out = a.edge_out != nullptr;
   uint32_t* bestsh = smem + (PAIR ? a.PS / 4 : 0);               // W x 128 words
-  uint32_t* prog = bestsh + W * SWB_TILE;                         // FLAGS: prog[16] | clr[16]
-  uint32_t* clr = prog + 16;
-  uint2* bnd = reinterpret_cast<uint2*>(bestsh + W * SWB_TILE + (FLAGS ? 32 : 0));  // row -1
+  uint2* bnd = reinterpret_cast<uint2*>(bestsh + W * SWB_TILE);  // row -1 boundary
   uint2* sink = bnd + 64;                                        // last wave's bottom row
   uint2* ein = sink + (seg_out ? C * 64 : 64);                   // previous segment, 2 x 8 cols
   uint2* ring = ein + (seg_in ? 2 * C * 64 : 0);
@@ -648,10 +627,6 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const uint32_t S = a.S;
 
   for (int i = threadIdx.x; i < W * SWB_TILE; i += blockDim.x) bestsh[i] = 0;
-  if (FLAGS && (int)threadIdx.x < 16) {
-    prog[threadIdx.x] = 0;
-    clr[threadIdx.x] = threadIdx.x;  // slot s is free for tile s
-  }
   // row -1: u16 H~ = S, G/F = 0 | f16 H = 0, T = -(o+e)
   // f16 encodings of -(o+e), -e, -o (host-computed, so they stay in SGPRs)
   const f16x2 NOE2 = as_f16x2(as_u16x2(a.f16_noe)), NE2 = as_f16x2(as_u16x2(a.f16_ne)),
@@ -752,11 +727,6 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   for (int ph = 0; ph < nph; ++ph) {
     const int g = ph - wave;
     if (g >= 0 && g < total) {
-      if constexpr (FLAGS) {
-        if (wave > 0) wait_ge(&prog[wave - 1], (uint32_t)ph);     // chunk g is in the ring
-        if (wave < W - 1) wait_ge(&prog[wave + 1], (uint32_t)ph); // slot g & 1 was read
-        if (seg_in && wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // edge DMA
-      }
       const uint2 clo = rlo, chi = rhi;
       const bool last = c + 1 == nch;
       const int ntile = tile + G;
@@ -919,7 +889,6 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       }
       if (last) {  // this wave's part of tile k is done
         uint32_t* bs = bestsh + (k % W) * SWB_TILE;
-        if constexpr (FLAGS) wait_ge(&clr[k % W], (uint32_t)k);  // slot cleared for tile k - W
         atomicMax(&bs[lane], (uint32_t)best.x);
         atomicMax(&bs[lane + 64], (uint32_t)best.y);
         if (wave == W - 1) {  // every other wave folded tile k in an earlier phase
@@ -927,7 +896,6 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           int32_t blo = (int32_t)bs[lane], bhi = (int32_t)bs[lane + 64];
           bs[lane] = 0;
           bs[lane + 64] = 0;
-          if constexpr (FLAGS) publish(&clr[k % W], (uint32_t)(k + W));
           if constexpr (F16) {  // f16 bit patterns of non-negative integers -> int
             blo = f16_unscore((uint32_t)blo);
             bhi = f16_unscore((uint32_t)bhi);
@@ -957,11 +925,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         ++c;
       }
     }
-    if constexpr (FLAGS) {
-      if (lane == 0) publish(&prog[wave], (uint32_t)ph + 1);
-    } else {
-      __syncthreads();
-    }
+    __syncthreads();
   }
 }
 
@@ -1008,15 +972,14 @@ static unsigned persistent_grid(const void* fn, size_t ntiles, int threads, size
   return (unsigned)((ntiles + rounds - 1) / rounds);
 }
 
-template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
-          bool FLAGS = false>
+template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false>
 static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st) {
   const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE;
-  const size_t lds = (size_t)W * SWB_TILE * 4 + (FLAGS ? 128 : 0) +
+  const size_t lds = (size_t)W * SWB_TILE * 4 +
                      (size_t)(64 + (a.edge_out ? 8 * 64 : 64) + (a.edge_in ? 2 * 8 * 64 : 0) +
                               (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8 +
                      (PROF ? prof_bytes : 0) + (PAIR ? a.PS : 0);
-  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR, FLAGS>;
+  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -1521,13 +1484,8 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                          swk::f16_pair(-(int)O), nullptr, 0u, 0u, 0};
   const uint32_t prof_bytes = (pad + 1) * PS;
   if (pair) {  // PS = pair-table bytes
-    if (R == 32 && f16 && !prof && !gotoh && !col0) {
-      // SWBANK_FLAGS=1: neighbour progress flags instead of the per-phase barrier
-      const char* fl = std::getenv("SWBANK_FLAGS");
-      if (fl && *fl == '1')
-        return swk::launch_score<32, 4, false, false, false, true, true, true>(a, W, 0, st);
+    if (R == 32 && f16 && !prof && !gotoh && !col0)
       return swk::launch_score<32, 4, false, false, false, true, true>(a, W, 0, st);
-    }
     return hipErrorInvalidValue;
   }
 #define SWK_CASE(RR, BB, C0, PF, GT, FH)                                                      \
