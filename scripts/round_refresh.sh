@@ -11,16 +11,18 @@ mkdir -p "$OUT"
 cd "$ROOT"
 fatal() { case "$1" in 0|1) return 1;; esac; return 0; }
 step() { echo "[refresh] $1 rc=$2"; }
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > "$OUT/pytest_gpu_$TAG.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1
 rc=$?; step pytest $rc; tail -2 "$OUT/pytest_gpu_$TAG.log"; if fatal $rc; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1
 rc=$?; step smoke $rc; tail -1 "$OUT/smoke_$TAG.log"; if [ $rc -ne 0 ]; then exit $rc; fi
-for w in q100xdata500 reads150x1k protein512x1k; do
+for w in q100xdata500 reads150x1k protein512x1k ragged data500; do
   timeout -k 10 600 python bench.py --workload $w > "$OUT/bench_${TAG}_$w.json" 2> "$OUT/bench_${TAG}_$w.err"
   rc=$?; step "bench $w" $rc; cut -c1-200 "$OUT/bench_${TAG}_$w.json"; if [ $rc -ne 0 ]; then exit $rc; fi
 done
 bash scripts/gpu_profile.sh "$TAG"
 rc=$?; step profile $rc; if [ $rc -ne 0 ]; then exit $rc; fi
 bash scripts/gpu_profile.sh "${TAG}_protein" --workload protein512x1k
-rc=$?; step profile_protein $rc
+rc=$?; step profile_protein $rc; if [ $rc -ne 0 ]; then exit $rc; fi
+bash scripts/gpu_profile.sh "${TAG}_reads" --workload reads150x1k
+rc=$?; step profile_reads $rc
 exit $rc
