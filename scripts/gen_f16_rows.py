@@ -145,10 +145,13 @@ def main():
     parts.append("#define SWK_F16PAIR_F \\\n" + fmt(pair_block(True, False)))
     parts.append("#define SWK_F16PAIR_M \\\n" + fmt(pair_block(False, False)))
     parts.append("#define SWK_F16PAIR_L \\\n" + fmt(pair_block(False, True)))
-    # 4-row single blocks (the wave kernel's K = 4: a whole column in one block)
-    for mode in ("L", "P"):
-        parts.append(f"#define SWK_F16M_{mode}_Z0_L1_R4 \\\n" + fmt(merged_block(mode, 0, 1, 4)))
-        parts.append(f"#define SWK_F16G_{mode}_L1_R4 \\\n" + fmt(gotoh_block(mode, 1, 4)))
+    # 4- and 2-row single blocks (the wave kernel's K = 4, and K = 2 of its split tail: a
+    # whole column in one block)
+    for nr in (4, 2):
+        for mode in ("L", "P"):
+            parts.append(f"#define SWK_F16M_{mode}_Z0_L1_R{nr} \\\n" +
+                         fmt(merged_block(mode, 0, 1, nr)))
+            parts.append(f"#define SWK_F16G_{mode}_L1_R{nr} \\\n" + fmt(gotoh_block(mode, 1, nr)))
     open(OUT, "w").write("".join(parts))
     print("wrote", OUT)
 

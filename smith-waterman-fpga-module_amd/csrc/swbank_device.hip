@@ -37,7 +37,8 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
                                       const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
                                       int packed, const uint32_t* fb_qtab, uint32_t fb_nv,
-                                      uint32_t fb_PS, int32_t fb_thresh, hipStream_t st);
+                                      uint32_t fb_PS, int32_t fb_thresh,
+                                      const SwkWaveSplit* split, hipStream_t st);
 extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh, int f16,
                                        const uint8_t* res, const uint64_t* offs,
                                        const uint32_t* lens, size_t n, const uint32_t* qtab,
@@ -219,6 +220,7 @@ class HostPool {
 struct sw_bank {
   sw_config cfg{};
   int device = 0;
+  int cus = 0;  // compute units (4 SIMDs each): the wave kernel's split-tail policy
   hipStream_t stream = nullptr;
   char err[512] = {0};
 
@@ -268,6 +270,14 @@ struct sw_bank {
   DevBuf<uint32_t> wtab;   // LUT: 64K row words | PROF: (A+1) x 64K profile bytes
   DevBuf<uint32_t> wtab16; // the same in f16 (LUT: high bytes | PROF: 2-byte entries)
   uint32_t wPS16 = 0;
+  // wave kernel split tail (one segment, K >= 8): [i] = the query as P = 2 << i segments of
+  // sK = K/P rows per lane (stab: u16, stab16: f16, sseg_words* apart); sring: 256 columns x
+  // uint2 per segment boundary of every tail pair
+  int sK[2] = {0, 0};
+  size_t sseg_words[2] = {0, 0}, sseg_words16[2] = {0, 0};
+  uint32_t sPS[2] = {0, 0}, sPS16[2] = {0, 0};
+  DevBuf<uint32_t> stab[2], stab16[2];
+  DevBuf<uint2> sring;
 
   // host-buffer feeder (sw_score_batch / sw_score_records): NSLOT pinned staging slots and
   // device slots, chunk i gathered on the host while chunk i-1 crosses PCIe on copy_stream
@@ -490,6 +500,8 @@ extern "C" sw_status sw_bank_create(sw_bank** out, const sw_config* cfg_in) {
     return SW_ERR_HIP;
   }
   b->alpha = cfg.alphabet == SW_ALPHABET_DNA ? SW_DNA_ALPHA : SW_PROTEIN_ALPHA;
+  if (hipDeviceGetAttribute(&b->cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    b->cus = 0;
   if (cfg.alphabet == SW_ALPHABET_PROTEIN) {  // BLOSUM62 -11/-1 until sw_set_matrix is called
     int8_t m[SW_PROTEIN_ALPHA * SW_PROTEIN_ALPHA];
     sw_fill_matrix(SW_ALPHABET_PROTEIN, 0, 0, m);
@@ -538,6 +550,11 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->dsort.release();
   b->wtab.release();
   b->wtab16.release();
+  for (int i = 0; i < 2; ++i) {
+    b->stab[i].release();
+    b->stab16[i].release();
+  }
+  b->sring.release();
   b->edge[0].release();
   b->edge[1].release();
   if (b->copy_stream) (void)hipStreamSynchronize(b->copy_stream);
@@ -827,54 +844,65 @@ static sw_status prepare(sw_bank* b) {
   }
   // wave-kernel layout of the same query: rows padded to 64K; queries past 1024 rows run as
   // 1024-row segments (K = 16), one table per segment, concatenated
+  const auto wave_tables = [&](int wrows, int nsegs, std::vector<uint32_t>& wt,
+                               std::vector<uint32_t>& wt16) {
+    for (int sg = 0; sg < nsegs; ++sg) {
+      const int r0 = sg * wrows, nr = std::min(wrows, std::max(0, qlen - r0));
+      if (!prof) {
+        const size_t base = wt.size();
+        wt.resize(base + wrows, 0xFFFFFFFFu);
+        for (int i = 0; i < nr; ++i) {
+          uint32_t w = 0;
+          for (int c = 0; c < 4; ++c)
+            w |= (uint32_t)(uint8_t)(S - m[b->query[r0 + i] * A + c]) << (8 * c);
+          wt[base + i] = w;
+        }
+        if (f16) {
+          const size_t b16 = wt16.size();
+          wt16.resize(b16 + wrows, 0xBCBCBCBCu);  // rows past the query: -2048
+          for (int i = 0; i < nr; ++i) {
+            uint32_t w = 0;
+            for (int c = 0; c < 4; ++c) {
+              uint8_t h;
+              f16_hi(m[b->query[r0 + i] * A + c], &h);
+              w |= (uint32_t)h << (8 * c);
+            }
+            wt16[b16 + i] = w;
+          }
+        }
+      } else {
+        std::vector<uint8_t> qp((size_t)(A + 1) * wrows, 0xFF);
+        for (int c = 0; c < A; ++c)
+          for (int i = 0; i < nr; ++i)
+            qp[(size_t)c * wrows + i] = (uint8_t)(S - m[b->query[r0 + i] * A + c]);
+        const size_t base = wt.size();
+        wt.resize(base + qp.size() / 4);
+        std::memcpy(wt.data() + base, qp.data(), qp.size());
+        if (f16) {
+          std::vector<uint16_t> q16((size_t)(A + 1) * wrows, 0xBC00u);
+          for (int c = 0; c < A; ++c)
+            for (int i = 0; i < nr; ++i)
+              q16[(size_t)c * wrows + i] = f16_score_bits(m[b->query[r0 + i] * A + c]);
+          const size_t b16 = wt16.size();
+          wt16.resize(b16 + q16.size() / 2);
+          std::memcpy(wt16.data() + b16, q16.data(), q16.size() * 2);
+        }
+      }
+    }
+  };
   std::vector<uint32_t> wt, wt16;
   const int wK = qlen <= 256 ? 4 : qlen <= 512 ? 8 : 16;
   const int wrows = 64 * wK;
   const int wsegs = std::max(1, (qlen + wrows - 1) / wrows);
   const uint32_t wPS = prof ? (uint32_t)wrows : 0, wPS16 = prof ? (uint32_t)wrows * 2 : 0;
-  for (int sg = 0; sg < wsegs; ++sg) {
-    const int r0 = sg * wrows, nr = std::min(wrows, std::max(0, qlen - r0));
-    if (!prof) {
-      const size_t base = wt.size();
-      wt.resize(base + wrows, 0xFFFFFFFFu);
-      for (int i = 0; i < nr; ++i) {
-        uint32_t w = 0;
-        for (int c = 0; c < 4; ++c)
-          w |= (uint32_t)(uint8_t)(S - m[b->query[r0 + i] * A + c]) << (8 * c);
-        wt[base + i] = w;
-      }
-      if (f16) {
-        const size_t b16 = wt16.size();
-        wt16.resize(b16 + wrows, 0xBCBCBCBCu);  // rows past the query: -2048
-        for (int i = 0; i < nr; ++i) {
-          uint32_t w = 0;
-          for (int c = 0; c < 4; ++c) {
-            uint8_t h;
-            f16_hi(m[b->query[r0 + i] * A + c], &h);
-            w |= (uint32_t)h << (8 * c);
-          }
-          wt16[b16 + i] = w;
-        }
-      }
-    } else {
-      std::vector<uint8_t> qp((size_t)(A + 1) * wPS, 0xFF);
-      for (int c = 0; c < A; ++c)
-        for (int i = 0; i < nr; ++i)
-          qp[(size_t)c * wPS + i] = (uint8_t)(S - m[b->query[r0 + i] * A + c]);
-      const size_t base = wt.size();
-      wt.resize(base + qp.size() / 4);
-      std::memcpy(wt.data() + base, qp.data(), qp.size());
-      if (f16) {
-        std::vector<uint16_t> q16((size_t)(A + 1) * wrows, 0xBC00u);
-        for (int c = 0; c < A; ++c)
-          for (int i = 0; i < nr; ++i)
-            q16[(size_t)c * wrows + i] =
-                f16_score_bits(m[b->query[r0 + i] * A + c]);
-        const size_t b16 = wt16.size();
-        wt16.resize(b16 + q16.size() / 2);
-        std::memcpy(wt16.data() + b16, q16.data(), q16.size() * 2);
-      }
-    }
+  wave_tables(wrows, wsegs, wt, wt16);
+  // split tail of the wave kernel (one segment, K >= 8): the query as P = 2 and 4 segments of
+  // K/P rows per lane, tables concatenated like the segments above
+  std::vector<uint32_t> st[2], st16[2];
+  int sK[2] = {0, 0};
+  for (int i = 0; i < 2; ++i) {
+    sK[i] = (wsegs == 1 && wK >= 8) ? wK / (2 << i) : 0;
+    if (sK[i]) wave_tables(64 * sK[i], 2 << i, st[i], st16[i]);
   }
   HIPOK(b, hipSetDevice(b->device));
   if (!b->ev_ready) {
@@ -885,7 +913,9 @@ static sw_status prepare(sw_bank* b) {
   }
   // the previous upload must have left the staging buffer before it is refilled
   HIPOK(b, hipEventSynchronize(b->ev_ready));
-  const size_t nbytes = (wt16.size() + wt.size() + tab.size() + tab16.size() + tpair.size()) * 4;
+  const size_t nbytes =
+      (wt16.size() + wt.size() + st16[0].size() + st[0].size() + st16[1].size() +
+       st[1].size() + tab.size() + tab16.size() + tpair.size()) * 4;
   HIPOK(b, b->stage.reserve(nbytes));
   // earlier launches (any stream) must be done reading the tables this upload overwrites
   HIPOK(b, hipStreamWaitEvent(b->stream, b->ev_used, 0));
@@ -906,6 +936,15 @@ static sw_status prepare(sw_bank* b) {
   b->wsegs = wsegs;
   b->wseg_words = wt.size() / wsegs;
   b->wseg_words16 = wt16.empty() ? 0 : wt16.size() / wsegs;
+  for (int i = 0; i < 2; ++i) {
+    if (!st16[i].empty()) HIPOK(b, upload(b->stab16[i], st16[i]));
+    HIPOK(b, upload(b->stab[i], st[i]));
+    b->sK[i] = sK[i];
+    b->sseg_words[i] = st[i].size() / (2 << i);
+    b->sseg_words16[i] = st16[i].size() / (2 << i);
+    b->sPS[i] = prof ? (uint32_t)(64 * sK[i]) : 0;
+    b->sPS16[i] = prof ? (uint32_t)(128 * sK[i]) : 0;
+  }
   HIPOK(b, upload(b->qtab, tab));
   if (f16) HIPOK(b, upload(b->qtab16, tab16));
   if (!tpair.empty()) HIPOK(b, upload(b->qpair, tpair));
@@ -1077,6 +1116,39 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
     // optimistic f16 with one query segment: the wave re-scores a flagged pair in u16 itself
     // (no flag kernel, no re-score launches)
     wave_fb = opt16 && b->wsegs == 1 && env_int("SWBANK_WAVE_FB", 1) != 0;
+    // Split tail: pairs beyond a whole number of waves per SIMD (one wave per pair, all
+    // resident) would put one more wave on some SIMDs and set the kernel's length; the last
+    // pairs % SIMDs pairs (when at most half the SIMDs) run instead as P row segments of K/P
+    // rows per lane each (P = 4 with 4 x that many waves, else 2), in the same launch.
+    // SWBANK_WAVE_SPLIT=0 disables, =N splits the last N pairs (tests); SWBANK_WAVE_SPLIT_P
+    // forces P.
+    SwkWaveSplit sp{};
+    const size_t pairs = (n + 1) / 2;
+    const int sforce = env_int("SWBANK_WAVE_SPLIT", -1);
+    if (b->sK[0] && b->wsegs == 1 && n == wspan && env_int("SWBANK_WAVE_BLOCK", 4) == 4 &&
+        pairs <= 0xFFFFFFFFull) {
+      const size_t simds = 4 * (size_t)std::max(b->cus, 1);
+      size_t T = 0;
+      if (sforce >= 0) T = std::min(pairs, (size_t)sforce);
+      else if (pairs >= simds && pairs % simds <= simds / 2) T = pairs % simds;
+      const int pforce = env_int("SWBANK_WAVE_SPLIT_P", 0);
+      const int i = pforce == 2 ? 0 : pforce == 4 ? 1 : (4 * T <= simds ? 1 : 0);
+      if (T && b->sK[i]) {
+        const unsigned P = 2u << i;
+        HIPOK(b, b->sring.reserve((T + 4 / P - 1) / (4 / P) * (4 / P) * (P - 1) * 256));
+        sp.pairs = (unsigned)T;
+        sp.P = P;
+        sp.qtab = use_f16 ? b->stab16[i].p : b->stab[i].p;
+        sp.words = (unsigned)(use_f16 ? b->sseg_words16[i] : b->sseg_words[i]);
+        sp.PS = use_f16 && b->prof ? b->sPS16[i] : b->sPS[i];
+        sp.fb_qtab = b->stab[i].p;
+        sp.fb_words = (unsigned)b->sseg_words[i];
+        sp.fb_PS = b->sPS[i];
+        sp.ring = b->sring.p;
+        const size_t L = strlen(b->last_kernel);
+        snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " split=%zu/%u", T, P);
+      }
+    }
     for (size_t p0 = 0; p0 < n; p0 += wspan) {
       const size_t np = std::min(wspan, n - p0);
       for (int sg = 0; sg < b->wsegs; ++sg) {
@@ -1090,7 +1162,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                      use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
                      use_f16 && b->prof ? b->wPS16 : b->wPS, b->pad, d_scores + p0,
                      (int)packed, wave_fb ? b->wtab.p : nullptr, b->nv, b->wPS,
-                     2048 - std::max(0, b->smax), st));
+                     2048 - std::max(0, b->smax), &sp, st));
       }
     }
   } else {

@@ -25,4 +25,17 @@
 /* 4-bit stream: 2 codes per byte, low nibble first (DNA chunks that hold an N). */
 #define SWK_PACK_NIBBLE 3u
 
+/* Wave kernel split tail (swk_launch_wave): the last `pairs` pairs run as P (2 or 4) row
+ * segments of K/P rows per lane, one wave each, each segment's bottom row handed down through
+ * `ring` (256 columns x 8 B per segment boundary and pair).  qtab / fb_qtab: the P segments'
+ * tables for the main pass and the u16 fallback, `words` / `fb_words` 32-bit words apart,
+ * letter strides PS / fb_PS bytes (profiles). */
+typedef struct SwkWaveSplit {
+  unsigned pairs, P;
+  const unsigned* qtab;
+  const unsigned* fb_qtab;
+  unsigned words, fb_words, PS, fb_PS;
+  void* ring;
+} SwkWaveSplit;
+
 #endif

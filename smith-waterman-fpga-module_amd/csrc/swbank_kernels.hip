@@ -542,6 +542,20 @@ struct ScoreArgs {
   const uint32_t* fb_qtab;
   uint32_t fb_nv, fb_PS;
   int32_t fb_thresh;
+  // wave kernel, split tail (K >= 8, one query segment): blocks [0, split_blocks) score pairs
+  // [main_pairs, main_pairs + 2 split_blocks) as two row segments of K/2 rows per lane, one wave
+  // per segment, the upper segment's bottom row handed to the lower one through split_ring (256
+  // columns x uint2 per pair) one 64-step phase apart; blocks past split_blocks score pairs
+  // [0, main_pairs) one wave per pair.  split_qtab / split_fb_qtab: the 2-segment tables (the
+  // main pass's arithmetic / the u16 fallback), segment stride split_words / split_fb_words
+  // 32-bit words, letter stride split_PS / split_fb_PS bytes.
+  uint32_t split_blocks;
+  uint32_t split_P;       // row segments per split pair: 2 or 4
+  uint32_t main_pairs;
+  const uint32_t* split_qtab;
+  const uint32_t* split_fb_qtab;
+  uint32_t split_words, split_fb_words, split_PS, split_fb_PS;
+  uint2* split_ring;
 };
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -1004,7 +1018,7 @@ static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, h
 // codes and boundary inputs, which leave the boundary state unchanged — no masking needed.
 template <int K>
 struct ProfLookupK {
-  uint32_t lo[K / 4], hi[K / 4];
+  uint32_t lo[(K + 3) / 4], hi[(K + 3) / 4];
   __device__ __forceinline__ u16x2 operator()(int r) const {
     const uint32_t sel = (uint32_t)(r & 3) | ((uint32_t)(4 + (r & 3)) << 16) | 0x0C000C00u;
     return as_u16x2(__builtin_amdgcn_perm(hi[r >> 2], lo[r >> 2], sel));
@@ -1094,6 +1108,17 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
       [t1] "+v"(Xl[1]), [t2] "+v"(Xl[2]), [t3] "+v"(Xl[3]), [Da] "+v"(Da), [Db] "=&v"(Db),     \
       [S1] "=&v"(S1), [best] "+v"(best)
 #define SWK_W4_OUT_M SWK_W4_HT, [X] "=&v"(X), [DN] "=&v"(DN), [IN] "=&v"(IN)
+// K = 2 (the split tail's quarter segments)
+#define SWK_W2_HT                                                                             \
+  [h0] "+v"(Hl[0]), [h1] "+v"(Hl[SWK_CLAMP(1, K)]), [t0] "+v"(Xl[0]),                          \
+      [t1] "+v"(Xl[SWK_CLAMP(1, K)]), [Da] "+v"(Da), [Db] "=&v"(Db), [S1] "=&v"(S1),             \
+      [best] "+v"(best)
+#define SWK_W2_OUT_M SWK_W2_HT, [X] "=&v"(X), [DN] "=&v"(DN), [IN] "=&v"(IN)
+#define SWK_W2_OUT_G SWK_W2_HT, [EN] "=&v"(X), [HN] "=&v"(DN), [FN] "=&v"(IN), [F] "+v"(up)
+#define SWK_W2_IN_LM [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [no] "s"(no), [up] "v"(up), [tb0] "v"(lk.lut[SWK_CLAMP(1, K)])
+#define SWK_W2_IN_LG [nv] "v"(lk.nv), [sel] "v"(lk.selw), [noe] "s"(noe), [ne] "s"(ne), [tb0] "v"(lk.lut[SWK_CLAMP(1, K)])
+#define SWK_W2_IN_PM [noe] "s"(noe), [ne] "s"(ne), [no] "s"(no), [up] "v"(up), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), [lo0] "v"(lk.lo[0]), [hi0] "v"(lk.hi[0])
+#define SWK_W2_IN_PG [noe] "s"(noe), [ne] "s"(ne), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), [lo0] "v"(lk.lo[0]), [hi0] "v"(lk.hi[0])
 #define SWK_W4_OUT_G SWK_W4_HT, [EN] "=&v"(X), [HN] "=&v"(DN), [FN] "=&v"(IN), [F] "+v"(up)
 #define SWK_W_OUT_G(B) SWK_W_HT(B), [EN] "=&v"(X), [HN] "=&v"(DN), [FN] "=&v"(IN), [F] "+v"(up)
 #define SWK_W_TB(B)                                                                           \
@@ -1134,7 +1159,13 @@ __device__ __forceinline__ void column_f16_lane_asm(const LK& lk, u16x2& diag_, 
         "v_pk_add_f16 %[Da], %[dg], %[Da] clamp"
         : [Da] "=&v"(Da)
         : [nv] "v"(lk.nv), [t0] "v"(lk.lut[0]), [sel] "v"(lk.selw), [dg] "v"(diag_));
-  if constexpr (K == 4) {
+  if constexpr (K == 2) {
+    if constexpr (GOTOH && PROF) asm volatile(SWK_F16G_P_L1_R2 : SWK_W2_OUT_G : SWK_W2_IN_PG);
+    else if constexpr (GOTOH)    asm volatile(SWK_F16G_L_L1_R2 : SWK_W2_OUT_G : SWK_W2_IN_LG);
+    else if constexpr (PROF)     asm volatile(SWK_F16M_P_Z0_L1_R2 : SWK_W2_OUT_M : SWK_W2_IN_PM);
+    else                         asm volatile(SWK_F16M_L_Z0_L1_R2 : SWK_W2_OUT_M : SWK_W2_IN_LM);
+    if constexpr (!GOTOH) up = Xl[SWK_CLAMP(1, K)];
+  } else if constexpr (K == 4) {
     if constexpr (GOTOH && PROF) asm volatile(SWK_F16G_P_L1_R4 : SWK_W4_OUT_G : SWK_W_IN_PG(0));
     else if constexpr (GOTOH)    asm volatile(SWK_F16G_L_L1_R4 : SWK_W4_OUT_G : SWK_W_IN_LG(0));
     else if constexpr (PROF)     asm volatile(SWK_F16M_P_Z0_L1_R4 : SWK_W4_OUT_M : SWK_W_IN_PM(0));
@@ -1177,10 +1208,17 @@ __device__ __forceinline__ uint32_t dpp_shr1_zero(uint32_t v) {  // lane 0 reads
 // qtab (wave layout): LUT: 64*K row words | PROF: (pad+1) x PS bytes, PS = 64*K (u16) or
 // 128*K (f16).  prof: the profile (PROF), in LDS for the main pass or in HBM for the u16
 // re-score of an optimistic f16 pass (the compiler emits ds_ or flat loads per call site).
-template <int K, bool COL0, bool PROF, bool GOTOH, bool F16>
+// SPLIT (the split tail): this wave is row segment `seg` of P of the pair; lin (the ring from
+// the segment above, none for seg 0) / lout (the ring to the segment below, none for the last)
+// hold 256 columns each, and the waves of the block run nph + 2(P - 1) phases of 64 steps
+// with one barrier each, segment s two phases behind segment s - 1: its first step of a phase
+// loads 64 ring columns that the segment above finished writing by the previous barrier.
+template <int K, bool COL0, bool PROF, bool GOTOH, bool F16, bool SPLIT = false>
 __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* prof,
                                            const uint32_t* qtab, uint32_t nv, uint32_t PSb,
-                                           size_t pair, int lane) {
+                                           size_t pair, int lane, const uint2* lin = nullptr,
+                                           uint2* lout = nullptr, int nph = 0, int seg = 0,
+                                           int P = 1) {
   const size_t tA = 2 * pair, tB = tA + 1;
   const size_t n = a.n;
   const bool packed = a.packed != SWK_PACK_BYTES, rec = a.packed == SWK_PACK_RECORDS;
@@ -1237,9 +1275,11 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
   // query segments (queries longer than 64K rows): lane 0 reads row -1 of this segment (the
   // previous segment's bottom row) from edge_in, lane 63 writes this segment's bottom row;
   // layout [pair][column] {H, G/T/F} of both targets
-  const bool seg_in = a.edge_in != nullptr, seg_out = a.edge_out != nullptr;
-  const uint2* ein = seg_in ? a.edge_in + pair * a.ecols : nullptr;
-  uint2* eout = seg_out ? a.edge_out + pair * a.ecols : nullptr;
+  const bool seg_in = SPLIT ? lin != nullptr : a.edge_in != nullptr;
+  const bool seg_out = SPLIT ? lout != nullptr : a.edge_out != nullptr;
+  const uint2* ein = SPLIT ? lin : seg_in ? a.edge_in + pair * a.ecols : nullptr;
+  uint2* eout = SPLIT ? lout : seg_out ? a.edge_out + pair * a.ecols : nullptr;
+  const uint32_t rmask = SPLIT ? 255u : ~0u;  // the split ring holds 256 columns
   uint2 ebuf = make_uint2(as_u32(H0), as_u32(X0));
 
   // two steps per iteration (the loop-carried values alternate registers instead of being
@@ -1261,7 +1301,7 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
         if (c < LB) y = pB[c];
       }
       buf = code_word(min(x, pad), min(y, pad));
-      if (SEG) ebuf = c < (uint32_t)Lmax ? ein[c] : make_uint2(as_u32(H0), as_u32(X0));
+      if (SEG) ebuf = c < (uint32_t)Lmax ? ein[c & rmask] : make_uint2(as_u32(H0), as_u32(X0));
     }
     const uint32_t inj = __builtin_amdgcn_readlane(buf, t & 63);
     u16x2 upH, upX;
@@ -1289,7 +1329,10 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
         ProfLookupK16<K> lk;
         const uint8_t* lds = prof;
         const uint32_t olo = let & 0xFFFFu, ohi = let >> 16;
-        if constexpr (K == 4) {
+        if constexpr (K == 2) {
+          lk.lo[0] = *reinterpret_cast<const uint32_t*>(lds + olo);
+          lk.hi[0] = *reinterpret_cast<const uint32_t*>(lds + ohi);
+        } else if constexpr (K == 4) {
           const uint2 x = *reinterpret_cast<const uint2*>(lds + olo);
           const uint2 y = *reinterpret_cast<const uint2*>(lds + ohi);
           lk.lo[0] = x.x; lk.lo[1] = x.y; lk.hi[0] = y.x; lk.hi[1] = y.y;
@@ -1318,7 +1361,10 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
     } else if constexpr (PROF) {
       ProfLookupK<K> lk;
       const uint32_t blo = let & 0xFFu, bhi = (let >> 16) & 0xFFu;
-      if constexpr (K == 4) {
+      if constexpr (K == 2) {  // 2 rows = 2 bytes
+        lk.lo[0] = *reinterpret_cast<const uint16_t*>(prow + __umul24(blo, PSb));
+        lk.hi[0] = *reinterpret_cast<const uint16_t*>(prow + __umul24(bhi, PSb));
+      } else if constexpr (K == 4) {
         lk.lo[0] = *reinterpret_cast<const uint32_t*>(prow + __umul24(blo, PSb));
         lk.hi[0] = *reinterpret_cast<const uint32_t*>(prow + __umul24(bhi, PSb));
       } else if constexpr (K == 8) {
@@ -1355,9 +1401,30 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
     asm volatile("" : "+v"(best));
     botH = as_u32(Hl[K - 1]);
     botX = as_u32(upX);
-    if (seg_out && lane == 63 && t >= 63 && t - 63 < Lmax) eout[t - 63] = make_uint2(botH, botX);
+    if (seg_out && lane == 63 && t >= 63 && t - 63 < Lmax)
+      eout[(uint32_t)(t - 63) & rmask] = make_uint2(botH, botX);
   };
-  if (seg_in) {
+  if constexpr (SPLIT) {
+    // every wave of the block takes part in every phase's barrier (wave-uniform branches)
+    const int lag = 2 * seg;
+    for (int ph = 0; ph < nph + 2 * (P - 1); ++ph) {
+      const int blk = ph - lag;
+      if (blk >= 0 && blk < nph) {
+        if (seg_in) {
+          for (int t = 64 * blk; t < 64 * blk + 64; t += 2) {
+            step(t, true, std::true_type{});
+            step(t + 1, false, std::true_type{});
+          }
+        } else {
+          for (int t = 64 * blk; t < 64 * blk + 64; t += 2) {
+            step(t, true, std::false_type{});
+            step(t + 1, false, std::false_type{});
+          }
+        }
+      }
+      __syncthreads();
+    }
+  } else if (seg_in) {
     for (int t = 0; t < nsteps; t += 2) {
       step(t, true, std::true_type{});
       step(t + 1, false, std::true_type{});
@@ -1382,11 +1449,105 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
   return make_uint2(bx, by);
 }
 
+// Split-tail block (4 waves): 4 / P pairs from main_pairs + (4 / P) blockIdx.x on, wave w
+// scoring row segment w % P of pair w / P at KS = K / P rows per lane (the main waves' K).  The
+// segments' bests combine through LDS; an optimistic f16 pass whose block holds a pair above
+// fb_thresh re-runs the whole block in u16 (a block-uniform choice: the barriers need every wave).
+template <int KS, int P, bool COL0, bool PROF, bool GOTOH, bool F16>
+__device__ __forceinline__ void wave_split_block(const ScoreArgs& a, uint32_t* smem, int lane) {
+  constexpr int PPB = 4 / P;  // pairs per block
+  uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int seg = wave % P;
+  const size_t n = a.n, first = (size_t)a.main_pairs + (size_t)PPB * blockIdx.x;
+  const size_t pair = first + wave / P;
+  const size_t npairs = (n + 1) / 2;
+  // the block's longest target -> phases (every wave runs the same number of barriers)
+  uint32_t L = 0;
+  if (lane < 2 * PPB) {
+    const size_t t = 2 * first + lane;
+    if (t < n)
+      L = a.packed == SWK_PACK_RECORDS ? record_len(a.res + t * SWB_RECORD) : a.lens[t];
+  }
+#pragma unroll
+  for (int off = 2; off >= 1; off >>= 1) L = max(L, (uint32_t)__shfl_xor((int)L, off));
+  const int nph = (int)((__builtin_amdgcn_readfirstlane(L) + 63 + 63) / 64);
+  // a wave whose pair lies past the batch end (an odd tail) still runs every barrier: it
+  // scores the block's first pair again and writes nothing
+  const bool real = pair < npairs;
+  const size_t p = real ? pair : first;
+  uint2* ring = a.split_ring + ((size_t)PPB * blockIdx.x + wave / P) * (P - 1) * 256;
+  const uint2* lin = seg > 0 ? ring + (seg - 1) * 256 : nullptr;
+  uint2* lout = seg < P - 1 ? ring + seg * 256 : nullptr;
+  if constexpr (PROF) {
+    const uint32_t words = P * a.split_words / 4;  // every segment's profile, 16 B at a time
+    const uint4* src = reinterpret_cast<const uint4*>(a.split_qtab);
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+      reinterpret_cast<uint4*>(prof)[i] = src[i];
+    __syncthreads();
+  }
+  const uint8_t* sprof = PROF ? prof + (size_t)seg * a.split_words * 4 : nullptr;
+  const uint32_t* sq = a.split_qtab + (size_t)seg * a.split_words;
+  uint2 b = wave_pair<KS, COL0, PROF, GOTOH, F16, true>(a, sprof, sq, a.nv, a.split_PS, p, lane,
+                                                         lin, lout, nph, seg, P);
+  // LDS is free again (the last phase ended with a barrier): combine the pair's segments
+  uint32_t blockmax = 0;
+  const auto combine = [&](uint2 v) -> uint2 {
+    if (lane == 0) {
+      smem[2 * wave] = v.x;
+      smem[2 * wave + 1] = v.y;
+    }
+    __syncthreads();
+    const int w0 = wave - seg;
+    uint2 r = make_uint2(0u, 0u);
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      r.x = max(r.x, smem[2 * (w0 + k)]);
+      r.y = max(r.y, smem[2 * (w0 + k) + 1]);
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = max(m, smem[k]);
+    blockmax = m;
+    __syncthreads();  // read before anyone rewrites the slots
+    return r;
+  };
+  b = combine(b);
+  if constexpr (F16) {
+    if (a.fb_qtab && (int32_t)blockmax > a.fb_thresh) {
+      const uint8_t* fprof = PROF ? reinterpret_cast<const uint8_t*>(a.split_fb_qtab) +
+                                        (size_t)seg * a.split_fb_words * 4
+                                  : nullptr;
+      b = wave_pair<KS, COL0, PROF, GOTOH, false, true>(
+          a, fprof, a.split_fb_qtab + (size_t)seg * a.split_fb_words, a.fb_nv, a.split_fb_PS, p,
+          lane, lin, lout, nph, seg, P);
+      b = combine(b);
+    }
+  }
+  if (lane == 0 && seg == 0 && real) {
+    const size_t tA = 2 * p, tB = tA + 1;
+    int32_t sa = (int32_t)b.x, sb = (int32_t)b.y;
+    if (a.accum) {
+      sa = max(sa, a.scores[tA]);
+      if (tB < n) sb = max(sb, a.scores[tB]);
+    }
+    a.scores[tA] = sa;
+    if (tB < n) a.scores[tB] = sb;
+  }
+}
+
 template <int K, bool COL0, bool PROF, bool GOTOH, bool F16>
 __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
   const int lane = threadIdx.x & 63;
+  if constexpr (K >= 8) {
+    if (blockIdx.x < a.split_blocks) {  // block-uniform
+      if (a.split_P == 4) wave_split_block<K / 4, 4, COL0, PROF, GOTOH, F16>(a, smem, lane);
+      else wave_split_block<K / 2, 2, COL0, PROF, GOTOH, F16>(a, smem, lane);
+      return;
+    }
+  }
   if constexpr (PROF) {
     const uint32_t words = (a.pad + 1) * a.PS / 16;
     const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
@@ -1394,11 +1555,11 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
       reinterpret_cast<uint4*>(prof)[i] = src[i];
     __syncthreads();
   }
-  const size_t pair = (size_t)blockIdx.x * (blockDim.x >> 6) +
+  const size_t pair = (size_t)(blockIdx.x - a.split_blocks) * (blockDim.x >> 6) +
                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const size_t tA = 2 * pair, tB = tA + 1;
   const size_t n = a.n;
-  if (tA >= n) return;  // whole wave
+  if (tA >= n || pair >= a.main_pairs) return;  // whole wave
   uint2 b = wave_pair<K, COL0, PROF, GOTOH, F16>(a, prof, a.qtab, a.nv, a.PS, pair, lane);
   if constexpr (F16) {
     // optimistic f16: a pair above 2048 - max(s) may have rounded; re-score it in u16 now
@@ -1420,13 +1581,17 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
 
 template <int K, bool COL0, bool PROF, bool GOTOH, bool F16>
 static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream_t st) {
-  const size_t pairs = (a.n + 1) / 2;
   // 4 waves (pairs) per block, sharing one LDS copy of the profile; SWBANK_WAVE_BLOCK=1..8
-  // for tuning (measured on 12.5k protein targets: 4 and 5 best, 8 -11 %, 2 -25 %)
+  // for tuning (measured on 12.5k protein targets: 4 and 5 best, 8 -11 %, 2 -25 %); a split
+  // tail (split_blocks > 0) needs 4-wave blocks
   const char* wenv = std::getenv("SWBANK_WAVE_BLOCK");
-  const unsigned wpb = wenv && *wenv ? (unsigned)std::min(std::max(std::atoi(wenv), 1), 8) : 4u;
-  const size_t blocks = (pairs + wpb - 1) / wpb;
-  const size_t lds = PROF ? prof_bytes : 0;
+  const unsigned wpb = a.split_blocks ? 4u
+                       : wenv && *wenv ? (unsigned)std::min(std::max(std::atoi(wenv), 1), 8)
+                                       : 4u;
+  const size_t blocks = a.split_blocks + ((size_t)a.main_pairs + wpb - 1) / wpb;
+  size_t lds = PROF ? prof_bytes : 0;
+  if (a.split_blocks)  // every segment's profile, or the 8 words of the segment combine
+    lds = std::max<size_t>(lds, PROF ? (size_t)a.split_words * 4 * a.split_P : 64);
   auto fn = &score_wave<K, COL0, PROF, GOTOH, F16>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -1592,13 +1757,33 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
                                       const uint32_t* qtab, uint32_t nv, uint32_t S, uint32_t O,
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
                                       int packed, const uint32_t* fb_qtab, uint32_t fb_nv,
-                                      uint32_t fb_PS, int32_t fb_thresh, hipStream_t st) {
+                                      uint32_t fb_PS, int32_t fb_thresh,
+                                      const SwkWaveSplit* split, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  const swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
-                         static_cast<const uint2*>(edge_in), static_cast<uint2*>(edge_out), ecols,
-                         (uint32_t)accum, (uint32_t)packed, nullptr, nullptr, 0u, nullptr, 0u, 0u,
-                         swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
-                         swk::f16_pair(-(int)O), fb_qtab, fb_nv, fb_PS, fb_thresh};
+  swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
+                   static_cast<const uint2*>(edge_in), static_cast<uint2*>(edge_out), ecols,
+                   (uint32_t)accum, (uint32_t)packed, nullptr, nullptr, 0u, nullptr, 0u, 0u,
+                   swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
+                   swk::f16_pair(-(int)O), fb_qtab, fb_nv, fb_PS, fb_thresh};
+  const size_t pairs = (n + 1) / 2;
+  a.main_pairs = (uint32_t)pairs;
+  if (split && split->pairs > 0) {
+    // the split tail is the last split->pairs pairs (K >= 8, one segment); with an odd count
+    // the last block's second pair lies past the batch end
+    if (K < 8 || edge_in || edge_out || accum || split->pairs > pairs || pairs > 0xFFFFFFFFull ||
+        (split->P != 2 && split->P != 4))
+      return hipErrorInvalidValue;
+    a.split_P = split->P;
+    a.split_blocks = (split->pairs + 4 / split->P - 1) / (4 / split->P);
+    a.main_pairs = (uint32_t)(pairs - split->pairs);
+    a.split_qtab = split->qtab;
+    a.split_fb_qtab = split->fb_qtab;
+    a.split_words = split->words;
+    a.split_fb_words = split->fb_words;
+    a.split_PS = split->PS;
+    a.split_fb_PS = split->fb_PS;
+    a.split_ring = static_cast<uint2*>(split->ring);
+  }
   const uint32_t prof_bytes = (pad + 1) * PS;
 #define SWK_WCASE(KK, C0, PF, GT)                                                         \
   if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                                 \
