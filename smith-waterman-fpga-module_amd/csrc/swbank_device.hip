@@ -25,6 +25,9 @@
 #if defined(__SSE2__)
 #include <emmintrin.h>
 #endif
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 
 #include "swbank.h"
 #include "swbank_internal.h"
@@ -1531,6 +1534,8 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     HIPOK(b, hipEventRecord(b->h2d_done[s], b->copy_stream));
     hipStream_t ks = overlap && (i & 1) ? b->stream2 : b->stream;
     HIPOK(b, hipStreamWaitEvent(ks, b->h2d_done[s], 0));
+    // the last chunk has no later launch to share the chip with: the whole GPU
+    if (overlap && i + 1 == chunks.size()) swk_set_occ_cap(0);
     if ((st = score(b->dslot[s].p, c, b->scores.p + c.c0, ks)) != SW_OK) return fail_sync(st);
     trace_mark("launched");
     HIPOK(b, hipEventRecord(b->kern_done[s], ks));
@@ -1656,6 +1661,66 @@ static inline uint32_t pack_4bit(const uint8_t* src, uint32_t l, uint8_t* dst) {
   return mx;
 }
 
+#if defined(__x86_64__)
+// AVX2 forms of the two packers (selected at run time when the host CPU has AVX2): 32 codes per
+// step.  2-bit: u8 pairs (c0 + 4 c1) by one multiply-add, u16 pairs into the byte
+// c0 + 4 c1 + 16 c2 + 64 c3 by a second, byte 0 of every dword gathered by a shuffle and a
+// dword permute.  4-bit: c0 + 16 c1 per u16 by one multiply-add, then a pack and a permute.
+// Codes past 3 (resp. 15) give garbage bytes, but the returned OR (max) rejects the chunk.
+__attribute__((target("avx2"))) static uint32_t pack_2bit_avx2(const uint8_t* src, uint32_t l,
+                                                               uint8_t* dst) {
+  uint32_t j = 0;
+  __m256i orv = _mm256_setzero_si256();
+  const __m256i w1 = _mm256_set1_epi16(0x0401), w2 = _mm256_set1_epi32(0x00100001);
+  const __m256i sh = _mm256_setr_epi8(0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                                      0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
+  const __m256i pd = _mm256_setr_epi32(0, 4, 1, 1, 1, 1, 1, 1);
+  for (; j + 32 <= l; j += 32) {
+    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + j));
+    orv = _mm256_or_si256(orv, v);
+    const __m256i u = _mm256_madd_epi16(_mm256_maddubs_epi16(v, w1), w2);
+    const __m256i x = _mm256_permutevar8x32_epi32(_mm256_shuffle_epi8(u, sh), pd);
+    _mm_storel_epi64(reinterpret_cast<__m128i*>(dst + j / 4), _mm256_castsi256_si128(x));
+  }
+  __m128i o = _mm_or_si128(_mm256_castsi256_si128(orv), _mm256_extracti128_si256(orv, 1));
+  o = _mm_or_si128(o, _mm_srli_si128(o, 8));
+  o = _mm_or_si128(o, _mm_srli_si128(o, 4));
+  o = _mm_or_si128(o, _mm_srli_si128(o, 2));
+  o = _mm_or_si128(o, _mm_srli_si128(o, 1));
+  return ((uint32_t)_mm_cvtsi128_si32(o) & 0xFFu) | pack_2bit(src + j, l - j, dst + j / 4);
+}
+
+__attribute__((target("avx2"))) static uint32_t pack_4bit_avx2(const uint8_t* src, uint32_t l,
+                                                               uint8_t* dst) {
+  uint32_t j = 0;
+  __m256i mv = _mm256_setzero_si256();
+  const __m256i w = _mm256_set1_epi16(0x1001);
+  for (; j + 32 <= l; j += 32) {
+    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + j));
+    mv = _mm256_max_epu8(mv, v);
+    const __m256i p = _mm256_maddubs_epi16(v, w);
+    const __m256i x = _mm256_permute4x64_epi64(_mm256_packus_epi16(p, p), 0x08);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + j / 2), _mm256_castsi256_si128(x));
+  }
+  __m128i m = _mm_max_epu8(_mm256_castsi256_si128(mv), _mm256_extracti128_si256(mv, 1));
+  m = _mm_max_epu8(m, _mm_srli_si128(m, 8));
+  m = _mm_max_epu8(m, _mm_srli_si128(m, 4));
+  m = _mm_max_epu8(m, _mm_srli_si128(m, 2));
+  m = _mm_max_epu8(m, _mm_srli_si128(m, 1));
+  return std::max((uint32_t)_mm_cvtsi128_si32(m) & 0xFFu, pack_4bit(src + j, l - j, dst + j / 2));
+}
+#endif
+
+typedef uint32_t (*PackFn)(const uint8_t*, uint32_t, uint8_t*);
+// the packers for this host (SWBANK_AVX2=0 keeps the SSE2 forms)
+static PackFn packer(int bits) {
+#if defined(__x86_64__)
+  static const bool avx2 = __builtin_cpu_supports("avx2") && env_int("SWBANK_AVX2", 1) != 0;
+  if (avx2) return bits == 2 ? pack_2bit_avx2 : pack_4bit_avx2;
+#endif
+  return bits == 2 ? pack_2bit : pack_4bit;
+}
+
 // True when launches for targets of at most max_len use no bank scratch (one query segment,
 // no optimistic f16 re-score list, no int32 re-score), so host-feeder chunks may run on two
 // streams (SWBANK_OVERLAP=0 disables).  Mirrors launch()'s choices.
@@ -1741,6 +1806,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   // DNA: the 2-bit stream while the chunks hold no N; from the first chunk with N on, the
   // 4-bit stream (2-bit attempts would be discarded packing passes where N is common)
   const bool dna_pack = b->alpha == SW_DNA_ALPHA && env_int("SWBANK_PACK2", 1) != 0;
+  const PackFn pack2fn = packer(2), pack4fn = packer(4);
   bool pack2 = dna_pack;
   HIPOK(b, hipSetDevice(b->device));
   std::vector<char> has_perm(chunks.size(), 0);
@@ -1813,7 +1879,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
         for (size_t i = std::min(cnt, p * step); i < std::min(cnt, (p + 1) * step); ++i) {
           const size_t k = c.c0 + i;
           const uint32_t l = lens[k];
-          orc |= pack_2bit(residues + offsets[k], l, codes + at);
+          orc |= pack2fn(residues + offsets[k], l, codes + at);
           so[i] = at;
           sl[i] = l;
           at += (l + 3) / 4;
@@ -1836,7 +1902,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
         for (size_t i = std::min(cnt, p * step); i < std::min(cnt, (p + 1) * step); ++i) {
           const size_t k = c.c0 + i;
           const uint32_t l = lens[k];
-          mx = std::max(mx, pack_4bit(residues + offsets[k], l, codes + at));
+          mx = std::max(mx, pack4fn(residues + offsets[k], l, codes + at));
           so[i] = at;
           sl[i] = l;
           at += (l + 1) / 2;
