@@ -42,6 +42,32 @@ __global__ void __launch_bounds__(256) k(uint32_t* out, uint32_t seed, unsigned 
         x = __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y),
                                           (h2){(_Float16)-3, (_Float16)-3});
         a[i] = __builtin_bit_cast(uint32_t, x);
+      } else if (KIND == 8) {  // chains 0-3: v_pk_add_f16 + v_pk_maximum3_f16, 4-7: f32 add + max
+        if (i < 4) {
+          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+          h2 x = __builtin_bit_cast(h2, a[i]), y = __builtin_bit_cast(h2, b);
+          x = x + (h2){(_Float16)1, (_Float16)1};
+          x = __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y),
+                                            (h2){(_Float16)-3, (_Float16)-3});
+          a[i] = __builtin_bit_cast(uint32_t, x);
+        } else {
+          float x = __builtin_bit_cast(float, a[i]);
+          x = __builtin_fmaxf(x + 1.5f, __builtin_bit_cast(float, b));
+          a[i] = __builtin_bit_cast(uint32_t, x);
+        }
+      } else if (KIND == 9) {  // f32 add with clamp (VOP3) + v_max3_f32
+        float x = __builtin_bit_cast(float, a[i]);
+        asm volatile("v_add_f32_e64 %0, %0, 0.5 clamp\n\tv_max3_f32 %0, %0, %1, %2"
+                     : "+v"(x) : "v"(b), "v"(a[(i + 1) & 7]));
+        a[i] = __builtin_bit_cast(uint32_t, x);
+      } else if (KIND == 10) {  // chains 0-3: v_max_u32 + v_add_u32, 4-7: f32 add + max
+        if (i < 4) {
+          a[i] = max(a[i], b) + 1u;
+        } else {
+          float x = __builtin_bit_cast(float, a[i]);
+          x = __builtin_fmaxf(x + 1.5f, __builtin_bit_cast(float, b));
+          a[i] = __builtin_bit_cast(uint32_t, x);
+        }
       } else if (KIND == 7) {  // v_max3_u32 + v_add_u32
         a[i] = max(max(a[i], b), b ^ 5u) + 1u;
       } else {  // v_pk_sub_u16 clamp + v_pk_add_u16
@@ -97,6 +123,9 @@ int main() {
     run<5>("v_fma_f32+v_fma_f32", blocks);
     run<6>("v_pk_add_f16+v_pk_maximum3_f16", blocks);
     run<7>("v_max3_u32+v_add_u32", blocks);
+    run<8>("mix: pk_f16 add+max3 (4 chains) | f32 add+max (4 chains)", blocks);
+    run<9>("v_add_f32_e64 clamp+v_max3_f32", blocks);
+    run<10>("mix: u32 max+add (4 chains) | f32 add+max (4 chains)", blocks);
   }
   return 0;
 }
