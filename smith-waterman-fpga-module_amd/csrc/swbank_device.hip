@@ -31,6 +31,7 @@
 
 #include "swbank.h"
 #include "swbank_internal.h"
+#include "swbank_pack.h"
 
 extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh, int f16);
 extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int f16,
@@ -295,6 +296,7 @@ struct sw_bank {
   hipEvent_t ev_s2 = nullptr;
   double host_pack_ms = 0;         // feeder gather time of host calls (with timing on)
   DevBuf<uint8_t> dslot[NSLOT];
+  DevBuf<uint32_t> sortscr[NSLOT];  // device sort scratch of each slot's chunk
   std::unique_ptr<HostPool> pool;
 
   // workspaces
@@ -567,6 +569,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   for (int i = 0; i < sw_bank::NSLOT; ++i) {
     b->hslot[i].release();
     b->dslot[i].release();
+    b->sortscr[i].release();
     if (b->h2d_done[i]) (void)hipEventDestroy(b->h2d_done[i]);
     if (b->kern_done[i]) (void)hipEventDestroy(b->kern_done[i]);
   }
@@ -1021,7 +1024,8 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                         hipStream_t st, uint32_t packed = SWK_PACK_BYTES,
                         const uint32_t* perm = nullptr,
                         const uint32_t* perm_n = nullptr, bool dsort = false,
-                        bool wait_prev = true) {
+                        bool wait_prev = true, uint32_t* sort_out = nullptr,
+                        uint32_t* sort_scr = nullptr) {
   // Past the 16-bit lanes (min(|q|, max|t|) * max(s) + max(s) > 65535) the 16-bit passes are
   // still exact for every pair scoring <= 65535 - max(s); the pairs above are re-scored by the
   // int32 kernel through an index list (swk_launch_i32).
@@ -1175,19 +1179,28 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   // A device batch (dsort) visits its targets longest first, sorted on the device, so every
   // tile holds similar lengths (a tile runs to its longest lane); SWBANK_DSORT=0 disables.
   const uint32_t* ident = nullptr;  // device sort: 1 when the lengths share one bin
-  if (dsort && !use_wave && !perm && packed == SWK_PACK_BYTES && ntiles > 1 &&
+  // (the host feeder passes a chunk's own order (n + 2 words in its slot) and sort scratch, so
+  // chunks on two streams do not share them)
+  if (dsort && !use_wave && !perm && packed != SWK_PACK_RECORDS && ntiles > 1 &&
       n <= 0xFFFFFFFFull && env_int("SWBANK_DSORT", 1) != 0) {
-    HIPOK(b, b->dperm.reserve(n + 2));
-    const size_t sw = swk_sort_scratch_bytes() / 4;
-    if (b->dsort.cap < sw) {  // zeroed once; the sort kernels leave it zeroed
-      HIPOK(b, b->dsort.reserve(sw));
-      HIPOK(b, hipMemsetAsync(b->dsort.p, 0, sw * 4, st));
+    uint32_t* order = sort_out;
+    if (!order) {
+      HIPOK(b, b->dperm.reserve(n + 2));
+      order = b->dperm.p;
     }
-    HIPOK(b, swk_sort_lens(d_lens, n, max_len, b->dperm.p, b->dperm.p + n, b->dperm.p + n + 1,
-                           b->dsort.p, st));
-    perm = b->dperm.p;
-    perm_n = b->dperm.p + n;
-    ident = b->dperm.p + n + 1;
+    uint32_t* scr = sort_scr;
+    if (!scr) {
+      const size_t sw = swk_sort_scratch_bytes() / 4;
+      if (b->dsort.cap < sw) {  // zeroed once; the sort kernels leave it zeroed
+        HIPOK(b, b->dsort.reserve(sw));
+        HIPOK(b, hipMemsetAsync(b->dsort.p, 0, sw * 4, st));
+      }
+      scr = b->dsort.p;
+    }
+    HIPOK(b, swk_sort_lens(d_lens, n, max_len, order, order + n, order + n + 1, scr, st));
+    perm = order;
+    perm_n = order + n;
+    ident = order + n + 1;
   }
   // Segmented queries hand each segment's bottom row to the next through HBM: ntiles x ecols
   // x 512 B per edge buffer.  Past SWBANK_EDGE_MB (default 2048) the batch runs as
@@ -1599,128 +1612,6 @@ static SlotTail slot_tail(size_t tail_at, size_t cnt) {
   return {tail_at, tail_at + cnt * 4, tail_at + cnt * 8};
 }
 
-// l code bytes -> ceil(l/4) bytes of 2-bit codes, 4 per byte LSB first (the CAPI host's
-// charTo2bit order, aligner_Header.c:25-40).  Returns the OR of all l codes: the packing is
-// valid only when it is <= 3 (a DNA chunk without N).
-static inline uint32_t pack_2bit(const uint8_t* src, uint32_t l, uint8_t* dst) {
-  uint32_t j = 0, orc = 0;
-#if defined(__SSE2__)
-  __m128i orv = _mm_setzero_si128();
-  const __m128i m16 = _mm_set1_epi16(0x000F), m32 = _mm_set1_epi32(0xFF);
-  for (; j + 16 <= l; j += 16) {  // 16 codes -> 4 bytes
-    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + j));
-    orv = _mm_or_si128(orv, v);
-    __m128i x = _mm_and_si128(_mm_or_si128(v, _mm_srli_epi16(v, 6)), m16);  // 2 codes / u16
-    x = _mm_and_si128(_mm_or_si128(x, _mm_srli_epi32(x, 12)), m32);        // 4 codes / u32
-    x = _mm_packus_epi16(_mm_packs_epi32(x, x), x);
-    const uint32_t w = (uint32_t)_mm_cvtsi128_si32(x);
-    std::memcpy(dst + j / 4, &w, 4);
-  }
-  orv = _mm_or_si128(orv, _mm_srli_si128(orv, 8));
-  orv = _mm_or_si128(orv, _mm_srli_si128(orv, 4));
-  orv = _mm_or_si128(orv, _mm_srli_si128(orv, 2));
-  orv = _mm_or_si128(orv, _mm_srli_si128(orv, 1));
-  orc = (uint32_t)_mm_cvtsi128_si32(orv) & 0xFFu;
-#endif
-  for (; j < l; j += 4) {
-    uint32_t byte = 0;
-    for (uint32_t t = 0; t < 4 && j + t < l; ++t) {
-      orc |= src[j + t];
-      byte |= (uint32_t)(src[j + t] & 3u) << (2 * t);
-    }
-    dst[j / 4] = (uint8_t)byte;
-  }
-  return orc;
-}
-
-// l code bytes -> ceil(l/2) bytes of 4-bit codes, low nibble first.  Returns the largest code
-// (the packing is valid when it is below the alphabet size, at most 15).
-static inline uint32_t pack_4bit(const uint8_t* src, uint32_t l, uint8_t* dst) {
-  uint32_t j = 0, mx = 0;
-#if defined(__SSE2__)
-  __m128i mv = _mm_setzero_si128();
-  const __m128i m16 = _mm_set1_epi16(0x00FF);
-  for (; j + 16 <= l; j += 16) {  // 16 codes -> 8 bytes
-    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + j));
-    mv = _mm_max_epu8(mv, v);
-    __m128i x = _mm_and_si128(_mm_or_si128(v, _mm_srli_epi16(v, 4)), m16);
-    x = _mm_packus_epi16(x, x);
-    _mm_storel_epi64(reinterpret_cast<__m128i*>(dst + j / 2), x);
-  }
-  mv = _mm_max_epu8(mv, _mm_srli_si128(mv, 8));
-  mv = _mm_max_epu8(mv, _mm_srli_si128(mv, 4));
-  mv = _mm_max_epu8(mv, _mm_srli_si128(mv, 2));
-  mv = _mm_max_epu8(mv, _mm_srli_si128(mv, 1));
-  mx = (uint32_t)_mm_cvtsi128_si32(mv) & 0xFFu;
-#endif
-  for (; j < l; j += 2) {
-    const uint32_t a = src[j], c = j + 1 < l ? src[j + 1] : 0u;
-    mx = std::max(mx, std::max(a, c));
-    dst[j / 2] = (uint8_t)((a & 15u) | (c & 15u) << 4);
-  }
-  return mx;
-}
-
-#if defined(__x86_64__)
-// AVX2 forms of the two packers (selected at run time when the host CPU has AVX2): 32 codes per
-// step.  2-bit: u8 pairs (c0 + 4 c1) by one multiply-add, u16 pairs into the byte
-// c0 + 4 c1 + 16 c2 + 64 c3 by a second, byte 0 of every dword gathered by a shuffle and a
-// dword permute.  4-bit: c0 + 16 c1 per u16 by one multiply-add, then a pack and a permute.
-// Codes past 3 (resp. 15) give garbage bytes, but the returned OR (max) rejects the chunk.
-__attribute__((target("avx2"))) static uint32_t pack_2bit_avx2(const uint8_t* src, uint32_t l,
-                                                               uint8_t* dst) {
-  uint32_t j = 0;
-  __m256i orv = _mm256_setzero_si256();
-  const __m256i w1 = _mm256_set1_epi16(0x0401), w2 = _mm256_set1_epi32(0x00100001);
-  const __m256i sh = _mm256_setr_epi8(0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
-                                      0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
-  const __m256i pd = _mm256_setr_epi32(0, 4, 1, 1, 1, 1, 1, 1);
-  for (; j + 32 <= l; j += 32) {
-    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + j));
-    orv = _mm256_or_si256(orv, v);
-    const __m256i u = _mm256_madd_epi16(_mm256_maddubs_epi16(v, w1), w2);
-    const __m256i x = _mm256_permutevar8x32_epi32(_mm256_shuffle_epi8(u, sh), pd);
-    _mm_storel_epi64(reinterpret_cast<__m128i*>(dst + j / 4), _mm256_castsi256_si128(x));
-  }
-  __m128i o = _mm_or_si128(_mm256_castsi256_si128(orv), _mm256_extracti128_si256(orv, 1));
-  o = _mm_or_si128(o, _mm_srli_si128(o, 8));
-  o = _mm_or_si128(o, _mm_srli_si128(o, 4));
-  o = _mm_or_si128(o, _mm_srli_si128(o, 2));
-  o = _mm_or_si128(o, _mm_srli_si128(o, 1));
-  return ((uint32_t)_mm_cvtsi128_si32(o) & 0xFFu) | pack_2bit(src + j, l - j, dst + j / 4);
-}
-
-__attribute__((target("avx2"))) static uint32_t pack_4bit_avx2(const uint8_t* src, uint32_t l,
-                                                               uint8_t* dst) {
-  uint32_t j = 0;
-  __m256i mv = _mm256_setzero_si256();
-  const __m256i w = _mm256_set1_epi16(0x1001);
-  for (; j + 32 <= l; j += 32) {
-    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + j));
-    mv = _mm256_max_epu8(mv, v);
-    const __m256i p = _mm256_maddubs_epi16(v, w);
-    const __m256i x = _mm256_permute4x64_epi64(_mm256_packus_epi16(p, p), 0x08);
-    _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + j / 2), _mm256_castsi256_si128(x));
-  }
-  __m128i m = _mm_max_epu8(_mm256_castsi256_si128(mv), _mm256_extracti128_si256(mv, 1));
-  m = _mm_max_epu8(m, _mm_srli_si128(m, 8));
-  m = _mm_max_epu8(m, _mm_srli_si128(m, 4));
-  m = _mm_max_epu8(m, _mm_srli_si128(m, 2));
-  m = _mm_max_epu8(m, _mm_srli_si128(m, 1));
-  return std::max((uint32_t)_mm_cvtsi128_si32(m) & 0xFFu, pack_4bit(src + j, l - j, dst + j / 2));
-}
-#endif
-
-typedef uint32_t (*PackFn)(const uint8_t*, uint32_t, uint8_t*);
-// the packers for this host (SWBANK_AVX2=0 keeps the SSE2 forms)
-static PackFn packer(int bits) {
-#if defined(__x86_64__)
-  static const bool avx2 = __builtin_cpu_supports("avx2") && env_int("SWBANK_AVX2", 1) != 0;
-  if (avx2) return bits == 2 ? pack_2bit_avx2 : pack_4bit_avx2;
-#endif
-  return bits == 2 ? pack_2bit : pack_4bit;
-}
-
 // True when launches for targets of at most max_len use no bank scratch (one query segment,
 // no optimistic f16 re-score list, no int32 re-score), so host-feeder chunks may run on two
 // streams (SWBANK_OVERLAP=0 disables).  Mirrors launch()'s choices.
@@ -1770,10 +1661,10 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   const size_t total = psum[P];
   const uint32_t max_len = *std::max_element(pmax.begin(), pmax.end());
   if (max_len && !residues) return fail(b, SW_ERR_ARG, "null residues");
-  // slot: offsets u64 | lens | perm | count (SlotTail) | codes at codes_at(cnt): one byte per
+  // slot: offsets u64 | lens | perm | count | ident (SlotTail) | codes at codes_at(cnt): one byte per
   // residue, or, for a DNA chunk without N, the 2-bit stream (a quarter of the PCIe bytes;
   // SWBANK_PACK2=0 disables), each target from a byte boundary, 16 zero bytes after the last
-  const auto codes_at = [](size_t cnt) { return align16(cnt * 16 + 4); };
+  const auto codes_at = [](size_t cnt) { return align16(cnt * 16 + 8); };
   std::vector<size_t> bounds = chunk_bounds(total);
   bounds.push_back(SIZE_MAX);  // sentinel
   std::vector<std::vector<std::pair<size_t, size_t>>> pcut(P);  // (end position, code prefix)
@@ -1806,13 +1697,28 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   // DNA: the 2-bit stream while the chunks hold no N; from the first chunk with N on, the
   // 4-bit stream (2-bit attempts would be discarded packing passes where N is common)
   const bool dna_pack = b->alpha == SW_DNA_ALPHA && env_int("SWBANK_PACK2", 1) != 0;
-  const PackFn pack2fn = packer(2), pack4fn = packer(4);
+  // AVX2 packers when the host has them (SWBANK_AVX2=0: the SSE2 forms); a target whose last
+  // 32-code step has 32 readable bytes and whose full-step stores (8 or 16 bytes per step) end
+  // inside its pool part's output packs its tail in the same vector step (swbank_pack.h): the
+  // bytes it stores past its own end belong to later targets of the same part, which rewrite
+  // them afterwards on the same thread
+  const bool avx2 = env_int("SWBANK_AVX2", 1) != 0;
+  const swpack::PackFn pack2fn = swpack::packer(2, avx2), pack4fn = swpack::packer(4, avx2);
+  const auto wide_ok = [&](size_t k, uint32_t l, size_t at, size_t step_bytes, size_t part_end) {
+    const size_t steps = (l + 31u) / 32u;
+    return offsets[k] + steps * 32 <= nres && at + steps * step_bytes <= part_end;
+  };
   bool pack2 = dna_pack;
   HIPOK(b, hipSetDevice(b->device));
   std::vector<char> has_perm(chunks.size(), 0);
+  // ragged chunks: longest-first order sorted on the device (the sort kernels of
+  // sw_score_batch_device, into the chunk's slot) instead of on the host; SWBANK_HOST_DSORT=0
+  // sorts on the host
+  std::vector<char> dev_sort(chunks.size(), 0);
+  const bool host_dsort = env_int("SWBANK_HOST_DSORT", 1) != 0 && env_int("SWBANK_DSORT", 1) != 0;
   std::vector<uint32_t> chunk_mode(chunks.size(), SWK_PACK_BYTES);
   std::vector<size_t> part(T + 1), part2(T + 1), part4(T + 1);
-  std::vector<uint32_t> partmax(T);
+  std::vector<uint32_t> partmax(T), partmin(T);
   std::atomic<size_t> bad{SIZE_MAX}, oob{SIZE_MAX};
   std::atomic<uint32_t> wide{0};
   size_t gi = 0, si = 0;
@@ -1831,7 +1737,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     oob = SIZE_MAX;
     pool.run([&](unsigned p) {
       size_t acc = 0, acc2 = 0, acc4 = 0;
-      uint32_t m = 0;
+      uint32_t m = 0, mn = UINT32_MAX;
       bool out = false;
       for (size_t k = c.c0 + std::min(cnt, p * step); k < c.c0 + std::min(cnt, (p + 1) * step);
            ++k) {
@@ -1839,6 +1745,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
         acc2 += (lens[k] + 3) / 4;
         acc4 += (lens[k] + 1) / 2;
         m = std::max(m, lens[k]);
+        mn = std::min(mn, lens[k]);
         // the target must lie inside the caller's residues (checked before any byte is read;
         // the pack passes below re-read this part's offsets from cache)
         out |= offsets[k] > nres || lens[k] > nres - offsets[k];
@@ -1856,6 +1763,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       part2[p + 1] = acc2;
       part4[p + 1] = acc4;
       partmax[p] = m;
+      partmin[p] = mn;
     });
     if (oob.load() != SIZE_MAX) {
       const size_t k = oob.load();
@@ -1863,6 +1771,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
            (unsigned long long)offsets[k], lens[k], nres);
       return 0;
     }
+    trace_mark("g-lens");
     chunk_max[gi] = *std::max_element(partmax.begin(), partmax.end());
     for (unsigned p = 0; p < T; ++p) {
       part[p + 1] += part[p];
@@ -1876,10 +1785,11 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       pool.run([&](unsigned p) {
         size_t at = part2[p];
         uint32_t orc = 0;
-        for (size_t i = std::min(cnt, p * step); i < std::min(cnt, (p + 1) * step); ++i) {
+        const size_t ie = std::min(cnt, (p + 1) * step);
+        for (size_t i = std::min(cnt, p * step); i < ie; ++i) {
           const size_t k = c.c0 + i;
           const uint32_t l = lens[k];
-          orc |= pack2fn(residues + offsets[k], l, codes + at);
+          orc |= pack2fn(residues + offsets[k], l, codes + at, wide_ok(k, l, at, 8, part2[p + 1]));
           so[i] = at;
           sl[i] = l;
           at += (l + 3) / 4;
@@ -1887,6 +1797,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
         if (orc > 3u) wide = 1;
       });
       two = wide.load() == 0;
+      trace_mark("g-pack2");
       if (two) {
         std::memset(codes + part2[T], 0, 16);  // a last chunk reads 1 byte past
         mode = SWK_PACK_STREAM;
@@ -1899,16 +1810,19 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       pool.run([&](unsigned p) {
         size_t at = part4[p];
         uint32_t mx = 0;
-        for (size_t i = std::min(cnt, p * step); i < std::min(cnt, (p + 1) * step); ++i) {
+        const size_t ie = std::min(cnt, (p + 1) * step);
+        for (size_t i = std::min(cnt, p * step); i < ie; ++i) {
           const size_t k = c.c0 + i;
           const uint32_t l = lens[k];
-          mx = std::max(mx, pack4fn(residues + offsets[k], l, codes + at));
+          mx = std::max(mx, pack4fn(residues + offsets[k], l, codes + at,
+                                    wide_ok(k, l, at, 16, part4[p + 1])));
           so[i] = at;
           sl[i] = l;
           at += (l + 1) / 2;
         }
         if (mx >= alpha) wide = 1;
       });
+      trace_mark("g-pack4");
       if (wide.load() == 0) {
         std::memset(codes + part4[T], 0, 16);  // a last chunk reads up to 3 bytes past
         mode = SWK_PACK_NIBBLE;
@@ -1947,7 +1861,13 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       }
     }
     chunk_mode[gi] = mode;
-    has_perm[gi++] = chunk_perm(pool, sl, cnt, reinterpret_cast<uint32_t*>(slot + tl.perm_at));
+    const bool uniform = *std::min_element(partmin.begin(), partmin.end()) == chunk_max[gi];
+    if (!uniform && host_dsort && cnt > SWB_TILE)
+      dev_sort[gi++] = 1;
+    else
+      has_perm[gi++] =
+          !uniform && chunk_perm(pool, sl, cnt, reinterpret_cast<uint32_t*>(slot + tl.perm_at));
+    trace_mark("g-perm");
     *reinterpret_cast<uint32_t*>(slot + tl.cnt_at) = (uint32_t)cnt;
     return ca + (mode == SWK_PACK_STREAM   ? align16(part2[T] + 16)
                  : mode == SWK_PACK_NIBBLE ? align16(part4[T] + 16)
@@ -1958,15 +1878,25 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                          hipStream_t ks) -> sw_status {
     const size_t cnt = c.c1 - c.c0;
     const SlotTail tl = slot_tail(cnt * 8, cnt);
-    const bool pm = has_perm[si];
+    const bool pm = has_perm[si], ds = dev_sort[si];
     const uint32_t mode = chunk_mode[si];
+    const int slot = (int)(si % sw_bank::NSLOT);
     const uint32_t ml = chunk_max[si++];
+    uint32_t* scr = nullptr;
+    if (ds) {  // the slot's own sort scratch, zeroed once (the sort kernels leave it zeroed)
+      const size_t sw = swk_sort_scratch_bytes() / 4;
+      if (b->sortscr[slot].cap < sw) {
+        HIPOK(b, b->sortscr[slot].reserve(sw));
+        HIPOK(b, hipMemset(b->sortscr[slot].p, 0, sw * 4));
+      }
+      scr = b->sortscr[slot].p;
+    }
     return launch(b, dslot + codes_at(cnt), reinterpret_cast<const uint64_t*>(dslot),
                   reinterpret_cast<const uint32_t*>(dslot + tl.lens_at), cnt, ml, d_scores,
                   ks, mode,
                   pm ? reinterpret_cast<const uint32_t*>(dslot + tl.perm_at) : nullptr,
-                  pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr, false,
-                  !overlap);
+                  pm ? reinterpret_cast<const uint32_t*>(dslot + tl.cnt_at) : nullptr, ds,
+                  !overlap, ds ? reinterpret_cast<uint32_t*>(dslot + tl.perm_at) : nullptr, scr);
   };
   return feed(b, n, chunks, gather, score, out, overlap);
 }

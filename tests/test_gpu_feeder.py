@@ -37,9 +37,13 @@ def _device_scores(bank, res, offs, lens):
     return d_sc.cpu().numpy()
 
 
+@pytest.mark.parametrize("host_dsort", ["1", "0"])
 @pytest.mark.parametrize("chunk_mb", ["1", "3"])
-def test_feeder_many_chunks_ragged(monkeypatch, chunk_mb):
+def test_feeder_many_chunks_ragged(monkeypatch, chunk_mb, host_dsort):
+    """ragged chunks visited longest first, the order sorted on the device into each chunk's
+    slot (SWBANK_HOST_DSORT=1, default) or on the host (0)"""
     monkeypatch.setenv("SWBANK_CHUNK_MB", chunk_mb)
+    monkeypatch.setenv("SWBANK_HOST_DSORT", host_dsort)
     rng = np.random.default_rng(11)
     res, offs, lens = _ragged(rng, 60000, 0, 220)  # ~6.6 MB of codes: 2-7 chunks
     q = rng.integers(0, 4, 100, dtype=np.uint8)
@@ -118,14 +122,16 @@ def test_feeder_records_many_chunks(monkeypatch):
         assert ei.value.status == S.ERR_ARG and "record 40000" in str(ei.value)
 
 
+@pytest.mark.parametrize("avx2", ["1", "0"])
 @pytest.mark.parametrize("case", ["merged", "gotoh", "profile", "long-query", "wave"])
-def test_feeder_two_bit_chunks(monkeypatch, case):
+def test_feeder_two_bit_chunks(monkeypatch, case, avx2):
     """DNA chunks without N cross PCIe as the 2-bit stream (SWK_PACK_STREAM, each target from
     a byte boundary); the chunk holding an N and those after it cross as 4-bit codes
     (SWK_PACK_NIBBLE).  Ragged lengths 0-300
     (every residue count mod 4/8/16, empty targets), N only in the middle of the batch, several
     chunks in flight: the scores equal the byte path's (SWBANK_PACK2=0) and the oracle's."""
     monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
+    monkeypatch.setenv("SWBANK_AVX2", avx2)
     if case == "profile":
         monkeypatch.setenv("SWBANK_PROFILE", "1")
     if case == "wave":
