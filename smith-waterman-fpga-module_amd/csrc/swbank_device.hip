@@ -42,7 +42,8 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
                                       int packed, const uint32_t* fb_qtab, uint32_t fb_nv,
                                       uint32_t fb_PS, int32_t fb_thresh,
-                                      const SwkWaveSplit* split, hipStream_t st);
+                                      const SwkWaveSplit* split, uint32_t ulen,
+                                      uint32_t ustride, hipStream_t st);
 extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh, int f16,
                                        const uint8_t* res, const uint64_t* offs,
                                        const uint32_t* lens, size_t n, const uint32_t* qtab,
@@ -52,7 +53,7 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        int accum, int packed, const uint32_t* idx,
                                        const uint32_t* nidx, uint32_t idx_base,
                                        const uint32_t* ident, int pair, uint32_t pS1,
-                                       uint32_t pS2, hipStream_t st);
+                                       uint32_t pS2, uint32_t ulen, uint32_t ustride, hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
                                    hipStream_t st);
@@ -1025,13 +1026,15 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                         const uint32_t* perm = nullptr,
                         const uint32_t* perm_n = nullptr, bool dsort = false,
                         bool wait_prev = true, uint32_t* sort_out = nullptr,
-                        uint32_t* sort_scr = nullptr) {
+                        uint32_t* sort_scr = nullptr, uint32_t ulen = 0, uint32_t ustride = 0) {
   // Past the 16-bit lanes (min(|q|, max|t|) * max(s) + max(s) > 65535) the 16-bit passes are
   // still exact for every pair scoring <= 65535 - max(s); the pairs above are re-scored by the
   // int32 kernel through an index list (swk_launch_i32).
   const uint64_t bound = std::min<uint64_t>(b->query.size(), max_len) *
                              (uint64_t)std::max(0, b->smax) + (uint64_t)std::max(0, b->smax);
   const bool need32 = bound > 65535u || env_int("SWBANK_I32", 0) != 0;
+  // a uniform batch (ustride != 0: no offset / length arrays) cannot feed the int32 kernel
+  if (need32 && ustride) return fail(b, SW_ERR_ARG, "uniform batch past the 16-bit bound");
   if (need32) {
     if (n > 0xFFFFFFFFull)
       return fail(b, SW_ERR_RANGE, "batches past the 16-bit score bound hold < 2^32 targets");
@@ -1169,7 +1172,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                      use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
                      use_f16 && b->prof ? b->wPS16 : b->wPS, b->pad, d_scores + p0,
                      (int)packed, wave_fb ? b->wtab.p : nullptr, b->nv, b->wPS,
-                     2048 - std::max(0, b->smax), &sp, st));
+                     2048 - std::max(0, b->smax), &sp, ulen, ustride, st));
       }
     }
   } else {
@@ -1263,7 +1266,8 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                                   pair ? b->pair_bytes : f16 && b->prof ? b->PS16 : b->PS,
                                   b->pad, b->segs[s].W, scores, ein, eout, ecols, s > 0 ? 1 : 0,
                                   (int)packed, idx, nidx, (uint32_t)p0,
-                                  pass == 0 ? ident : nullptr, pair ? 1 : 0, b->pS1, b->pS2, st));
+                                  pass == 0 ? ident : nullptr, pair ? 1 : 0, b->pS1, b->pS2,
+                                  ulen, ustride, st));
       }
     }
   }
@@ -1484,8 +1488,8 @@ struct Chunk {
   size_t c0, c1, bytes;
 };
 
-// Runs the feeder: gather(slot, chunk) fills the host slot and returns how many leading bytes
-// of it to copy (0: bad input, message set); they go to the device on the copy stream, score(dslot, chunk, d_scores) launches the
+// Runs the feeder: gather(slot, chunk, from) fills the host slot and returns how many leading
+// bytes of it to copy, from byte `from` on (0: bad input, message set); they go to the device on the copy stream, score(dslot, chunk, d_scores) launches the
 // kernel on the bank stream; the scores come back to the pinned hscores in input order.
 // out != nullptr: every chunk's scores go back to the pinned hscores on out_stream right after
 // its kernel (beside the next chunk's kernel on the bank stream) and are copied into out in
@@ -1534,7 +1538,8 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     if (i >= (size_t)sw_bank::NSLOT) HIPOK(b, hipEventSynchronize(b->h2d_done[s]));
     trace_mark("gather<");
     const auto t0 = std::chrono::steady_clock::now();
-    const size_t bytes = gather(b->hslot[s].p, c);
+    size_t from = 0;  // leading slot bytes the device does not need (a uniform chunk's headers)
+    const size_t bytes = gather(b->hslot[s].p, c, from);
     trace_mark("gather>");
     if (b->timing)
       b->host_pack_ms +=
@@ -1542,8 +1547,8 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     if (bytes == 0) return fail_sync(SW_ERR_ARG);
     if (i >= (size_t)sw_bank::NSLOT)
       HIPOK(b, hipStreamWaitEvent(b->copy_stream, b->kern_done[s], 0));
-    HIPOK(b, hipMemcpyAsync(b->dslot[s].p, b->hslot[s].p, bytes, hipMemcpyHostToDevice,
-                            b->copy_stream));
+    HIPOK(b, hipMemcpyAsync(b->dslot[s].p + from, b->hslot[s].p + from, bytes - from,
+                            hipMemcpyHostToDevice, b->copy_stream));
     HIPOK(b, hipEventRecord(b->h2d_done[s], b->copy_stream));
     hipStream_t ks = overlap && (i & 1) ? b->stream2 : b->stream;
     HIPOK(b, hipStreamWaitEvent(ks, b->h2d_done[s], 0));
@@ -1717,12 +1722,19 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   std::vector<char> dev_sort(chunks.size(), 0);
   const bool host_dsort = env_int("SWBANK_HOST_DSORT", 1) != 0 && env_int("SWBANK_DSORT", 1) != 0;
   std::vector<uint32_t> chunk_mode(chunks.size(), SWK_PACK_BYTES);
+  // equal-length chunks cross PCIe without the per-target offsets and lengths (the kernels
+  // compute them: ScoreArgs.ulen / ustride) unless the int32 re-score would need them;
+  // SWBANK_UNIFORM=0 always sends them
+  std::vector<uint32_t> chunk_stride(chunks.size(), 0);
+  const uint64_t smax0 = (uint64_t)std::max(0, b->smax);
+  const bool uni_ok = env_int("SWBANK_UNIFORM", 1) != 0 && env_int("SWBANK_I32", 0) == 0 &&
+                      std::min<uint64_t>(b->query.size(), max_len) * smax0 + smax0 <= 65535u;
   std::vector<size_t> part(T + 1), part2(T + 1), part4(T + 1);
   std::vector<uint32_t> partmax(T), partmin(T);
   std::atomic<size_t> bad{SIZE_MAX}, oob{SIZE_MAX};
   std::atomic<uint32_t> wide{0};
   size_t gi = 0, si = 0;
-  const auto gather = [&](uint8_t* slot, const Chunk& c) -> size_t {
+  const auto gather = [&](uint8_t* slot, const Chunk& c, size_t& from) -> size_t {
     const size_t cnt = c.c1 - c.c0, ca = codes_at(cnt);
     const SlotTail tl = slot_tail(cnt * 8, cnt);
     uint64_t* so = reinterpret_cast<uint64_t*>(slot);
@@ -1773,6 +1785,8 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     }
     trace_mark("g-lens");
     chunk_max[gi] = *std::max_element(partmax.begin(), partmax.end());
+    const uint32_t chunk_min = *std::min_element(partmin.begin(), partmin.end());
+    const bool uni = uni_ok && chunk_min == chunk_max[gi] && chunk_min > 0;
     for (unsigned p = 0; p < T; ++p) {
       part[p + 1] += part[p];
       part2[p + 1] += part2[p];
@@ -1790,8 +1804,10 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
           const size_t k = c.c0 + i;
           const uint32_t l = lens[k];
           orc |= pack2fn(residues + offsets[k], l, codes + at, wide_ok(k, l, at, 8, part2[p + 1]));
-          so[i] = at;
-          sl[i] = l;
+          if (!uni) {
+            so[i] = at;
+            sl[i] = l;
+          }
           at += (l + 3) / 4;
         }
         if (orc > 3u) wide = 1;
@@ -1816,8 +1832,10 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
           const uint32_t l = lens[k];
           mx = std::max(mx, pack4fn(residues + offsets[k], l, codes + at,
                                     wide_ok(k, l, at, 16, part4[p + 1])));
-          so[i] = at;
-          sl[i] = l;
+          if (!uni) {
+            so[i] = at;
+            sl[i] = l;
+          }
           at += (l + 1) / 2;
         }
         if (mx >= alpha) wide = 1;
@@ -1861,7 +1879,13 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       }
     }
     chunk_mode[gi] = mode;
-    const bool uniform = *std::min_element(partmin.begin(), partmin.end()) == chunk_max[gi];
+    if (uni) {  // the device needs the codes only
+      from = ca;
+      chunk_stride[gi] = mode == SWK_PACK_STREAM   ? (chunk_max[gi] + 3) / 4
+                         : mode == SWK_PACK_NIBBLE ? (chunk_max[gi] + 1) / 2
+                                                   : chunk_max[gi];
+    }
+    const bool uniform = chunk_min == chunk_max[gi];
     if (!uniform && host_dsort && cnt > SWB_TILE)
       dev_sort[gi++] = 1;
     else
@@ -1879,7 +1903,7 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     const size_t cnt = c.c1 - c.c0;
     const SlotTail tl = slot_tail(cnt * 8, cnt);
     const bool pm = has_perm[si], ds = dev_sort[si];
-    const uint32_t mode = chunk_mode[si];
+    const uint32_t mode = chunk_mode[si], ustride = chunk_stride[si];
     const int slot = (int)(si % sw_bank::NSLOT);
     const uint32_t ml = chunk_max[si++];
     uint32_t* scr = nullptr;
@@ -1891,6 +1915,9 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       }
       scr = b->sortscr[slot].p;
     }
+    if (ustride)
+      return launch(b, dslot + codes_at(cnt), nullptr, nullptr, cnt, ml, d_scores, ks, mode,
+                    nullptr, nullptr, false, !overlap, nullptr, nullptr, ml, ustride);
     return launch(b, dslot + codes_at(cnt), reinterpret_cast<const uint64_t*>(dslot),
                   reinterpret_cast<const uint32_t*>(dslot + tl.lens_at), cnt, ml, d_scores,
                   ks, mode,
@@ -1963,7 +1990,7 @@ static sw_status records_feed(sw_bank* b, const uint8_t* recs, size_t n, int32_t
   std::atomic<size_t> bad{SIZE_MAX};
   std::atomic<uint32_t> cmax{0};
   size_t gi = 0, si = 0;
-  const auto gather = [&](uint8_t* slot, const Chunk& c) -> size_t {
+  const auto gather = [&](uint8_t* slot, const Chunk& c, size_t&) -> size_t {
     const size_t cnt = c.c1 - c.c0;
     const SlotTail tl = slot_tail(cnt * SWB_RECORD, cnt);
     uint32_t* sl = reinterpret_cast<uint32_t*>(slot + tl.lens_at);

@@ -453,7 +453,8 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint3
 // optimistic f16 pass flagged).
 __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t* offs,
                                               const uint32_t* lens, size_t n, int tile, int lane,
-                                              uint32_t packed, const uint32_t* idx) {
+                                              uint32_t packed, const uint32_t* idx,
+                                              uint32_t ulen, uint32_t ustride) {
   Lane2 t;
   size_t a = (size_t)tile * SWB_TILE + lane, b = a + 64;
   const bool va = a < n, vb = b < n;  // positions in the batch
@@ -465,7 +466,8 @@ __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t
   const size_t p0 = (size_t)tile * SWB_TILE;
   if (p0 >= n) {
     t.llo = t.lhi = 0u;
-    t.plo = t.phi = packed == SWK_PACK_RECORDS ? res + 6 : reinterpret_cast<const uint8_t*>(lens);
+    t.plo = t.phi = packed == SWK_PACK_RECORDS || ustride ? res + (packed ? 6 : 0)
+                                                          : reinterpret_cast<const uint8_t*>(lens);
     return t;
   }
   if (!va) a = p0;
@@ -479,6 +481,13 @@ __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t
     t.lhi = vb ? record_len(res + b * SWB_RECORD) : 0u;
     t.plo = res + a * SWB_RECORD + 6;
     t.phi = res + b * SWB_RECORD + 6;
+    return t;
+  }
+  if (ustride) {
+    t.llo = va ? ulen : 0u;
+    t.lhi = vb ? ulen : 0u;
+    t.plo = res + a * ustride;
+    t.phi = res + b * ustride;
     return t;
   }
   const uint32_t la = lens[a], lb = lens[b];
@@ -556,6 +565,10 @@ struct ScoreArgs {
   const uint32_t* split_fb_qtab;
   uint32_t split_words, split_fb_words, split_PS, split_fb_PS;
   uint2* split_ring;
+  // uniform batch (ustride != 0): every target is ulen codes long and target k starts at byte
+  // k * ustride of res; offs and lens are not read (the host feeder's equal-length chunks
+  // cross PCIe without per-target headers)
+  uint32_t ulen, ustride;
 };
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -572,10 +585,12 @@ __device__ __forceinline__ void dma_edge_chunk(const uint2* src, uint2* dst, int
 
 // Chunk count of a tile (uniform), from the lengths alone.
 __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens, size_t n,
-                                        int tile, int lane, uint32_t packed, const uint32_t* idx) {
+                                        int tile, int lane, uint32_t packed, const uint32_t* idx,
+                                        uint32_t ulen, uint32_t ustride) {
   const size_t a = (size_t)tile * SWB_TILE + lane, b = a + 64;
   auto len = [&](size_t k) -> uint32_t {
     if (k >= n) return 0u;
+    if (ustride) return ulen;
     if (idx) k = idx[k];
     return packed == SWK_PACK_RECORDS ? record_len(res + k * SWB_RECORD) : lens[k];
   };
@@ -631,10 +646,10 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   int total = 0;  // chunks of all this workgroup's tiles: every wave runs total + W - 1 phases
   const uint32_t packed = a.packed;
   for (int t = blockIdx.x; t < ntiles; t += G)
-    total += tile_nch(a.res, a.lens, n, t, lane, packed, idx);
+    total += tile_nch(a.res, a.lens, n, t, lane, packed, idx, a.ulen, a.ustride);
 
   int tile = blockIdx.x;
-  Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, idx);
+  Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen, a.ustride);
   int nch, nfull;
   tile_chunks(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
               nfull);
@@ -747,7 +762,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       if (!last) {
         load_raw(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
       } else if (ntile < ntiles) {  // first chunk of the next tile
-        cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed, idx);
+        cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed, idx, a.ulen,
+                           a.ustride);
         tile_chunks(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
                     n, nch_n, nfull_n);
         load_raw(cur, 0, nfull_n > 0, a.pad, packed, rlo, rhi);
@@ -1223,11 +1239,18 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
   const size_t n = a.n;
   const bool packed = a.packed != SWK_PACK_BYTES, rec = a.packed == SWK_PACK_RECORDS;
   const bool nib = a.packed == SWK_PACK_NIBBLE;
-  const uint32_t LA = rec ? record_len(a.res + tA * SWB_RECORD) : a.lens[tA];
-  const uint32_t LB = tB >= n ? 0u : rec ? record_len(a.res + tB * SWB_RECORD) : a.lens[tB];
-  const uint8_t* pA = rec ? a.res + tA * SWB_RECORD + 6 : a.res + (LA ? a.offs[tA] : 0);
+  const bool uni = a.ustride != 0;
+  const uint32_t LA = rec ? record_len(a.res + tA * SWB_RECORD) : uni ? a.ulen : a.lens[tA];
+  const uint32_t LB = tB >= n ? 0u
+                      : rec ? record_len(a.res + tB * SWB_RECORD)
+                      : uni ? a.ulen
+                            : a.lens[tB];
+  const uint8_t* pA = rec ? a.res + tA * SWB_RECORD + 6
+                      : uni ? a.res + tA * a.ustride
+                            : a.res + (LA ? a.offs[tA] : 0);
   const uint8_t* pB = rec ? a.res + (tB < n ? tB : tA) * SWB_RECORD + 6
-                          : a.res + (LB ? a.offs[tB] : 0);
+                      : uni ? a.res + (tB < n ? tB : tA) * a.ustride
+                            : a.res + (LB ? a.offs[tB] : 0);
   const int Lmax = (int)__builtin_amdgcn_readfirstlane(max(LA, LB));
   const uint32_t S = a.S, pad = a.pad;
   const u16x2 S2 = {(unsigned short)S, (unsigned short)S};
@@ -1467,7 +1490,9 @@ __device__ __forceinline__ void wave_split_block(const ScoreArgs& a, uint32_t* s
   if (lane < 2 * PPB) {
     const size_t t = 2 * first + lane;
     if (t < n)
-      L = a.packed == SWK_PACK_RECORDS ? record_len(a.res + t * SWB_RECORD) : a.lens[t];
+      L = a.packed == SWK_PACK_RECORDS ? record_len(a.res + t * SWB_RECORD)
+          : a.ustride                     ? a.ulen
+                                          : a.lens[t];
   }
 #pragma unroll
   for (int off = 2; off >= 1; off >>= 1) L = max(L, (uint32_t)__shfl_xor((int)L, off));
@@ -1639,14 +1664,17 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        int accum, int packed, const uint32_t* idx,
                                        const uint32_t* nidx, uint32_t idx_base,
                                        const uint32_t* ident, int pair, uint32_t pS1,
-                                       uint32_t pS2, hipStream_t st) {
+                                       uint32_t pS2, uint32_t ulen, uint32_t ustride,
+                                       hipStream_t st) {
   if (n == 0) return hipSuccess;
-  const swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
-                         O,    E,    PS,   pad, scores, static_cast<const uint2*>(edge_in),
-                         static_cast<uint2*>(edge_out), ecols, (uint32_t)accum, (uint32_t)packed,
-                         idx, nidx, idx_base, ident, pS1, pS2,
-                         swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
-                         swk::f16_pair(-(int)O), nullptr, 0u, 0u, 0};
+  swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
+                   O,    E,    PS,   pad, scores, static_cast<const uint2*>(edge_in),
+                   static_cast<uint2*>(edge_out), ecols, (uint32_t)accum, (uint32_t)packed,
+                   idx, nidx, idx_base, ident, pS1, pS2,
+                   swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
+                   swk::f16_pair(-(int)O), nullptr, 0u, 0u, 0};
+  a.ulen = ulen;
+  a.ustride = ustride;
   const uint32_t prof_bytes = (pad + 1) * PS;
   if (pair) {  // PS = pair-table bytes
     if (R == 32 && f16 && !prof && !gotoh && !col0)
@@ -1758,13 +1786,16 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
                                       uint32_t E, uint32_t PS, uint32_t pad, int32_t* scores,
                                       int packed, const uint32_t* fb_qtab, uint32_t fb_nv,
                                       uint32_t fb_PS, int32_t fb_thresh,
-                                      const SwkWaveSplit* split, hipStream_t st) {
+                                      const SwkWaveSplit* split, uint32_t ulen,
+                                      uint32_t ustride, hipStream_t st) {
   if (n == 0) return hipSuccess;
   swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
                    static_cast<const uint2*>(edge_in), static_cast<uint2*>(edge_out), ecols,
                    (uint32_t)accum, (uint32_t)packed, nullptr, nullptr, 0u, nullptr, 0u, 0u,
                    swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
                    swk::f16_pair(-(int)O), fb_qtab, fb_nv, fb_PS, fb_thresh};
+  a.ulen = ulen;
+  a.ustride = ustride;
   const size_t pairs = (n + 1) / 2;
   a.main_pairs = (uint32_t)pairs;
   if (split && split->pairs > 0) {

@@ -159,3 +159,50 @@ def test_feeder_two_bit_chunks(monkeypatch, case, avx2):
     want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(*params[:2]), *params[2:],
                          O.GAP_GOTOH if gotoh else O.GAP_MERGED)
     assert np.array_equal(got[sel], want), kern
+
+
+@pytest.mark.parametrize("case", ["2bit", "nibble", "protein", "wave", "long-query", "opt16"])
+def test_feeder_uniform_chunks(monkeypatch, case):
+    """Equal-length chunks cross PCIe as codes only (no per-target offsets / lengths: the
+    kernels compute them from the chunk's length and stride); the scores equal the headers path
+    (SWBANK_UNIFORM=0) and the oracle's, for 2-bit, 4-bit and byte chunks, both kernels, a
+    segmented query and an optimistic f16 pass with its u16 re-score."""
+    monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
+    rng = np.random.default_rng(len(case) * 31)
+    prot = case == "protein"
+    A = 20 if prot else 4
+    L = {"long-query": 90, "opt16": 300}.get(case, 133)
+    n = 20000
+    lens = np.full(n, L, np.uint32)
+    offs = np.arange(n, dtype=np.uint64) * L
+    res = rng.integers(0, A, n * L, dtype=np.uint8)
+    if case == "nibble":
+        res[rng.random(res.size) < 0.01] = 4
+    if case == "wave":
+        monkeypatch.setenv("SWBANK_KERNEL", "wave")
+    qlen = {"long-query": 1100, "opt16": 600}.get(case, 100)
+    q = rng.integers(0, A, qlen, dtype=np.uint8)
+    if case == "opt16":  # near-copies of the query: scores far past 2048 (u16 re-score)
+        for k in range(0, n, 97):
+            res[k * L:(k + 1) * L] = q[:L]
+    kw = dict(alphabet=S.ALPHABET_PROTEIN, gap_model=S.GAP_GOTOH) if prot else {}
+    with S.ScoreBank(**kw) as bank:
+        if prot:
+            bank.set_matrix(O.BLOSUM62, -11, -1)
+        else:
+            bank.set_penalties(*REF)
+        bank.load_query(q)
+        got = bank.score_batch(res, offs, lens)
+        kern = bank.last_kernel()
+        monkeypatch.setenv("SWBANK_UNIFORM", "0")
+        ref = bank.score_batch(res, offs, lens)
+    assert np.array_equal(got, ref), kern
+    sel = rng.choice(n, 400, replace=False)
+    if case == "opt16":
+        sel = np.concatenate([sel, np.arange(0, n, 97)[:60]])
+    sub = [res[int(offs[k]):int(offs[k]) + L] for k in sel]
+    if prot:
+        want = O.score_batch(q, *S.pack_targets(sub), O.BLOSUM62, -11, -1, O.GAP_GOTOH)
+    else:
+        want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(*REF[:2]), *REF[2:])
+    assert np.array_equal(got[sel], want), kern
