@@ -136,7 +136,9 @@ sw_status sw_score_batch(sw_bank *bank, const uint8_t *residues, size_t residues
  * lengths differ, then longest first (an on-device length sort).  d_scores receives int32
  * scores in input order.  With d_ids (device, may be NULL) the call also records the batch's
  * best hit on the device (sw_batch_best); without, it records nothing.  Nothing is copied to
- * or from the host.  Single-device banks only (SW_ERR_UNSUPPORTED on a multi-device bank). */
+ * or from the host.  Single-device banks only (SW_ERR_UNSUPPORTED on a multi-device bank).
+ * Device memory is not validated: the caller keeps every target inside d_residues
+ * (d_offsets[k] + d_lens[k] <= its size) and every d_lens[k] <= max_len. */
 sw_status sw_score_batch_device(sw_bank *bank, const uint8_t *d_residues,
                                 const uint64_t *d_offsets, const uint32_t *d_lens,
                                 const uint64_t *d_ids, size_t n, uint32_t max_len,

@@ -278,19 +278,23 @@ def score_pairs(qres, qoffs, qlens, tres, toffs, tlens, qidx, tidx, sub, go, ge,
 
 # ---------------------------------------------------------------------------------------
 # seeded synthetic workloads (splitmix64, shared with bench.py so both draw the same data)
-def splitmix64_bytes(seed: int, n: int) -> np.ndarray:
-    """n pseudo-random bytes from a splitmix64 stream (vectorised, deterministic)."""
-    words = (n + 7) // 8
-    idx = np.arange(1, words + 1, dtype=np.uint64)
+def splitmix64_bytes(seed: int, n: int, start: int = 0) -> np.ndarray:
+    """Bytes [start, start + n) of a splitmix64 stream (vectorised, deterministic; word i of the
+    stream depends on i alone, so any window is generated without its prefix)."""
+    w0 = start // 8
+    words = (start + n + 7) // 8 - w0
+    idx = np.arange(w0 + 1, w0 + words + 1, dtype=np.uint64)
     with np.errstate(over="ignore"):
         z = np.uint64(seed) + idx * np.uint64(0x9E3779B97F4A7C15)
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
-    return z.view(np.uint8)[:n].copy()
+    o = start - 8 * w0
+    return z.view(np.uint8)[o:o + n].copy()
 
 
-def random_codes(seed: int, n: int, alpha: int) -> np.ndarray:
-    """Uniform i.i.d. codes in [0, alpha) (like data/generate.py:7,13, but seeded)."""
-    b = splitmix64_bytes(seed, n).astype(np.uint32)
+def random_codes(seed: int, n: int, alpha: int, start: int = 0) -> np.ndarray:
+    """Uniform i.i.d. codes in [0, alpha) (like data/generate.py:7,13, but seeded): codes
+    [start, start + n) of the seed's stream."""
+    b = splitmix64_bytes(seed, n, start).astype(np.uint32)
     return (b * alpha >> 8).astype(np.uint8)

@@ -185,3 +185,11 @@ def test_splitmix_workload_is_deterministic():
     assert (a == b).all() and a.max() == 3 and a.min() == 0
     counts = np.bincount(a, minlength=4)
     assert counts.min() > 200
+
+
+def test_random_codes_windows():
+    """The seeded code stream is counter-based: any window equals the slice of the whole
+    stream (bench.py regenerates the rows it re-checks, e.g. a batch's last targets)."""
+    whole = O.random_codes(4242, 5000, 20)
+    for start, n in [(0, 10), (1, 7), (8, 64), (13, 1000), (4990, 10)]:
+        assert (O.random_codes(4242, n, 20, start=start) == whole[start:start + n]).all()
