@@ -12,10 +12,15 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["tile", "tile-u16", "wave", "wave-u16"])
+@pytest.fixture(autouse=True, params=["tile", "tile-u16", "wave", "wave-u16", "wave-split",
+                                      "wave-split-u16"])
 def kernel_choice(request, monkeypatch):
+    """-split: every pair through the wave kernel's split tail (queries of 257-1024 rows; the
+    segment count P = 2 or 4 drawn from the case seed in the test)"""
     monkeypatch.setenv("SWBANK_KERNEL", request.param.split("-")[0])
     monkeypatch.setenv("SWBANK_F16", "0" if request.param.endswith("-u16") else "1")
+    if "-split" in request.param:
+        monkeypatch.setenv("SWBANK_WAVE_SPLIT", "1000000")
     return request.param
 
 
@@ -64,7 +69,9 @@ _SEEDS = int(os.environ.get("SWBANK_FUZZ_SEEDS", "150"))
 
 
 @pytest.mark.parametrize("seed", range(_BASE, _BASE + _SEEDS))
-def test_fuzz_vs_oracle(seed):
+def test_fuzz_vs_oracle(seed, kernel_choice, monkeypatch):
+    if "-split" in kernel_choice:
+        monkeypatch.setenv("SWBANK_WAVE_SPLIT_P", "2" if seed % 2 else "4")
     dna, A, sub, pen, go, ge, model, q, seqs = _case(seed)
     with S.ScoreBank(alphabet=S.ALPHABET_DNA if dna else S.ALPHABET_PROTEIN,
                      gap_model=model) as bank:
