@@ -118,6 +118,19 @@ sw_status sw_set_matrix(sw_bank *bank, const int8_t *matrix, int32_t alpha, int3
 /* ---- ld_sequence (query) --------------------------------------------------------------- */
 sw_status sw_load_query(sw_bank *bank, uint64_t id, const uint8_t *codes, uint32_t len);
 
+/* A query set (ld_sequence for several queries; not in the reference, whose bank holds one):
+ * query i = codes[offsets[i] .. + lens[i]) with id ids[i] (ids may be NULL).  Until the next
+ * sw_load_query / sw_load_queries, sw_score_batch_device scores its batch against every query
+ * of the set into d_scores[i * n + k] (query-major), in one launch per query segment (the
+ * tile kernel streams (query, tile) units, so a workgroup scores many tiles per launch); the
+ * other scoring calls return SW_ERR_STATE while a set of more than one query is loaded.
+ * nq == 1 is sw_load_query.  Single-device banks. */
+sw_status sw_load_queries(sw_bank *bank, size_t nq, const uint64_t *ids, const uint8_t *codes,
+                          const uint64_t *offsets, const uint32_t *lens);
+
+/* Queries loaded (0 before any, 1 after sw_load_query). */
+size_t sw_query_count(const sw_bank *bank);
+
 /* ---- target stream -> scores ----------------------------------------------------------- */
 /* Host buffers, blocking.  Target k = residues[offsets[k] .. offsets[k]+lens[k]) (codes) of
  * the residues_len-byte buffer (a target outside it is SW_ERR_ARG, nothing past it is read),

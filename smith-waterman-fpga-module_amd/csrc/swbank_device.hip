@@ -53,7 +53,8 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        int accum, int packed, const uint32_t* idx,
                                        const uint32_t* nidx, uint32_t idx_base,
                                        const uint32_t* ident, int pair, uint32_t pS1,
-                                       uint32_t pS2, uint32_t ulen, uint32_t ustride, hipStream_t st);
+                                       uint32_t pS2, uint32_t ulen, uint32_t ustride, uint32_t nq,
+                                       uint32_t qwords, size_t sstride, hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
                                    hipStream_t st);
@@ -235,10 +236,15 @@ struct sw_bank {
   std::vector<int8_t> matrix;  // alpha x alpha
   int32_t gap_open = 0, gap_extend = 0;
 
-  // ld_sequence (query)
+  // ld_sequence (query); a query set (sw_load_queries, > 1 query) keeps every query in qset
+  // and its longest one in `query` (which sets the segment layout of all of them)
   bool have_query = false;
   uint64_t qid = 0;
   std::vector<uint8_t> query;
+  std::vector<std::vector<uint8_t>> qset;
+  bool mq_ready = false;               // mqtab / mqtab16 match qset and the penalties
+  DevBuf<uint32_t> mqtab, mqtab16;     // [query][the single-query LUT layout] (u16, f16)
+  size_t mq_words = 0;                 // words per query
 
   // derived per (penalties, query)
   bool dirty = true;
@@ -328,6 +334,7 @@ struct sw_bank {
   // dperm = visiting order + count, dsort = histogram / scan scratch
   DevBuf<uint32_t> dperm, dsort;
   bool is_multi() const { return !kids.empty(); }
+  bool gotoh() const { return cfg.gap_model == SW_GAP_GOTOH; }
 
   // Query tables are rewritten in place by prepare() while earlier launches may still read
   // them on the caller's stream: the upload (on the bank stream) waits for ev_used (recorded
@@ -541,6 +548,8 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   (void)sw_bank_timing(b, &nl, &pm, &sm);
   b->qtab.release();
   b->qtab16.release();
+  b->mqtab.release();
+  b->mqtab16.release();
   b->qpair.release();
   b->stage.release();
   if (b->ev_ready) (void)hipEventDestroy(b->ev_ready);
@@ -665,9 +674,48 @@ extern "C" sw_status sw_load_query(sw_bank* b, uint64_t id, const uint8_t* codes
       return fail(b, SW_ERR_ARG, "query code %u at %u outside alphabet %d", codes[i], i, b->alpha);
   b->query.assign(codes, codes + len);
   b->qid = id;
+  b->qset.clear();
   b->have_query = true;
   b->dirty = true;
   return SW_OK;
+}
+
+// A query set: ld_sequence for several queries that every following device batch is scored
+// against (scores query-major, nq x n).  One query = sw_load_query.
+extern "C" sw_status sw_load_queries(sw_bank* b, size_t nq, const uint64_t* ids,
+                                     const uint8_t* codes, const uint64_t* offsets,
+                                     const uint32_t* lens) {
+  if (!b || nq == 0 || !offsets || !lens) return SW_ERR_ARG;
+  if (b->is_multi())
+    return fail(b, SW_ERR_UNSUPPORTED, "query sets need a single-device bank");
+  if (nq > 65536) return fail(b, SW_ERR_UNSUPPORTED, "more than 65536 queries in one set");
+  if (nq == 1) return sw_load_query(b, ids ? ids[0] : 0, codes + offsets[0], lens[0]);
+  const uint32_t cap = b->cfg.max_query_len ? b->cfg.max_query_len : SWB_MAX_QUERY;
+  size_t longest = 0;
+  for (size_t i = 0; i < nq; ++i) {
+    if (lens[i] > cap)
+      return fail(b, SW_ERR_UNSUPPORTED, "query %zu length %u exceeds the bank maximum %u", i,
+                  lens[i], cap);
+    if (lens[i] && !codes) return fail(b, SW_ERR_ARG, "null query codes");
+    for (uint32_t j = 0; j < lens[i]; ++j)
+      if (codes[offsets[i] + j] >= (uint32_t)b->alpha)
+        return fail(b, SW_ERR_ARG, "query %zu code %u at %u outside alphabet %d", i,
+                    codes[offsets[i] + j], j, b->alpha);
+    if (lens[i] > lens[longest]) longest = i;
+  }
+  b->qset.assign(nq, {});
+  for (size_t i = 0; i < nq; ++i)
+    b->qset[i].assign(codes + offsets[i], codes + offsets[i] + lens[i]);
+  b->query = b->qset[longest];
+  b->qid = ids ? ids[longest] : 0;
+  b->have_query = true;
+  b->dirty = true;
+  b->mq_ready = false;
+  return SW_OK;
+}
+
+extern "C" size_t sw_query_count(const sw_bank* b) {
+  return !b || !b->have_query ? 0 : b->qset.size() > 1 ? b->qset.size() : 1;
 }
 
 // Build the resident query state (the ScoringModule's query + penalty registers,
@@ -977,7 +1025,58 @@ static sw_status prepare(sw_bank* b) {
   b->smax = smax;
   b->col0 = col0;
   b->i32_ready = false;
+  b->mq_ready = false;
   b->dirty = false;
+  return SW_OK;
+}
+
+// Row-LUT tables of every query of a set in the segment layout of the longest one (prepare()
+// ran on it): query i's words at i * mq_words, rows past its end padding (u16 0xFF: S - 255,
+// f16 0xBC: -2048, as in prepare()).  LUT mode only (DNA matrices without the column-0 rule).
+static sw_status prepare_multi(sw_bank* b) {
+  if (b->mq_ready) return SW_OK;
+  const int A = b->alpha;
+  const int8_t* m = b->matrix.data();
+  const int R = b->R, S = (int)b->S;
+  const size_t words = b->segs.back().off + (size_t)b->segs.back().W * R;
+  const int seg_rows = b->segs[0].W * R;
+  const size_t nq = b->qset.size();
+  std::vector<uint32_t> t16, t8(nq * words, 0xFFFFFFFFu);
+  if (b->f16) t16.assign(nq * words, 0xBCBCBCBCu);
+  for (size_t i = 0; i < nq; ++i) {
+    const std::vector<uint8_t>& qi = b->qset[i];
+    for (size_t sg = 0; sg < b->segs.size(); ++sg) {
+      const size_t base = i * words + b->segs[sg].off;
+      const int r0 = (int)sg * seg_rows;
+      for (int j = 0; j < b->segs[sg].W * R && r0 + j < (int)qi.size(); ++j) {
+        uint32_t w = 0, h = 0;
+        for (int c = 0; c < 4; ++c) {
+          const int v = m[qi[r0 + j] * A + c];
+          w |= (uint32_t)(uint8_t)(S - v) << (8 * c);
+          h |= (uint32_t)(f16_score_bits(v) >> 8) << (8 * c);
+        }
+        t8[base + j] = w;
+        if (b->f16) t16[base + j] = h;
+      }
+    }
+  }
+  HIPOK(b, hipSetDevice(b->device));
+  HIPOK(b, hipEventSynchronize(b->ev_ready));  // the staging buffer is free again
+  HIPOK(b, b->stage.reserve((t8.size() + t16.size()) * 4));
+  HIPOK(b, b->mqtab.reserve(t8.size()));
+  if (!t16.empty()) HIPOK(b, b->mqtab16.reserve(t16.size()));
+  HIPOK(b, hipStreamWaitEvent(b->stream, b->ev_used, 0));
+  std::memcpy(b->stage.p, t8.data(), t8.size() * 4);
+  HIPOK(b, hipMemcpyAsync(b->mqtab.p, b->stage.p, t8.size() * 4, hipMemcpyHostToDevice,
+                          b->stream));
+  if (!t16.empty()) {
+    std::memcpy(b->stage.p + t8.size() * 4, t16.data(), t16.size() * 4);
+    HIPOK(b, hipMemcpyAsync(b->mqtab16.p, b->stage.p + t8.size() * 4, t16.size() * 4,
+                            hipMemcpyHostToDevice, b->stream));
+  }
+  HIPOK(b, hipEventRecord(b->ev_ready, b->stream));
+  b->mq_words = words;
+  b->mq_ready = true;
   return SW_OK;
 }
 
@@ -1267,7 +1366,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                                   b->pad, b->segs[s].W, scores, ein, eout, ecols, s > 0 ? 1 : 0,
                                   (int)packed, idx, nidx, (uint32_t)p0,
                                   pass == 0 ? ident : nullptr, pair ? 1 : 0, b->pS1, b->pS2,
-                                  ulen, ustride, st));
+                                  ulen, ustride, 1u, 0u, 0, st));
       }
     }
   }
@@ -1309,6 +1408,112 @@ static sw_status track_best_device(sw_bank* b, const int32_t* d_scores, const ui
   return SW_OK;
 }
 
+// A device batch against every query of a set (sw_load_queries): d_scores[q * n + k].  The
+// tile kernel's several-queries variant takes the whole set in one launch per query segment
+// (units = (query, tile) pairs, so every workgroup streams many tiles and the pipeline fills
+// once); row-LUT tables only, exact 16-bit arithmetic.  Otherwise (profiles, the column-0 rule,
+// optimistic f16, int32 re-scores, a wave-kernel shape; SWBANK_MQ=0) the queries run one after
+// the other through launch().
+static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
+                            const uint32_t* d_lens, size_t n, uint32_t max_len,
+                            int32_t* d_scores, hipStream_t st) {
+  const size_t nq = b->qset.size();
+  const uint64_t smax = (uint64_t)std::max(0, b->smax);
+  const uint64_t top = std::min<uint64_t>(b->query.size(), max_len) * smax + smax;
+  const bool f16_ok = b->f16 && b->f16_neg >= -2048 && env_int("SWBANK_F16", 1) != 0;
+  const bool use_f16 = f16_ok && top <= 2048u;
+  const bool exact = use_f16 || top <= 65535u;
+  const size_t ntiles = (n + SWB_TILE - 1) / SWB_TILE;
+  const char* kforce = std::getenv("SWBANK_KERNEL");
+  const bool mq = env_int("SWBANK_MQ", 1) != 0 && !b->prof && !b->col0 && exact &&
+                  env_int("SWBANK_I32", 0) == 0 && (b->R == 16 || b->R == 32) && b->RB == 4 &&
+                  !(b->gotoh() && !use_f16 && b->R != 16) && n <= 0xFFFFFFFFull &&
+                  !(kforce && std::strcmp(kforce, "wave") == 0) && ntiles * nq <= 0x7FFFFFFFull;
+  if (!mq) {  // one query at a time (each prepare()d in turn), then the set's layout again
+    const std::vector<uint8_t> longest = b->query;
+    sw_status rs = SW_OK;
+    for (size_t i = 0; i < nq && rs == SW_OK; ++i) {
+      b->query = b->qset[i];
+      b->dirty = true;
+      rs = prepare(b);
+      if (rs == SW_OK)
+        rs = launch(b, d_res, d_offs, d_lens, n, max_len, d_scores + i * n, st, SWK_PACK_BYTES,
+                    nullptr, nullptr, true);
+    }
+    b->query = longest;
+    b->dirty = true;
+    const size_t L = strlen(b->last_kernel);
+    snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " x%zu queries", nq);
+    return rs;
+  }
+  sw_status rs = prepare_multi(b);
+  if (rs != SW_OK) return rs;
+  const bool gotoh = b->gotoh();
+  const size_t nseg = b->segs.size();
+  snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s R=%d W=%d segs=%zu queries=%zu",
+           use_f16 ? "f16" : "u16", b->R, b->segs[0].W, nseg, nq);
+  HIPOK(b, hipStreamWaitEvent(st, b->ev_ready, 0));  // the query tables are uploaded
+  HIPOK(b, hipStreamWaitEvent(st, b->ev_used, 0));   // bank scratch is free
+  sw_bank::Ev ev{};
+  if (b->timing) {
+    HIPOK(b, hipEventCreate(&ev.a));
+    HIPOK(b, hipEventCreate(&ev.b));
+    HIPOK(b, hipEventCreate(&ev.c));
+    HIPOK(b, hipEventRecord(ev.a, st));
+    HIPOK(b, hipEventRecord(ev.b, st));
+  }
+  const uint32_t ecols = (max_len + 7) / 8 * 8;
+  // longest-first order of a ragged batch (shared by every query)
+  const uint32_t *perm = nullptr, *perm_n = nullptr, *ident = nullptr;
+  if (ntiles > 1 && env_int("SWBANK_DSORT", 1) != 0) {
+    HIPOK(b, b->dperm.reserve(n + 2));
+    const size_t sw = swk_sort_scratch_bytes() / 4;
+    if (b->dsort.cap < sw) {
+      HIPOK(b, b->dsort.reserve(sw));
+      HIPOK(b, hipMemsetAsync(b->dsort.p, 0, sw * 4, st));
+    }
+    HIPOK(b, swk_sort_lens(d_lens, n, max_len, b->dperm.p, b->dperm.p + n, b->dperm.p + n + 1,
+                           b->dsort.p, st));
+    perm = b->dperm.p;
+    perm_n = b->dperm.p + n;
+    ident = b->dperm.p + n + 1;
+  }
+  // edge rows per (query, tile) unit; past SWBANK_EDGE_MB the batch runs as position ranges
+  size_t span = n;
+  if (nseg > 1) {
+    const size_t budget = (size_t)std::max(1, env_int("SWBANK_EDGE_MB", 2048)) << 20;
+    const size_t per_tile = (size_t)ecols * 64 * sizeof(uint2) * nq;
+    span = std::min(n, std::max<size_t>(1, budget / per_tile) * SWB_TILE);
+    const size_t words = (span + SWB_TILE - 1) / SWB_TILE * ecols * 64 * nq;
+    HIPOK(b, b->edge[0].reserve(words));
+    HIPOK(b, b->edge[1].reserve(words));
+  }
+  const uint32_t* tabs = use_f16 ? b->mqtab16.p : b->mqtab.p;
+  for (size_t p0 = 0; p0 < n; p0 += span) {
+    const size_t np = std::min(span, n - p0);
+    // with the order: whole arrays through it; else this range's slice
+    const uint64_t* offs = perm ? d_offs : d_offs + p0;
+    const uint32_t* lens = perm ? d_lens : d_lens + p0;
+    int32_t* scores = perm ? d_scores : d_scores + p0;
+    for (size_t sg = 0; sg < nseg; ++sg) {
+      const void* ein = sg > 0 ? b->edge[(sg - 1) & 1].p : nullptr;
+      void* eout = sg + 1 < nseg ? b->edge[sg & 1].p : nullptr;
+      HIPOK(b, swk_launch_score(b->R, b->RB, 0, 0, gotoh ? 1 : 0, use_f16 ? 1 : 0, d_res, offs,
+                                lens, np, tabs + b->segs[sg].off, use_f16 ? b->nv16 : b->nv,
+                                b->S, b->O, b->E, 0, b->pad, b->segs[sg].W, scores, ein, eout,
+                                ecols, sg > 0 ? 1 : 0, (int)SWK_PACK_BYTES,
+                                perm ? perm + p0 : nullptr, perm_n, (uint32_t)p0, ident, 0, 0, 0,
+                                0, 0, (uint32_t)nq, (uint32_t)b->mq_words, n, st));
+    }
+  }
+  HIPOK(b, hipEventRecord(b->ev_used, st));
+  if (b->timing) {
+    HIPOK(b, hipEventRecord(ev.c, st));
+    b->events.push_back(ev);
+  }
+  return SW_OK;
+}
+
 extern "C" sw_status sw_score_batch_device(sw_bank* b, const uint8_t* d_res,
                                            const uint64_t* d_offs, const uint32_t* d_lens,
                                            const uint64_t* d_ids, size_t n, uint32_t max_len,
@@ -1323,6 +1528,10 @@ extern "C" sw_status sw_score_batch_device(sw_bank* b, const uint8_t* d_res,
   if (st != SW_OK) return st;
   HIPOK(b, hipSetDevice(b->device));
   hipStream_t hs = stream ? reinterpret_cast<hipStream_t>(stream) : b->stream;
+  if (b->qset.size() > 1) {  // a query set: nq x n scores; the best hit is not tracked
+    if (d_ids) return fail(b, SW_ERR_UNSUPPORTED, "best hit over a query set");
+    return launch_set(b, d_res, d_offs, d_lens, n, max_len, d_scores, hs);
+  }
   if ((st = launch(b, d_res, d_offs, d_lens, n, max_len, d_scores, hs, SWK_PACK_BYTES, nullptr,
                    nullptr, true)) != SW_OK)
     return st;
@@ -1950,6 +2159,8 @@ extern "C" sw_status sw_load_query_record(sw_bank* b, const void* record) {
 
 extern "C" sw_status sw_score_records_device(sw_bank* b, const void* d_records, size_t n,
                                              int32_t* d_scores, void* stream) {
+  if (b && b->qset.size() > 1)
+    return fail(b, SW_ERR_STATE, "a query set is loaded: score it with sw_score_batch_device");
   if (!b) return SW_ERR_ARG;
   if (b->is_multi())
     return fail(b, SW_ERR_UNSUPPORTED, "device buffers need a single-device bank");
@@ -2194,6 +2405,8 @@ static sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_
 extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, size_t residues_len,
                                     const uint64_t* offsets, const uint32_t* lens,
                                     const uint64_t* ids, size_t n, int32_t* scores_out) {
+  if (b && b->qset.size() > 1)
+    return fail(b, SW_ERR_STATE, "a query set is loaded: score it with sw_score_batch_device");
   if (!b) return SW_ERR_ARG;
   b->best_kind = 0;
   if (n == 0) return SW_OK;
@@ -2217,6 +2430,8 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, size_t 
 
 extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
                                       int32_t* scores_out) {
+  if (b && b->qset.size() > 1)
+    return fail(b, SW_ERR_STATE, "a query set is loaded: score it with sw_score_batch_device");
   if (!b) return SW_ERR_ARG;
   b->best_kind = 0;
   if (n == 0) return SW_OK;

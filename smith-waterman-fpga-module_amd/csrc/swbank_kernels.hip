@@ -569,6 +569,11 @@ struct ScoreArgs {
   // k * ustride of res; offs and lens are not read (the host feeder's equal-length chunks
   // cross PCIe without per-target headers)
   uint32_t ulen, ustride;
+  // several queries, one batch (tile kernel, row-LUT variants): the grid's units are (query q,
+  // tile) pairs, unit u = q * ntiles + tile; query q's row LUTs start qwords 32-bit words after
+  // query q - 1's, its scores sstride entries after; edge rows are per unit.  nq <= 1: one query
+  uint32_t nq, qwords;
+  size_t sstride;
 };
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -618,8 +623,10 @@ __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens
 // 16 A/C/G/T slots on 16 different 4-bank groups (conflict-free ds_read_b128).  A column of
 // wave w reads its row words as 4 blocks of 8 (two ds_read_b128 each), one block ahead of
 // the asm block that consumes them: 6.5 VALU per 2 cells instead of 7.5.
-template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false>
+template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
+          bool MQ = false>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
+  static_assert(!MQ || (!PROF && !PAIR), "several queries: row-LUT variants");
   constexpr int C = 8;
   static_assert(!PAIR || (R == 32 && F16 && !PROF && !GOTOH && !COL0), "PAIR: f16 merged R=32");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -643,12 +650,24 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   }
   const int ntiles = (int)((n + SWB_TILE - 1) / SWB_TILE);
   const int G = (int)gridDim.x;
+  // units: (query, tile) pairs; one query: unit = tile.  A unit past the end keeps its number
+  // as the tile (lane_targets then reads nothing)
+  // (MQ only; otherwise unit = tile and q = 0)
+  const int nunits = MQ ? ntiles * (int)a.nq : ntiles;
   int total = 0;  // chunks of all this workgroup's tiles: every wave runs total + W - 1 phases
   const uint32_t packed = a.packed;
-  for (int t = blockIdx.x; t < ntiles; t += G)
-    total += tile_nch(a.res, a.lens, n, t, lane, packed, idx, a.ulen, a.ustride);
+  for (int u = blockIdx.x; u < nunits; u += G)
+    total += tile_nch(a.res, a.lens, n, MQ ? u % ntiles : u, lane, packed, idx, a.ulen,
+                      a.ustride);
 
-  int tile = blockIdx.x;
+  int unit = blockIdx.x, q = 0;
+  int tile = unit;
+  if constexpr (MQ) {
+    if (unit < nunits) {
+      q = unit / ntiles;
+      tile = unit - q * ntiles;
+    }
+  }
   Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen, a.ustride);
   int nch, nfull;
   tile_chunks(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
@@ -664,7 +683,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     bnd[lane] = F16 ? make_uint2(0u, GOTOH ? 0u : as_u32(as_u16x2(NOE2)))
                     : make_uint2(S | (S << 16), 0u);
     if (seg_in)  // the previous segment's bottom row of chunk 0
-      dma_edge_chunk(a.edge_in + (size_t)tile * a.ecols * 64, ein, lane);
+      dma_edge_chunk(a.edge_in + (size_t)(MQ ? unit : tile) * a.ecols * 64, ein, lane);
   }
   uint32_t nv = a.nv;
   uint32_t tab[PROF || PAIR ? 1 : R];
@@ -683,7 +702,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     // operand per VOP3 on gfx950).
     asm volatile("" : "+v"(nv));
 #pragma unroll
-    for (int r = 0; r < R; ++r) tab[r] = __builtin_amdgcn_readfirstlane(a.qtab[wave * R + r]);
+    for (int r = 0; r < R; ++r)
+      tab[r] = __builtin_amdgcn_readfirstlane(a.qtab[(MQ ? (size_t)q * a.qwords : 0) + wave * R + r]);
   }
   const u16x2 S2 = {(unsigned short)S, (unsigned short)S};
   const u16x2 O2 = {(unsigned short)a.O, (unsigned short)a.O};
@@ -758,10 +778,20 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     if (g >= 0 && g < total) {
       const uint2 clo = rlo, chi = rhi;
       const bool last = c + 1 == nch;
-      const int ntile = tile + G;
+      const int nunit = (MQ ? unit : tile) + G;
+      int ntile = nunit, nqq = q;  // the next unit's tile and query
+      if constexpr (MQ) {
+        if (nunit < nunits) {
+          ntile = tile + G;
+          while (ntile >= ntiles) {
+            ntile -= ntiles;
+            ++nqq;
+          }
+        }
+      }
       if (!last) {
         load_raw(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
-      } else if (ntile < ntiles) {  // first chunk of the next tile
+      } else if (nunit < nunits) {  // first chunk of the next tile
         cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed, idx, a.ulen,
                            a.ustride);
         tile_chunks(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
@@ -769,8 +799,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         load_raw(cur, 0, nfull_n > 0, a.pad, packed, rlo, rhi);
       }
       const int slot = g & 1;
-      if (seg_in && wave == 0 && (!last || ntile < ntiles))  // next chunk's boundary row
-        dma_edge_chunk(a.edge_in + ((size_t)(last ? ntile : tile) * a.ecols +
+      if (seg_in && wave == 0 && (!last || nunit < nunits))  // next chunk's boundary row
+        dma_edge_chunk(a.edge_in + ((size_t)(last ? nunit : MQ ? unit : tile) * a.ecols +
                                     (size_t)(last ? 0 : c + 1) * C) * 64,
                        ein + (size_t)((g + 1) & 1) * C * 64, lane);
       const uint2* rin = wave > 0 ? ring + ((size_t)((wave - 1) * 2 + slot) * C) * 64 + lane
@@ -913,7 +943,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         rout[jj * ostride] = make_uint2(as_u32(Hl[R - 1]), as_u32(upX));
       }
       if (seg_out && wave == W - 1) {  // this segment's bottom row -> the next segment
-        uint2* dst = a.edge_out + ((size_t)tile * a.ecols + (size_t)c * C) * 64 + lane;
+        uint2* dst = a.edge_out + ((size_t)(MQ ? unit : tile) * a.ecols + (size_t)c * C) * 64 + lane;
 #pragma unroll
         for (int jj = 0; jj < C; ++jj) dst[jj * 64] = sink[jj * 64 + lane];
       }
@@ -932,12 +962,13 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           }
           const size_t slo = idx && tlo < n ? idx[tlo] : tlo;
           const size_t shi = idx && thi < n ? idx[thi] : thi;
+          int32_t* qsc = MQ ? a.scores + (size_t)q * a.sstride : a.scores;
           if (a.accum) {  // best over the previous query segments
-            if (tlo < n) blo = max(blo, a.scores[slo]);
-            if (thi < n) bhi = max(bhi, a.scores[shi]);
+            if (tlo < n) blo = max(blo, qsc[slo]);
+            if (thi < n) bhi = max(bhi, qsc[shi]);
           }
-          if (tlo < n) a.scores[slo] = blo;
-          if (thi < n) a.scores[shi] = bhi;
+          if (tlo < n) qsc[slo] = blo;
+          if (thi < n) qsc[shi] = bhi;
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -947,6 +978,15 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         best = (u16x2){0, 0};
         prevUpH = H0;
         tile = ntile;
+        if constexpr (MQ) {  // several queries: the next unit's row LUTs
+          unit = nunit;
+          if (nqq != q) {
+            q = nqq;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+              tab[r] = __builtin_amdgcn_readfirstlane(a.qtab[(size_t)q * a.qwords + wave * R + r]);
+          }
+        }
         nch = nch_n;
         nfull = nfull_n;
         c = 0;
@@ -1002,14 +1042,15 @@ static unsigned persistent_grid(const void* fn, size_t ntiles, int threads, size
   return (unsigned)((ntiles + rounds - 1) / rounds);
 }
 
-template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false>
+template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
+          bool MQ = false>
 static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st) {
-  const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE;
+  const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE * (MQ ? a.nq : 1);  // units
   const size_t lds = (size_t)W * SWB_TILE * 4 +
                      (size_t)(64 + (a.edge_out ? 8 * 64 : 64) + (a.edge_in ? 2 * 8 * 64 : 0) +
                               (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8 +
                      (PROF ? prof_bytes : 0) + (PAIR ? a.PS : 0);
-  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR>;
+  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR, MQ>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -1665,6 +1706,7 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        const uint32_t* nidx, uint32_t idx_base,
                                        const uint32_t* ident, int pair, uint32_t pS1,
                                        uint32_t pS2, uint32_t ulen, uint32_t ustride,
+                                       uint32_t nq, uint32_t qwords, size_t sstride,
                                        hipStream_t st) {
   if (n == 0) return hipSuccess;
   swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
@@ -1675,7 +1717,19 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                    swk::f16_pair(-(int)O), nullptr, 0u, 0u, 0};
   a.ulen = ulen;
   a.ustride = ustride;
+  a.nq = nq;
+  a.qwords = qwords;
+  a.sstride = sstride;
   const uint32_t prof_bytes = (pad + 1) * PS;
+  if (nq > 1) {  // several queries: row-LUT variants without the column-0 rule
+#define SWK_MQ_CASE(RR, GT, FH)                                                                  \
+  if (R == RR && RB == 4 && !col0 && !prof && !pair && gotoh == GT && f16 == FH)                 \
+    return swk::launch_score<RR, 4, false, false, (GT != 0), (FH != 0), false, true>(a, W, 0, st);
+    SWK_MQ_CASE(32, 0, 1) SWK_MQ_CASE(32, 0, 0) SWK_MQ_CASE(16, 0, 1) SWK_MQ_CASE(16, 0, 0)
+    SWK_MQ_CASE(16, 1, 1) SWK_MQ_CASE(16, 1, 0) SWK_MQ_CASE(32, 1, 0)
+#undef SWK_MQ_CASE
+    return hipErrorInvalidValue;
+  }
   if (pair) {  // PS = pair-table bytes
     if (R == 32 && f16 && !prof && !gotoh && !col0)
       return swk::launch_score<32, 4, false, false, false, true, true>(a, W, 0, st);

@@ -40,7 +40,8 @@ EXPORTS = (
     "sw_score_batch_device", "sw_best_hit", "sw_encode_ascii", "sw_pack_2bit",
     "sw_unpack_2bit", "sw_fill_matrix", "sw_bank_set_timing", "sw_bank_timing",
     "sw_last_kernel", "sw_load_query_record", "sw_score_records", "sw_score_records_device",
-    "sw_best_hit_device", "sw_batch_best", "sw_bank_devices",
+    "sw_best_hit_device", "sw_batch_best", "sw_bank_devices", "sw_load_queries",
+    "sw_query_count",
 )
 ABI_VERSION = 2
 MAX_DEVICES = 16
@@ -112,6 +113,8 @@ def lib() -> ctypes.CDLL:
         "sw_score_records": (i32, [P, P, sz, P]),
         "sw_score_records_device": (i32, [P, P, sz, P, P]),
         "sw_best_hit_device": (i32, [P, P, P, sz, P, P]),
+        "sw_load_queries": (i32, [P, sz, P, P, P, P]),
+        "sw_query_count": (sz, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -294,6 +297,25 @@ class ScoreBank:
         c = np.ascontiguousarray(codes, dtype=np.uint8)
         buf = c if c.size else np.zeros(1, np.uint8)
         self._check(lib().sw_load_query(self._h, qid, _p(buf), len(c)))
+
+    def load_queries(self, queries, ids=None):
+        """A query set (sw_load_queries): every following score_batch_device call scores the
+        batch against each query, scores query-major (len(queries) x n)."""
+        qs = [np.ascontiguousarray(q, dtype=np.uint8) for q in queries]
+        if not qs:
+            raise ValueError("an empty query set")
+        codes, offs, lens = pack_targets(qs)
+        idv = None
+        if ids is not None:
+            idv = np.ascontiguousarray(ids, dtype=np.uint64)
+            if idv.size != len(qs):
+                raise ValueError(f"{idv.size} ids for {len(qs)} queries")
+        buf = codes if codes.size else np.zeros(1, np.uint8)
+        self._check(lib().sw_load_queries(self._h, len(qs), None if idv is None else _p(idv),
+                                          _p(buf), _p(offs), _p(lens)))
+
+    def query_count(self) -> int:
+        return int(lib().sw_query_count(self._h))
 
     # target stream
     def score_batch(self, residues: np.ndarray, offsets: np.ndarray, lens: np.ndarray,
