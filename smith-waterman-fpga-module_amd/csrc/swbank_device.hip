@@ -245,6 +245,11 @@ struct sw_bank {
   bool mq_ready = false;               // mqtab / mqtab16 match qset and the penalties
   DevBuf<uint32_t> mqtab, mqtab16;     // [query][the single-query LUT layout] (u16, f16)
   size_t mq_words = 0;                 // words per query
+  // letter-pair tables of a DNA merged f16 set: [128-row segment][query][mq_pair_words]
+  DevBuf<uint32_t> mqpair;
+  size_t mq_pair_words = 0;
+  int mq_pair_segs = 0;
+  uint32_t mq_pS1 = 0, mq_pS2 = 0;
 
   // derived per (penalties, query)
   bool dirty = true;
@@ -550,6 +555,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->qtab16.release();
   b->mqtab.release();
   b->mqtab16.release();
+  b->mqpair.release();
   b->qpair.release();
   b->stage.release();
   if (b->ev_ready) (void)hipEventDestroy(b->ev_ready);
@@ -718,6 +724,38 @@ extern "C" size_t sw_query_count(const sw_bank* b) {
   return !b || !b->have_query ? 0 : b->qset.size() > 1 ? b->qset.size() : 1;
 }
 
+// Letter-pair table layout for NR rows: slot (a, b) at 16 + a*pS1 + b*pS2 (bytes), pS2/16 = 1 and
+// pS1/16 = 4 (mod 16) so the 16 A/C/G/T slots sit on 16 different 4-bank LDS groups.
+static void pair_strides(uint32_t NR, uint32_t& pS1, uint32_t& pS2) {
+  const uint32_t B = 4 * NR;
+  pS2 = (B + 15) / 16 * 16;
+  while ((pS2 / 16) % 16 != 1) pS2 += 16;
+  pS1 = (4 * pS2 + B + 15) / 16 * 16;
+  while ((pS1 / 16) % 16 != 4) pS1 += 16;
+}
+
+// The letter-pair table of query rows [r0, r0 + NR) (the PAIR tile kernel, DNA merged f16):
+// slot (a, b) holds word k = {s(q_{r0+k+1}, a), s(q_{r0+k+1}, b)} (f16 halves; rows past the
+// query -2048) and the row-r0 word 4 bytes before it.
+static std::vector<uint32_t> pair_table(const uint8_t* q, int qlen, int r0, uint32_t NR,
+                                        const int8_t* m, int A, uint32_t pS1, uint32_t pS2) {
+  const uint32_t bytes = 16 + 4 * pS1 + 4 * pS2 + 4 * NR;
+  std::vector<uint32_t> t(bytes / 4, 0xBC00BC00u);
+  auto word = [&](int r, int x, int y) -> uint32_t {  // row r of the segment, letters x, y
+    if (r0 + r >= qlen) return 0xBC00BC00u;
+    const int c = q[r0 + r];
+    return (uint32_t)f16_score_bits(m[c * A + x]) | (uint32_t)f16_score_bits(m[c * A + y]) << 16;
+  };
+  for (int x = 0; x < A; ++x)
+    for (int y = 0; y < A; ++y) {
+      const uint32_t base = (16 + x * pS1 + y * pS2) / 4;
+      for (uint32_t k = 0; k + 1 < NR; ++k) t[base + k] = word((int)k + 1, x, y);
+    }
+  for (int x = 0; x < A; ++x)  // row-0 words last: they may reuse word NR-1 of a slot
+    for (int y = 0; y < A; ++y) t[(16 + x * pS1 + y * pS2) / 4 - 1] = word(0, x, y);
+  return t;
+}
+
 // Build the resident query state (the ScoringModule's query + penalty registers,
 // ScoringModule_v1.1.v:110-150): either per-row 4-byte LUTs (DNA fast path) or a query
 // profile QP[letter][row] = S - s(q_row, letter) (any alphabet).
@@ -876,26 +914,9 @@ static sw_status prepare(sw_bank* b) {
   uint32_t pS1 = 0, pS2 = 0;
   if (f16 && !prof && !gotoh && !col0 && R == 32 && segs.size() == 1 && segs[0].W <= 4 &&
       A == SW_DNA_ALPHA) {
-    const uint32_t NR = (uint32_t)segs[0].W * R, B = 4 * NR;
-    pS2 = (B + 15) / 16 * 16;
-    while ((pS2 / 16) % 16 != 1) pS2 += 16;
-    pS1 = (4 * pS2 + B + 15) / 16 * 16;
-    while ((pS1 / 16) % 16 != 4) pS1 += 16;
-    const uint32_t bytes = 16 + 4 * pS1 + 4 * pS2 + B;
-    tpair.assign(bytes / 4, 0xBC00BC00u);
-    auto word = [&](int r, int x, int y) -> uint32_t {  // row r of the segment, letters x, y
-      if (r >= qlen) return 0xBC00BC00u;
-      const int q = b->query[r];
-      return (uint32_t)f16_score_bits(m[q * A + x]) |
-             (uint32_t)f16_score_bits(m[q * A + y]) << 16;
-    };
-    for (int x = 0; x < A; ++x)
-      for (int y = 0; y < A; ++y) {
-        const uint32_t base = (16 + x * pS1 + y * pS2) / 4;
-        for (uint32_t k = 0; k + 1 < NR; ++k) tpair[base + k] = word((int)k + 1, x, y);
-      }
-    for (int x = 0; x < A; ++x)  // row-0 words last: they may reuse word NR-1 of a slot
-      for (int y = 0; y < A; ++y) tpair[(16 + x * pS1 + y * pS2) / 4 - 1] = word(0, x, y);
+    const uint32_t NR = (uint32_t)segs[0].W * R;
+    pair_strides(NR, pS1, pS2);
+    tpair = pair_table(b->query.data(), qlen, 0, NR, m, A, pS1, pS2);
   }
   // wave-kernel layout of the same query: rows padded to 64K; queries past 1024 rows run as
   // 1024-row segments (K = 16), one table per segment, concatenated
@@ -1060,9 +1081,27 @@ static sw_status prepare_multi(sw_bank* b) {
       }
     }
   }
+  // letter-pair tables (DNA merged f16 without the column-0 rule): 128-row segments (4 waves of
+  // 32 rows: the pair kernel's layout), one table per (segment, query)
+  std::vector<uint32_t> tp;
+  b->mq_pair_segs = 0;
+  if (b->f16 && !b->prof && !b->gotoh() && !b->col0 && A == SW_DNA_ALPHA &&
+      env_int("SWBANK_MQ_PAIR", 1) != 0) {
+    const uint32_t NR = 128;
+    pair_strides(NR, b->mq_pS1, b->mq_pS2);
+    const int qmax = (int)b->query.size();
+    b->mq_pair_segs = std::max(1, (qmax + (int)NR - 1) / (int)NR);
+    for (int sg = 0; sg < b->mq_pair_segs; ++sg)
+      for (size_t i = 0; i < nq; ++i) {
+        const std::vector<uint32_t> t = pair_table(b->qset[i].data(), (int)b->qset[i].size(),
+                                                   sg * (int)NR, NR, m, A, b->mq_pS1, b->mq_pS2);
+        b->mq_pair_words = t.size();
+        tp.insert(tp.end(), t.begin(), t.end());
+      }
+  }
   HIPOK(b, hipSetDevice(b->device));
   HIPOK(b, hipEventSynchronize(b->ev_ready));  // the staging buffer is free again
-  HIPOK(b, b->stage.reserve((t8.size() + t16.size()) * 4));
+  HIPOK(b, b->stage.reserve((t8.size() + t16.size() + tp.size()) * 4));
   HIPOK(b, b->mqtab.reserve(t8.size()));
   if (!t16.empty()) HIPOK(b, b->mqtab16.reserve(t16.size()));
   HIPOK(b, hipStreamWaitEvent(b->stream, b->ev_used, 0));
@@ -1073,6 +1112,13 @@ static sw_status prepare_multi(sw_bank* b) {
     std::memcpy(b->stage.p + t8.size() * 4, t16.data(), t16.size() * 4);
     HIPOK(b, hipMemcpyAsync(b->mqtab16.p, b->stage.p + t8.size() * 4, t16.size() * 4,
                             hipMemcpyHostToDevice, b->stream));
+  }
+  if (!tp.empty()) {
+    const size_t at = (t8.size() + t16.size()) * 4;
+    HIPOK(b, b->mqpair.reserve(tp.size()));
+    std::memcpy(b->stage.p + at, tp.data(), tp.size() * 4);
+    HIPOK(b, hipMemcpyAsync(b->mqpair.p, b->stage.p + at, tp.size() * 4, hipMemcpyHostToDevice,
+                            b->stream));
   }
   HIPOK(b, hipEventRecord(b->ev_ready, b->stream));
   b->mq_words = words;
@@ -1449,9 +1495,16 @@ static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_
   sw_status rs = prepare_multi(b);
   if (rs != SW_OK) return rs;
   const bool gotoh = b->gotoh();
-  const size_t nseg = b->segs.size();
-  snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s R=%d W=%d segs=%zu queries=%zu",
-           use_f16 ? "f16" : "u16", b->R, b->segs[0].W, nseg, nq);
+  // pair tables (5.5 instead of 6.5 VALU per row) when the set has them, the batch is f16-exact
+  // and a grid that is a multiple of nq (one query per workgroup) loses at most 1/8 of the
+  // resident slots
+  const size_t slots = 4 * (size_t)std::max(b->cus, 1);
+  const bool mpair = b->mq_pair_segs > 0 && use_f16 && nq <= slots &&
+                     8 * (slots - slots / nq * nq) <= slots;
+  const size_t nseg = mpair ? (size_t)b->mq_pair_segs : b->segs.size();
+  snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=%zu queries=%zu",
+           use_f16 ? "f16" : "u16", mpair ? " pair" : "", b->R,
+           mpair ? std::min(4, (int)(b->query.size() + 31) / 32) : b->segs[0].W, nseg, nq);
   HIPOK(b, hipStreamWaitEvent(st, b->ev_ready, 0));  // the query tables are uploaded
   HIPOK(b, hipStreamWaitEvent(st, b->ev_used, 0));   // bank scratch is free
   sw_bank::Ev ev{};
@@ -1498,6 +1551,18 @@ static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_
     for (size_t sg = 0; sg < nseg; ++sg) {
       const void* ein = sg > 0 ? b->edge[(sg - 1) & 1].p : nullptr;
       void* eout = sg + 1 < nseg ? b->edge[sg & 1].p : nullptr;
+      if (mpair) {  // 128-row segments, 4 waves of 32 rows (fewer for a short last one)
+        const int rows = std::min(128, (int)b->query.size() - (int)sg * 128);
+        const int Wp = std::max(1, (rows + 31) / 32);
+        HIPOK(b, swk_launch_score(32, 4, 0, 0, 0, 1, d_res, offs, lens, np,
+                                  b->mqpair.p + sg * nq * b->mq_pair_words, b->nv16, b->S, b->O,
+                                  b->E, (uint32_t)b->mq_pair_words * 4, b->pad, Wp, scores, ein,
+                                  eout, ecols, sg > 0 ? 1 : 0, (int)SWK_PACK_BYTES,
+                                  perm ? perm + p0 : nullptr, perm_n, (uint32_t)p0, ident, 1,
+                                  b->mq_pS1, b->mq_pS2, 0, 0, (uint32_t)nq,
+                                  (uint32_t)b->mq_pair_words, n, st));
+        continue;
+      }
       HIPOK(b, swk_launch_score(b->R, b->RB, 0, 0, gotoh ? 1 : 0, use_f16 ? 1 : 0, d_res, offs,
                                 lens, np, tabs + b->segs[sg].off, use_f16 ? b->nv16 : b->nv,
                                 b->S, b->O, b->E, 0, b->pad, b->segs[sg].W, scores, ein, eout,

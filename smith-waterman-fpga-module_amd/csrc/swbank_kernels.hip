@@ -626,7 +626,7 @@ __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
           bool MQ = false>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
-  static_assert(!MQ || (!PROF && !PAIR), "several queries: row-LUT variants");
+  static_assert(!MQ || !PROF, "several queries: row-LUT or pair-table variants");
   constexpr int C = 8;
   static_assert(!PAIR || (R == 32 && F16 && !PROF && !GOTOH && !COL0), "PAIR: f16 merged R=32");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -656,16 +656,19 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int nunits = MQ ? ntiles * (int)a.nq : ntiles;
   int total = 0;  // chunks of all this workgroup's tiles: every wave runs total + W - 1 phases
   const uint32_t packed = a.packed;
-  for (int u = blockIdx.x; u < nunits; u += G)
-    total += tile_nch(a.res, a.lens, n, MQ ? u % ntiles : u, lane, packed, idx, a.ulen,
-                      a.ustride);
+  for (int u = blockIdx.x; u < nunits; u += G)  // (the unit's tile: see the MQ order below)
+    total += tile_nch(a.res, a.lens, n, !MQ ? u : PAIR ? u / (int)a.nq : u % ntiles, lane, packed,
+                      idx, a.ulen, a.ustride);
 
+  // MQ order: row LUTs query-major (q = unit / ntiles; a wave reloads its LUT SGPRs when the
+  // query changes); pair tables query-minor (q = unit % nq) with the grid a multiple of nq, so
+  // a workgroup keeps one query and loads its LDS table once
   int unit = blockIdx.x, q = 0;
   int tile = unit;
   if constexpr (MQ) {
     if (unit < nunits) {
-      q = unit / ntiles;
-      tile = unit - q * ntiles;
+      q = PAIR ? unit % (int)a.nq : unit / ntiles;
+      tile = PAIR ? unit / (int)a.nq : unit - q * ntiles;
     }
   }
   Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen, a.ustride);
@@ -688,7 +691,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   uint32_t nv = a.nv;
   uint32_t tab[PROF || PAIR ? 1 : R];
   if constexpr (PAIR) {
-    const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
+    const uint4* src = reinterpret_cast<const uint4*>(a.qtab + (MQ ? (size_t)q * a.qwords : 0));
     for (uint32_t i = threadIdx.x; i < a.PS / 16; i += blockDim.x)
       reinterpret_cast<uint4*>(smem)[i] = src[i];
   } else if constexpr (PROF) {
@@ -782,10 +785,14 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       int ntile = nunit, nqq = q;  // the next unit's tile and query
       if constexpr (MQ) {
         if (nunit < nunits) {
-          ntile = tile + G;
-          while (ntile >= ntiles) {
-            ntile -= ntiles;
-            ++nqq;
+          if constexpr (PAIR) {
+            ntile = nunit / (int)a.nq;  // same query (G is a multiple of nq)
+          } else {
+            ntile = tile + G;
+            while (ntile >= ntiles) {
+              ntile -= ntiles;
+              ++nqq;
+            }
           }
         }
       }
@@ -799,7 +806,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         load_raw(cur, 0, nfull_n > 0, a.pad, packed, rlo, rhi);
       }
       const int slot = g & 1;
-      if (seg_in && wave == 0 && (!last || nunit < nunits))  // next chunk's boundary row
+      // next chunk's boundary row (never past the last unit's edge rows)
+      if (seg_in && wave == 0 && (last ? nunit < nunits : (MQ ? unit : tile) < nunits))
         dma_edge_chunk(a.edge_in + ((size_t)(last ? nunit : MQ ? unit : tile) * a.ecols +
                                     (size_t)(last ? 0 : c + 1) * C) * 64,
                        ein + (size_t)((g + 1) & 1) * C * 64, lane);
@@ -978,7 +986,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         best = (u16x2){0, 0};
         prevUpH = H0;
         tile = ntile;
-        if constexpr (MQ) {  // several queries: the next unit's row LUTs
+        if constexpr (MQ && PAIR) unit = nunit;
+        if constexpr (MQ && !PAIR) {  // several queries: the next unit's row LUTs
           unit = nunit;
           if (nqq != q) {
             q = nqq;
@@ -1059,7 +1068,8 @@ static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, h
     attr_set = true;
   }
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
-  const unsigned grid = persistent_grid(reinterpret_cast<const void*>(fn), ntiles, 64 * W, lds);
+  unsigned grid = persistent_grid(reinterpret_cast<const void*>(fn), ntiles, 64 * W, lds);
+  if (MQ && PAIR) grid = std::max(a.nq, grid / a.nq * a.nq);  // one query per workgroup
   hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * W), (unsigned)lds, st, a);
   return hipGetLastError();
 }
@@ -1721,6 +1731,11 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
   a.qwords = qwords;
   a.sstride = sstride;
   const uint32_t prof_bytes = (pad + 1) * PS;
+  if (nq > 1 && pair) {  // several queries, pair tables (PS = one table's bytes)
+    if (R == 32 && f16 && !prof && !gotoh && !col0)
+      return swk::launch_score<32, 4, false, false, false, true, true, true>(a, W, 0, st);
+    return hipErrorInvalidValue;
+  }
   if (nq > 1) {  // several queries: row-LUT variants without the column-0 rule
 #define SWK_MQ_CASE(RR, GT, FH)                                                                  \
   if (R == RR && RB == 4 && !col0 && !prof && !pair && gotoh == GT && f16 == FH)                 \

@@ -160,3 +160,29 @@ def test_query_set_api_rules():
         got = bank.score_targets(seqs)
     res, offs, lens = O.pack_residues(seqs)
     assert np.array_equal(got, O.score_batch(queries[1], res, offs, lens, O.dna_matrix(), -12, -4))
+
+
+@pytest.mark.parametrize("nq", [2, 5, 16, 33])
+def test_query_set_pair_tables(monkeypatch, nq):
+    """DNA merged f16 sets run on letter-pair tables in 128-row segments, one query per
+    workgroup (the grid a multiple of nq): equal to the row-LUT variant (SWBANK_MQ_PAIR=0) and
+    the oracle, for set sizes that do and do not divide the resident slots."""
+    monkeypatch.setenv("SWBANK_KERNEL", "tile")
+    rng = np.random.default_rng(nq)
+    queries = [rng.integers(0, 4, int(rng.integers(60, 700)), dtype=np.uint8) for _ in range(nq)]
+    seqs = _targets(rng, 900, 0, 150, 4, queries, p_n=0.01)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(5, -4, -12, -4)
+        bank.load_queries(queries)
+        got = _score_set(bank, queries, seqs)
+        kern = bank.last_kernel()
+        assert " pair " in kern and f"queries={nq}" in kern, kern
+        monkeypatch.setenv("SWBANK_MQ_PAIR", "0")
+        bank.load_queries(queries)  # the tables are rebuilt without pair tables
+        lut = _score_set(bank, queries, seqs)
+        assert " pair " not in bank.last_kernel()
+    assert np.array_equal(got, lut), kern
+    want = _oracle_set(queries, seqs, O.dna_matrix(), -12, -4, O.GAP_MERGED)
+    bad = np.argwhere(got != want)
+    assert bad.size == 0, (kern, [(int(i), int(k), int(got[i, k]), int(want[i, k]))
+                                  for i, k in bad[:6]])
