@@ -14,7 +14,7 @@ if [ -d $O/prof_${TAG}_reads ]; then
   python scripts/collect_profiles.py "$TAG" $O/prof_${TAG}_reads $O/pmc_${TAG}_reads \
     reads150x131072x1k16 score_kernel reads > /dev/null
   python scripts/pmc_decompose.py profiles/$TAG/pmc_summary_reads150x131072x1k16.json \
-    $((500 * 16 * 131072 * 150)) profiles/$TAG/pmc_decomposition_reads.json | grep -E "valu_instr|valu_busy"
+    $((125 * 16 * 131072 * 150)) profiles/$TAG/pmc_decomposition_reads.json | grep -E "valu_instr|valu_busy"
 fi
 python scripts/pmc_decompose.py profiles/$TAG/pmc_summary.json $((128 * 1021952 * 128)) \
   profiles/$TAG/pmc_decomposition.json | grep -E "valu_instr|valu_busy|kernel_ms"
