@@ -95,6 +95,9 @@ struct PhaseTrace {
       marks.push_back({what, std::chrono::duration<double, std::micro>(
                                  std::chrono::steady_clock::now() - t0).count()});
   }
+  void mark_at(const char* what, std::chrono::steady_clock::time_point t) {
+    if (path) marks.push_back({what, std::chrono::duration<double, std::micro>(t - t0).count()});
+  }
   ~PhaseTrace() {
     if (!path || marks.empty()) return;
     if (FILE* f = std::fopen(path, "a")) {
@@ -130,8 +133,31 @@ struct DevBuf {
   }
 };
 
+// Device memory the caches do not keep (hipDeviceMallocUncached): a streamed batch's codes land
+// there by DMA while the kernel that reads them runs, so no cache line can be stale.
+struct UcBuf {
+  uint8_t* p = nullptr;
+  size_t cap = 0;  // bytes
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&p), n, hipDeviceMallocUncached);
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
 // Pinned host staging for the query tables (so their uploads are truly asynchronous).
+// `flags`: hipHostMallocCoherent for words a running kernel reads (streamed chunk records).
 struct PinBuf {
+  unsigned flags = hipHostMallocDefault;
   uint8_t* p = nullptr;
   size_t cap = 0;  // bytes
   hipError_t reserve(size_t n) {
@@ -140,7 +166,7 @@ struct PinBuf {
     p = nullptr;
     cap = 0;
     const size_t want = std::max<size_t>(n, 4096);
-    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), want, flags);
     if (e == hipSuccess) cap = want;
     return e;
   }
@@ -309,6 +335,22 @@ struct sw_bank {
   double host_pack_ms = 0;         // feeder gather time of host calls (with timing on)
   DevBuf<uint8_t> dslot[NSLOT];
   DevBuf<uint32_t> sortscr[NSLOT];  // device sort scratch of each slot's chunk
+  // streamed host batches (one kernel for the whole call, equal-length DNA): the batch's codes
+  // (chunks 256-byte aligned: no cache line holds two chunks, and nothing of a chunk is read
+  // before its layout word is set, so no line is cached before its copy landed), the chunks'
+  // device layout words (uncached device memory), the chunk records (device,
+  // staged in srec, which also takes the layout words back), the host layout words (coherent
+  // host memory), a copy event per chunk
+  DevBuf<uint8_t> sbuf;
+  UcBuf sflag;
+  DevBuf<SwkStreamChunk> sdrec;
+  DevBuf<uint32_t> sctr;  // tiles the streamed kernel's workgroups took
+  // the streamed kernel's stream: a queue of its own (a CU-masked stream, every CU set), so no
+  // copy-stream marker the publisher waits on can sit behind the running kernel in a queue
+  // shared with another stream
+  hipStream_t kstream = nullptr;
+  PinBuf srec, shflag{hipHostMallocCoherent};
+  std::vector<hipEvent_t> sev;
   std::unique_ptr<HostPool> pool;
 
   // workspaces
@@ -586,6 +628,15 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
     b->hslot[i].release();
     b->dslot[i].release();
     b->sortscr[i].release();
+  }
+  b->sbuf.release();
+  b->sflag.release();
+  b->sdrec.release();
+  b->sctr.release();
+  b->srec.release();
+  b->shflag.release();
+  for (hipEvent_t e : b->sev) (void)hipEventDestroy(e);
+  for (int i = 0; i < sw_bank::NSLOT; ++i) {
     if (b->h2d_done[i]) (void)hipEventDestroy(b->h2d_done[i]);
     if (b->kern_done[i]) (void)hipEventDestroy(b->kern_done[i]);
   }
@@ -594,6 +645,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   if (b->copy_stream) (void)hipStreamDestroy(b->copy_stream);
   if (b->out_stream) (void)hipStreamDestroy(b->out_stream);
   if (b->stream2) (void)hipStreamDestroy(b->stream2);
+  if (b->kstream) (void)hipStreamDestroy(b->kstream);
   if (b->ev_s2) (void)hipEventDestroy(b->ev_s2);
   b->res.release();
   b->offs.release();
@@ -1904,6 +1956,284 @@ static bool scratch_free(const sw_bank* b, uint32_t max_len) {
   return b->segs.size() == 1 && b->wsegs == 1 && !need32 && !opt16;
 }
 
+// Streamed host batch: every target L codes long (DNA, one query segment, exact 16-bit
+// arithmetic, the tile kernel, enough tiles for two rounds of the resident workgroups).  ONE
+// kernel launch scores the whole call: chunks of whole tiles are gathered (2-bit, or 4-bit from
+// the first chunk holding an N on) into the pinned slots and copied to their own ranges of an
+// device buffer; a publisher thread sets a chunk's host layout word once its copy
+// landed, and the kernel's waves wait on it before they read the chunk (swk_launch_stream).
+// One pipeline fill and drain per call instead of one per chunk, and no chunk kernel on half
+// the chip.  `used` = false when the batch does not qualify (the chunked feeder runs instead;
+// always for a multi-device bank's per-device parts, out == nullptr); SWBANK_STREAM=0 disables.
+static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
+                             const uint64_t* offsets, size_t n, uint32_t L, int32_t* out,
+                             bool& used) {
+  used = false;
+  const int mode_env = env_int("SWBANK_STREAM", 1);  // 2: also below the size threshold (tests)
+  if (mode_env == 0 || !out || b->alpha != SW_DNA_ALPHA || b->prof || b->col0 || b->RB != 4 ||
+      env_int("SWBANK_PACK2", 1) == 0 || env_int("SWBANK_UNIFORM", 1) == 0 ||
+      !scratch_free(b, L) || n > 0x7FFFFFFFull)
+    return SW_OK;
+  const char* kforce = std::getenv("SWBANK_KERNEL");
+  if (kforce && std::strcmp(kforce, "wave") == 0) return SW_OK;
+  const size_t T = (n + SWB_TILE - 1) / SWB_TILE;
+  // two rounds of 4 workgroups per CU: the throughput model picks the tile kernel there
+  if (mode_env != 2 && T < 8 * (size_t)std::max(b->cus, 1)) return SW_OK;
+  const uint64_t smax = (uint64_t)std::max(0, b->smax);
+  const bool use_f16 = b->f16 && b->f16_neg >= -2048 && env_int("SWBANK_F16", 1) != 0 &&
+                       std::min<uint64_t>(b->query.size(), L) * smax + smax <= 2048u;
+  const bool pair = use_f16 && b->pair_bytes != 0 && env_int("SWBANK_PAIR", 1) != 0;
+  if (!(b->R == 16 || (b->R == 32 && !b->gotoh()))) return SW_OK;  // streamed variants
+  used = true;
+
+  // chunks of whole tiles: 1/64 of the batch first, doubling up to 1/8
+  std::vector<size_t> tile0;
+  const size_t cap = std::max<size_t>(1, T / 8);
+  for (size_t t = 0, sz = std::max<size_t>(1, T / 64); t < T; t += sz, sz = std::min(cap, 2 * sz))
+    tile0.push_back(t);
+  const size_t nsc = tile0.size();
+  tile0.push_back(T);
+  const size_t nib = (L + 1) / 2;  // 4-bit bytes per target (the 2-bit stream needs fewer)
+  std::vector<size_t> roff(nsc + 1, 0);
+  size_t slot_bytes = 0;
+  for (size_t i = 0; i < nsc; ++i) {
+    const size_t cnt = std::min(n, tile0[i + 1] * SWB_TILE) - tile0[i] * SWB_TILE;
+    roff[i + 1] = roff[i] + (cnt * nib + 64 + 255) / 256 * 256;
+    slot_bytes = std::max(slot_bytes, roff[i + 1] - roff[i]);
+  }
+  HIPOK(b, hipSetDevice(b->device));
+  if (!b->kstream) {
+    std::vector<uint32_t> mask((std::max(b->cus, 1) + 31) / 32, 0xFFFFFFFFu);
+    HIPOK(b, hipExtStreamCreateWithCUMask(&b->kstream, (uint32_t)mask.size(), mask.data()));
+  }
+  hipStream_t ks = b->kstream;
+  HIPOK(b, b->sbuf.reserve(roff[nsc]));
+  HIPOK(b, b->sflag.reserve(nsc * 4));
+  HIPOK(b, b->sdrec.reserve(nsc));
+  HIPOK(b, b->sctr.reserve(1));
+  HIPOK(b, b->srec.reserve(nsc * sizeof(SwkStreamChunk)));
+  HIPOK(b, b->shflag.reserve(nsc * 4));
+  for (int i = 0; i < std::min<int>(sw_bank::NSLOT, (int)nsc); ++i)
+    HIPOK(b, b->hslot[i].reserve(slot_bytes));
+  HIPOK(b, b->scores.reserve(n));
+  HIPOK(b, b->hscores.reserve(n * 4));
+  while (b->sev.size() < nsc) {
+    hipEvent_t e;
+    HIPOK(b, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    b->sev.push_back(e);
+  }
+  SwkStreamChunk* rec = reinterpret_cast<SwkStreamChunk*>(b->srec.p);
+  uint32_t* hflag = reinterpret_cast<uint32_t*>(b->shflag.p);
+  for (size_t i = 0; i < nsc; ++i) {
+    rec[i] = SwkStreamChunk{(unsigned)tile0[i], (unsigned)roff[i], (unsigned)(roff[i] >> 32), 0u};
+    __atomic_store_n(&hflag[i], 0u, __ATOMIC_RELAXED);
+  }
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+
+  // records and cleared device words, then the kernel (its waves wait on the layout words);
+  // enqueued once chunk 0's copy is, so the gather of chunk 0 starts at once
+  sw_bank::Ev ev{};
+  const auto start_kernel = [&]() -> sw_status {
+    HIPOK(b, hipStreamWaitEvent(ks, b->ev_ready, 0));  // query tables uploaded
+    HIPOK(b, hipStreamWaitEvent(ks, b->ev_used, 0));   // bank scratch free
+    HIPOK(b, hipMemcpyAsync(b->sdrec.p, rec, nsc * sizeof(SwkStreamChunk), hipMemcpyHostToDevice,
+                            ks));
+    HIPOK(b, hipMemsetAsync(b->sflag.p, 0, nsc * 4, ks));
+    HIPOK(b, hipMemsetAsync(b->sctr.p, 0, 4, ks));
+    if (b->timing) {
+      HIPOK(b, hipEventCreate(&ev.a));
+      HIPOK(b, hipEventCreate(&ev.b));
+      HIPOK(b, hipEventCreate(&ev.c));
+      HIPOK(b, hipEventRecord(ev.a, ks));
+      HIPOK(b, hipEventRecord(ev.b, ks));
+    }
+    HIPOK(b, swk_launch_stream(b->R, b->gotoh() ? 1 : 0, use_f16 ? 1 : 0, pair ? 1 : 0, b->sbuf.p,
+                               n, L, b->sdrec.p, hflag, reinterpret_cast<uint32_t*>(b->sflag.p),
+                               (uint32_t)nsc, b->sctr.p,
+                               pair ? b->qpair.p : use_f16 ? b->qtab16.p : b->qtab.p,
+                               use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
+                               pair ? b->pair_bytes : 0, b->pad, b->segs[0].W, b->scores.p,
+                               b->pS1, b->pS2, ks));
+    HIPOK(b, hipEventRecord(b->ev_used, ks));
+    if (b->timing) {
+      HIPOK(b, hipEventRecord(ev.c, ks));
+      b->events.push_back(ev);
+    }
+    snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=1 streamed=%zu",
+             use_f16 ? "f16" : "u16", pair ? " pair" : "", b->R, b->segs[0].W, nsc);
+    trace_mark("kernel");
+    return SW_OK;
+  };
+
+  // the publisher: chunk i's layout word once its copy event completed (issued chunks only)
+  std::vector<uint32_t> mode(nsc, 0);
+  std::vector<std::chrono::steady_clock::time_point> pub_t(nsc);  // (SWBANK_TRACE_FILE)
+  std::atomic<size_t> issued{0};
+  std::atomic<bool> stop{false};
+  std::thread publisher([&] {
+    for (size_t i = 0; i < nsc; ++i) {
+      while (issued.load(std::memory_order_acquire) <= i && !stop.load()) std::this_thread::yield();
+      if (issued.load(std::memory_order_acquire) <= i) return;
+      while (hipEventQuery(b->sev[i]) == hipErrorNotReady) std::this_thread::yield();
+      __atomic_store_n(&hflag[i], mode[i], __ATOMIC_RELEASE);
+      pub_t[i] = std::chrono::steady_clock::now();
+    }
+  });
+
+  HostPool& pool = *b->pool;
+  const unsigned PT = pool.size();
+  const bool avx2 = env_int("SWBANK_AVX2", 1) != 0;
+  const swpack::PackFn pack2fn = swpack::packer(2, avx2), pack4fn = swpack::packer(4, avx2);
+  const size_t steps32 = (L + 31u) / 32u;
+  bool nib_mode = false;  // from the first chunk holding an N on: 4-bit chunks
+  std::atomic<size_t> oob{SIZE_MAX};
+  std::atomic<uint32_t> wide{0};
+  sw_status err = SW_OK;
+  bool started = false;  // the kernel is enqueued
+  for (size_t i = 0; i < nsc && err == SW_OK; ++i) {
+    const int s = (int)(i % sw_bank::NSLOT);
+    if (i >= (size_t)sw_bank::NSLOT) {
+      const hipError_t e = hipEventSynchronize(b->h2d_done[s]);
+      if (e != hipSuccess) {
+        fail(b, SW_ERR_HIP, "hipEventSynchronize: %s", hipGetErrorString(e));
+        err = SW_ERR_HIP;
+        break;
+      }
+    }
+    const size_t c0 = tile0[i] * SWB_TILE, c1 = std::min(n, tile0[i + 1] * SWB_TILE);
+    const size_t cnt = c1 - c0, step = (cnt + PT - 1) / PT;
+    uint8_t* codes = b->hslot[s].p;
+    trace_mark("gather<");
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t md = 0;
+    size_t sb = 0;
+    for (int pass = nib_mode ? 1 : 0; pass < 2 && md == 0; ++pass) {
+      sb = pass == 0 ? (L + 3) / 4 : nib;
+      const size_t stepb = pass == 0 ? 8 : 16;  // bytes one 32-code vector step stores
+      const swpack::PackFn fn = pass == 0 ? pack2fn : pack4fn;
+      wide = 0;
+      pool.run([&](unsigned p) {
+        const size_t lo = std::min(cnt, p * step), hi = std::min(cnt, (p + 1) * step);
+        uint32_t acc = 0;
+        for (size_t j = lo; j < hi; ++j) {
+          const size_t k = c0 + j;
+          if (offsets[k] > nres || L > nres - offsets[k]) {
+            size_t cur = oob.load();
+            while (k < cur && !oob.compare_exchange_weak(cur, k)) {
+            }
+            return;
+          }
+          // full vector steps past the target's end stay inside this part's output (later
+          // targets of the part rewrite those bytes) and read inside the residues
+          const bool w = offsets[k] + steps32 * 32 <= nres && j * sb + steps32 * stepb <= hi * sb;
+          const uint32_t v = fn(residues + offsets[k], L, codes + j * sb, w);
+          acc = pass == 0 ? (acc | v) : std::max(acc, v);
+        }
+        if (pass == 0 ? acc > 3u : acc >= (uint32_t)SW_DNA_ALPHA) wide = 1;
+      });
+      if (oob.load() != SIZE_MAX) break;
+      if (wide.load() == 0) md = pass == 0 ? SWK_PACK_STREAM : SWK_PACK_NIBBLE;
+      else if (pass == 0) nib_mode = true;
+    }
+    if (b->timing)
+      b->host_pack_ms +=
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    trace_mark("gather>");
+    if (oob.load() != SIZE_MAX) {
+      const size_t k = oob.load();
+      fail(b, SW_ERR_ARG, "target %zu [%llu, +%u) outside the %zu residues", k,
+           (unsigned long long)offsets[k], L, nres);
+      err = SW_ERR_ARG;
+      break;
+    }
+    if (md == 0) {  // a code outside the alphabet: the first such target
+      for (size_t j = 0; j < cnt && err == SW_OK; ++j)
+        for (uint32_t x = 0; x < L; ++x)
+          if (residues[offsets[c0 + j] + x] >= (uint8_t)SW_DNA_ALPHA) {
+            fail(b, SW_ERR_ARG, "target %zu code %u outside alphabet", c0 + j,
+                 (unsigned)residues[offsets[c0 + j] + x]);
+            err = SW_ERR_ARG;
+            break;
+          }
+      if (err == SW_OK) err = fail(b, SW_ERR_ARG, "code outside alphabet");
+      break;
+    }
+    const size_t bytes = cnt * sb;
+    std::memset(codes + bytes, 0, 16);  // the last targets' final step reads a few bytes past
+    const hipError_t e1 = hipMemcpyAsync(b->sbuf.p + roff[i], codes, bytes + 16,
+                                         hipMemcpyHostToDevice, b->copy_stream);
+    const hipError_t e2 = e1 != hipSuccess ? e1 : hipEventRecord(b->h2d_done[s], b->copy_stream);
+    const hipError_t e3 = e2 != hipSuccess ? e2 : hipEventRecord(b->sev[i], b->copy_stream);
+    if (e3 != hipSuccess) {
+      fail(b, SW_ERR_HIP, "streamed chunk copy: %s", hipGetErrorString(e3));
+      err = SW_ERR_HIP;
+      break;
+    }
+    mode[i] = md;
+    issued.store(i + 1, std::memory_order_release);
+    trace_mark("launched");
+    if (i == 0 && (err = start_kernel()) != SW_OK) break;
+    started = i == 0 || started;
+  }
+  // on failure the chunks never sent are released to the kernel as aborted (it reads whatever
+  // their range holds) so it drains; the call reports the error
+  stop.store(true);
+  publisher.join();
+  if (g_trace)
+    for (size_t i = 0; i < issued.load(); ++i) g_trace->mark_at("published", pub_t[i]);
+  for (size_t i = issued.load(); i < nsc; ++i)
+    __atomic_store_n(&hflag[i], SWK_STREAM_ABORT, __ATOMIC_RELEASE);
+  if (!started) {  // nothing enqueued on the bank stream; chunk 0's copy may be in flight
+    (void)hipStreamSynchronize(b->copy_stream);
+    return err;
+  }
+  // the scores and the layout words back only now: a copy enqueued behind the kernel may hold
+  // the copy engine the chunks' copies need until the kernel ends (seen as chunks that never
+  // reach the kernel)
+  if (err == SW_OK) {
+    hipError_t e = hipMemcpyAsync(b->hscores.p, b->scores.p, n * 4, hipMemcpyDeviceToHost,
+                                  ks);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(rec, b->sflag.p, nsc * 4, hipMemcpyDeviceToHost, ks);
+    if (e != hipSuccess) err = fail(b, SW_ERR_HIP, "streamed scores: %s", hipGetErrorString(e));
+  }
+  const hipError_t se = hipStreamSynchronize(ks);
+  if (err != SW_OK) return err;
+  if (se != hipSuccess) return fail(b, SW_ERR_HIP, "streamed batch: %s", hipGetErrorString(se));
+  trace_mark("landed");
+  // a chunk whose wait ran out (its copy held up past the kernel's bound, e.g. by other work on
+  // the device's copy engines): the call runs again through the chunked feeder
+  const uint32_t* dflag = reinterpret_cast<const uint32_t*>(rec);
+  for (size_t i = 0; i < nsc; ++i)
+    if (dflag[i] == SWK_STREAM_ABORT) {
+      used = false;
+      return SW_OK;
+    }
+  // scores into the caller's buffer with the best hit (lowest index of the maximum)
+  const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
+  std::vector<size_t> pbest(PT, SIZE_MAX);
+  const size_t ostep = (n + PT - 1) / PT;
+  pool.run([&](unsigned p) {
+    const size_t lo = std::min(n, p * ostep), hi = std::min(n, (p + 1) * ostep);
+    size_t bi = lo;
+    for (size_t k = lo; k < hi; ++k) {
+      const int32_t v = hs[k];
+      out[k] = v;
+      if (v > hs[bi]) bi = k;
+    }
+    if (lo < hi) pbest[p] = bi;
+  });
+  size_t best = 0;
+  for (size_t x : pbest)  // parts in index order: strictly greater keeps the lowest
+    if (x != SIZE_MAX && hs[x] > hs[best]) best = x;
+  b->best_index = best;
+  b->best_id = best;
+  b->best_score = hs[best];
+  b->best_kind = 1;
+  trace_mark("done");
+  return SW_OK;
+}
+
 // The host-buffer batch through the feeder (n >= 1, buffers checked by the caller).
 static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                             const uint64_t* offsets, const uint32_t* lens, size_t n,
@@ -1924,22 +2254,30 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     else f(0u);
   };
   std::vector<size_t> psum(P + 1, 0);
-  std::vector<uint32_t> pmax(P, 0);
+  std::vector<uint32_t> pmax(P, 0), pmin(P, UINT32_MAX);
   run_parts([&](unsigned p) {
     size_t acc = 0;
-    uint32_t m = 0;
+    uint32_t m = 0, mn = UINT32_MAX;
     for (size_t k = std::min(n, p * pstep); k < std::min(n, (p + 1) * pstep); ++k) {
       acc += lens[k];
       m = std::max(m, lens[k]);
+      mn = std::min(mn, lens[k]);
     }
     psum[p + 1] = acc;
     pmax[p] = m;
+    pmin[p] = mn;
   });
   for (unsigned p = 0; p < P; ++p) psum[p + 1] += psum[p];
   trace_mark("lens-pass");
   const size_t total = psum[P];
   const uint32_t max_len = *std::max_element(pmax.begin(), pmax.end());
   if (max_len && !residues) return fail(b, SW_ERR_ARG, "null residues");
+  // equal-length DNA batches: one streamed kernel for the whole call (stream_feed)
+  if (max_len && *std::min_element(pmin.begin(), pmin.end()) == max_len) {
+    bool used = false;
+    st = stream_feed(b, residues, nres, offsets, n, max_len, out, used);
+    if (used) return st;
+  }
   // slot: offsets u64 | lens | perm | count | ident (SlotTail) | codes at codes_at(cnt): one byte per
   // residue, or, for a DNA chunk without N, the 2-bit stream (a quarter of the PCIe bytes;
   // SWBANK_PACK2=0 disables), each target from a byte boundary, 16 zero bytes after the last

@@ -38,4 +38,26 @@ typedef struct SwkWaveSplit {
   void* ring;
 } SwkWaveSplit;
 
+/* One chunk of a streamed host batch (uploaded before the launch): its first tile and the
+ * offset of its codes in the device batch buffer.  Its code layout travels in a flag word per
+ * chunk, 0 until the chunk's copy landed, then SWK_PACK_STREAM or SWK_PACK_NIBBLE;
+ * SWK_STREAM_ABORT from a wave whose wait ran out (read as 2-bit codes; the host fails the
+ * call). */
+typedef struct SwkStreamChunk {
+  unsigned tile0, res_off_lo, res_off_hi, pad;
+} SwkStreamChunk;
+#define SWK_STREAM_ABORT 0xFFFFFFFFu
+
+#ifdef __cplusplus
+/* (declared here so the definition in swbank_kernels.hip and the call in swbank_device.hip are
+ * checked against one signature) */
+extern "C" hipError_t swk_launch_stream(int R, int gotoh, int f16, int pair, const uint8_t* res,
+                                        size_t n, uint32_t ulen, const SwkStreamChunk* sc,
+                                        const uint32_t* hflag, uint32_t* dflag, uint32_t nsc,
+                                        uint32_t* tctr, const uint32_t* qtab, uint32_t nv,
+                                        uint32_t S, uint32_t O, uint32_t E, uint32_t PS,
+                                        uint32_t pad, int W, int32_t* scores, uint32_t pS1,
+                                        uint32_t pS2, hipStream_t st);
+#endif
+
 #endif

@@ -574,6 +574,17 @@ struct ScoreArgs {
   // query q - 1's, its scores sstride entries after; edge rows are per unit.  nq <= 1: one query
   uint32_t nq, qwords;
   size_t sstride;
+  // streamed batch (STREAM variants, the host feeder): equal-length targets (ulen codes) in
+  // chunks of whole tiles that land in HBM while the kernel runs; chunk c's record sc[c] (nsc
+  // records) gives its first tile and its codes (res + res_off); its layout word is hflag[c]
+  // in host memory (set by the host once the copy landed) and dflag[c] in uncached device
+  // memory (set by the first wave that saw hflag[c], polled by the others); tiles past the
+  // first G go to workgroups dynamically (tctr: tiles taken, zeroed by the host), so a
+  // workgroup that waited on a late chunk takes fewer tiles.  These travel in fields the
+  // streamed variants never read (no target arrays, no re-score list, one query): sc = offs,
+  // hflag = lens, dflag = nidx, tctr = ident, nsc = qwords -- the argument block keeps its
+  // size (with 40 more bytes here, later launches of every variant read wrong arguments now
+  // and then on MI355X: scores of other targets, or none written)
 };
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -623,10 +634,36 @@ __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens
 // 16 A/C/G/T slots on 16 different 4-bank groups (conflict-free ds_read_b128).  A column of
 // wave w reads its row words as 4 blocks of 8 (two ds_read_b128 each), one block ahead of
 // the asm block that consumes them: 6.5 VALU per 2 cells instead of 7.5.
+// Wave-uniform code layout of streamed chunk c, waiting until its copy landed.  Every wait
+// polls the device word; one poll in 16 (staggered by workgroup) also reads the host word over
+// PCIe, and the wave that sees it set copies it to the device word for the others.  Bounded
+// (2^20 polls, about a second): a wave that runs out marks the chunk SWK_STREAM_ABORT.
+__device__ __forceinline__ uint32_t stream_mode(const uint32_t* hflag, uint32_t* dflag, int c,
+                                                int lane) {
+  for (int it = 0; it < (1 << 20); ++it) {
+    uint32_t v = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(dflag + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
+    if (v) return v;
+    if (((it + (int)blockIdx.x) & 15) == 0) {
+      v = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(hflag + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+      if (v) {
+        if (lane == 0) __hip_atomic_store(dflag + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return v;
+      }
+    }
+    __builtin_amdgcn_s_sleep(16);
+  }
+  if (lane == 0)
+    __hip_atomic_store(dflag + c, SWK_STREAM_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return SWK_STREAM_ABORT;
+}
+
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
-          bool MQ = false>
+          bool MQ = false, bool STREAM = false>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
   static_assert(!MQ || !PROF, "several queries: row-LUT or pair-table variants");
+  static_assert(!STREAM || (!MQ && !PROF), "streamed batches: single-query LUT / pair variants");
   constexpr int C = 8;
   static_assert(!PAIR || (R == 32 && F16 && !PROF && !GOTOH && !COL0), "PAIR: f16 merged R=32");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -655,10 +692,51 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   // (MQ only; otherwise unit = tile and q = 0)
   const int nunits = MQ ? ntiles * (int)a.nq : ntiles;
   int total = 0;  // chunks of all this workgroup's tiles: every wave runs total + W - 1 phases
-  const uint32_t packed = a.packed;
-  for (int u = blockIdx.x; u < nunits; u += G)  // (the unit's tile: see the MQ order below)
-    total += tile_nch(a.res, a.lens, n, !MQ ? u : PAIR ? u / (int)a.nq : u % ntiles, lane, packed,
-                      idx, a.ulen, a.ustride);
+  uint32_t packed = a.packed;
+  // STREAM: tiles taken dynamically, so the total is open until wave 0 finds no tile left
+  // (it then stores it in sq[W]; every wave reads sq[W] at each phase)
+  int* sq = reinterpret_cast<int*>(prof);  // STREAM: next tile of ordinal k at [k % W] | total
+  if constexpr (STREAM) {
+    total = (int)blockIdx.x < ntiles ? (1 << 30) : 0;
+  } else {
+    for (int u = blockIdx.x; u < nunits; u += G)  // (the unit's tile: see the MQ order below)
+      total += tile_nch(a.res, a.lens, n, !MQ ? u : PAIR ? u / (int)a.nq : u % ntiles, lane,
+                        packed, idx, a.ulen, a.ustride);
+  }
+  // STREAM: the chunk of this wave's current tile (tiles only grow), its first tile, target
+  // count, code offset and layout
+  // (wave-uniform, kept in SGPRs)
+  const SwkStreamChunk* const ssc = reinterpret_cast<const SwkStreamChunk*>(a.offs);
+  const int snc = (int)a.qwords;
+  int scur = -1, st0 = 0;
+  uint32_t scn = 0, sro_lo = 0, sro_hi = 0, smode = SWK_PACK_STREAM;
+  const auto stream_tile = [&](int t, uint32_t& pk) -> Lane2 {
+    if (t >= ntiles) {  // past the batch: reads nothing
+      pk = SWK_PACK_STREAM;
+      Lane2 e;
+      e.llo = e.lhi = 0u;
+      e.plo = e.phi = a.res;
+      return e;
+    }
+    int c = scur < 0 ? 0 : scur;
+    while (c + 1 < snc && t >= (int)ssc[c + 1].tile0) ++c;
+    if (c != scur) {
+      scur = __builtin_amdgcn_readfirstlane(c);
+      st0 = __builtin_amdgcn_readfirstlane((int)ssc[c].tile0);
+      scn = __builtin_amdgcn_readfirstlane(
+          (uint32_t)((c + 1 < snc ? (size_t)ssc[c + 1].tile0 * SWB_TILE : n) -
+                     (size_t)st0 * SWB_TILE));
+      sro_lo = __builtin_amdgcn_readfirstlane(ssc[c].res_off_lo);
+      sro_hi = __builtin_amdgcn_readfirstlane(ssc[c].res_off_hi);
+      smode = stream_mode(a.lens, const_cast<uint32_t*>(a.nidx), c, lane) == SWK_PACK_NIBBLE
+                  ? SWK_PACK_NIBBLE
+                  : SWK_PACK_STREAM;
+    }
+    pk = smode;
+    return lane_targets(a.res + ((size_t)sro_hi << 32 | sro_lo), nullptr, nullptr, scn, t - st0,
+                        lane, pk, nullptr, a.ulen,
+                        pk == SWK_PACK_NIBBLE ? (a.ulen + 1) / 2 : (a.ulen + 3) / 4);
+  };
 
   // MQ order: row LUTs query-major (q = unit / ntiles; a wave reloads its LUT SGPRs when the
   // query changes); pair tables query-minor (q = unit % nq) with the grid a multiple of nq, so
@@ -671,7 +749,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       tile = PAIR ? unit / (int)a.nq : unit - q * ntiles;
     }
   }
-  Lane2 cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen, a.ustride);
+  Lane2 cur;
+  if constexpr (STREAM) cur = stream_tile(tile, packed);
+  else cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen, a.ustride);
   int nch, nfull;
   tile_chunks(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
               nfull);
@@ -727,6 +807,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   u16x2 prevUpH = H0;  // H(row above, column -1)
   uint2 rlo, rhi;      // raw codes of the next chunk (prefetched one phase ahead)
   load_raw(cur, 0, nfull > 0, a.pad, packed, rlo, rhi);
+  if (STREAM && threadIdx.x == 0) sq[W] = total;
   __syncthreads();
 
   // PAIR: column state one column ahead: acur = this column's table address (slot + this
@@ -775,13 +856,31 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const uint32_t padc = a.pad;
   int c = 0, k = 0;           // chunk within the current tile, tile ordinal in this workgroup
   int nch_n = 1, nfull_n = 0;  // the next tile's chunk counts
-  const int nph = total + W - 1;
-  for (int ph = 0; ph < nph; ++ph) {
+  uint32_t packed_n = packed;  // STREAM: the next tile's code layout
+  for (int ph = 0;; ++ph) {
+    if constexpr (STREAM) total = __builtin_amdgcn_readfirstlane(sq[W]);
+    if (ph >= total + W - 1) break;
     const int g = ph - wave;
     if (g >= 0 && g < total) {
       const uint2 clo = rlo, chi = rhi;
       const bool last = c + 1 == nch;
-      const int nunit = (MQ ? unit : tile) + G;
+      int nunit = (MQ ? unit : tile) + G;
+      if constexpr (STREAM) {  // wave 0 takes the next tile; the others read it W-1 phases on
+        if (last) {
+          if (wave == 0) {
+            int nt = 0;
+            if (lane == 0) nt = G + (int)atomicAdd(const_cast<uint32_t*>(a.ident), 1u);
+            nt = min(__builtin_amdgcn_readfirstlane(nt), ntiles);
+            if (lane == 0) {
+              sq[(k + 1) % W] = nt;
+              if (nt >= ntiles) sq[W] = g + 1;
+            }
+            nunit = nt;
+          } else {
+            nunit = __builtin_amdgcn_readfirstlane(sq[(k + 1) % W]);
+          }
+        }
+      }
       int ntile = nunit, nqq = q;  // the next unit's tile and query
       if constexpr (MQ) {
         if (nunit < nunits) {
@@ -799,11 +898,13 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       if (!last) {
         load_raw(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
       } else if (nunit < nunits) {  // first chunk of the next tile
-        cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed, idx, a.ulen,
-                           a.ustride);
+        if constexpr (STREAM) cur = stream_tile(ntile, packed_n);
+        else
+          cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed, idx, a.ulen,
+                             a.ustride);
         tile_chunks(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
                     n, nch_n, nfull_n);
-        load_raw(cur, 0, nfull_n > 0, a.pad, packed, rlo, rhi);
+        load_raw(cur, 0, nfull_n > 0, a.pad, STREAM ? packed_n : packed, rlo, rhi);
       }
       const int slot = g & 1;
       // next chunk's boundary row (never past the last unit's edge rows)
@@ -986,6 +1087,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         best = (u16x2){0, 0};
         prevUpH = H0;
         tile = ntile;
+        if constexpr (STREAM) packed = packed_n;
         if constexpr (MQ && PAIR) unit = nunit;
         if constexpr (MQ && !PAIR) {  // several queries: the next unit's row LUTs
           unit = nunit;
@@ -1052,14 +1154,14 @@ static unsigned persistent_grid(const void* fn, size_t ntiles, int threads, size
 }
 
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
-          bool MQ = false>
+          bool MQ = false, bool STREAM = false>
 static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st) {
   const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE * (MQ ? a.nq : 1);  // units
   const size_t lds = (size_t)W * SWB_TILE * 4 +
                      (size_t)(64 + (a.edge_out ? 8 * 64 : 64) + (a.edge_in ? 2 * 8 * 64 : 0) +
                               (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8 +
-                     (PROF ? prof_bytes : 0) + (PAIR ? a.PS : 0);
-  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR, MQ>;
+                     (PROF ? prof_bytes : 0) + (PAIR ? a.PS : 0) + (STREAM ? 256 : 0);
+  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR, MQ, STREAM>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -1756,6 +1858,44 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                                                                prof_bytes, st);
   SWK_VARIANTS(SWK_CASE)
 #undef SWK_CASE
+  return hipErrorInvalidValue;
+}
+
+// Streamed host batch (the feeder's one-launch path): equal-length targets (ulen codes), the
+// chunk records `sc` and layout words dflag (device) / hflag (host), the codes in the device
+// buffer `res`; row-LUT or
+// pair-table variants without the column-0 rule, one query segment.
+extern "C" hipError_t swk_launch_stream(int R, int gotoh, int f16, int pair, const uint8_t* res,
+                                        size_t n, uint32_t ulen, const SwkStreamChunk* sc,
+                                        const uint32_t* hflag, uint32_t* dflag, uint32_t nsc,
+                                        uint32_t* tctr, const uint32_t* qtab, uint32_t nv,
+                                        uint32_t S, uint32_t O, uint32_t E, uint32_t PS,
+                                        uint32_t pad, int W, int32_t* scores, uint32_t pS1,
+                                        uint32_t pS2, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (!sc || !hflag || !dflag || !tctr || nsc == 0 || ulen == 0) return hipErrorInvalidValue;
+  swk::ScoreArgs a{res,  nullptr, nullptr, n, qtab, nv, S, O, E, PS, pad, scores, nullptr, nullptr,
+                   0u, 0u, (uint32_t)SWK_PACK_STREAM, nullptr, nullptr, 0u, nullptr, pS1, pS2,
+                   swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
+                   swk::f16_pair(-(int)O), nullptr, 0u, 0u, 0};
+  a.ulen = ulen;
+  a.offs = reinterpret_cast<const uint64_t*>(sc);  // (see ScoreArgs: the streamed fields)
+  a.lens = hflag;
+  a.nidx = dflag;
+  a.ident = tctr;
+  a.qwords = nsc;
+  if (pair) {
+    if (R == 32 && f16 && !gotoh)
+      return swk::launch_score<32, 4, false, false, false, true, true, false, true>(a, W, 0, st);
+    return hipErrorInvalidValue;
+  }
+#define SWK_ST_CASE(RR, GT, FH)                                                                  \
+  if (R == RR && gotoh == GT && f16 == FH)                                                       \
+    return swk::launch_score<RR, 4, false, false, (GT != 0), (FH != 0), false, false, true>(     \
+        a, W, 0, st);
+  SWK_ST_CASE(32, 0, 1) SWK_ST_CASE(32, 0, 0) SWK_ST_CASE(16, 0, 1) SWK_ST_CASE(16, 0, 0)
+  SWK_ST_CASE(16, 1, 1) SWK_ST_CASE(16, 1, 0)
+#undef SWK_ST_CASE
   return hipErrorInvalidValue;
 }
 

@@ -1,0 +1,194 @@
+"""GPU: streamed host batches (sw_score_batch on equal-length DNA targets): one kernel launch
+for the whole call, chunks of whole tiles published to the running kernel as their copies land
+(swbank_device.hip stream_feed, swbank_kernels.hip STREAM variants).  Scores must equal the
+chunked feeder's (SWBANK_STREAM=0, itself checked against the oracle in test_gpu_feeder.py) and
+the oracle's on a sample; the best hit the lowest index of the maximum; a bad code or a target
+outside the residues fails the call and leaves the bank usable."""
+import numpy as np
+import pytest
+
+import swbank as S
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+REF = (5, -4, -12, -4)
+
+
+def _uniform(rng, n, L, p_n=0.0):
+    res = rng.integers(0, 4, n * L, dtype=np.uint8)
+    if p_n:
+        res[rng.random(res.size) < p_n] = 4
+    return res, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32)
+
+
+def _check(monkeypatch, bank, q, res, offs, lens, params, gotoh, rng, extra=()):
+    got = bank.score_batch(res, offs, lens)
+    kern = bank.last_kernel()
+    best = bank.best()
+    assert "streamed=" in kern, kern
+    monkeypatch.setenv("SWBANK_STREAM", "0")
+    ref = bank.score_batch(res, offs, lens)
+    assert "streamed=" not in bank.last_kernel()
+    monkeypatch.delenv("SWBANK_STREAM")
+    assert np.array_equal(got, ref), kern
+    top = int(np.argmax(got))
+    assert best[1] == int(got[top]) and best[2] == top, (best, top)
+    n = len(lens)
+    sel = np.unique(np.concatenate([rng.choice(n, min(n, 600), replace=False),
+                                    np.arange(min(n, 130)), np.arange(max(0, n - 130), n),
+                                    np.asarray(extra, dtype=np.int64)]))
+    L = int(lens[0])
+    sub = [res[int(offs[k]):int(offs[k]) + L] for k in sel]
+    want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(*params[:2]), *params[2:],
+                         O.GAP_GOTOH if gotoh else O.GAP_MERGED)
+    assert np.array_equal(got[sel], want), kern
+    return kern
+
+
+@pytest.mark.parametrize("L", [150, 33, 1])
+def test_stream_pair_f16(monkeypatch, L):
+    """The headline form: f16 letter-pair tables, 2-bit chunks, a full-size batch (>= two
+    rounds of resident workgroups) and a forced small one (fewer tiles than chunks' minimum)."""
+    rng = np.random.default_rng(L)
+    n = 300_000 if L == 150 else 5_000
+    if L != 150:
+        monkeypatch.setenv("SWBANK_STREAM", "2")
+    res, offs, lens = _uniform(rng, n, L)
+    q = rng.integers(0, 4, 100, dtype=np.uint8)
+    for k in range(0, n, 4001):  # local homologs: high scores, a best hit that is not 0
+        a = int(rng.integers(0, 50))
+        m = min(L, 100 - a)
+        res[k * L:k * L + m] = q[a:a + m]
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        if L != 150:
+            monkeypatch.setenv("SWBANK_STREAM", "2")
+        kern = _check(monkeypatch, bank, q, res, offs, lens, REF, False, rng)
+        if L != 150:
+            monkeypatch.delenv("SWBANK_STREAM", raising=False)
+    assert " pair " in kern or L == 1, kern
+
+
+@pytest.mark.parametrize("case", ["nibble-mid", "nibble-all", "u16", "gotoh-f16", "gotoh-u16",
+                                  "lut-f16"])
+def test_stream_variants(monkeypatch, case):
+    """4-bit chunks from the first chunk holding an N on; the row-LUT variants (u16, Gotoh
+    R = 16, f16 without pair tables)."""
+    monkeypatch.setenv("SWBANK_STREAM", "2")
+    rng = np.random.default_rng(len(case) * 7)
+    n, L = 40_000, 120
+    res, offs, lens = _uniform(rng, n, L)
+    extra = []
+    if case == "nibble-mid":  # N codes only from target 25000 on: 2-bit chunks, then 4-bit
+        tail = res[25000 * L:]
+        tail[rng.random(tail.size) < 0.01] = 4
+        extra = list(range(24900, 25100))
+    if case == "nibble-all":
+        res[rng.random(res.size) < 0.02] = 4
+    if case == "lut-f16":
+        monkeypatch.setenv("SWBANK_PAIR", "0")
+    if case in ("u16", "gotoh-u16"):
+        monkeypatch.setenv("SWBANK_F16", "0")
+    gotoh = case.startswith("gotoh")
+    params = (5, -4, -10, -1) if gotoh else REF
+    q = rng.integers(0, 4, 140, dtype=np.uint8)
+    with S.ScoreBank(gap_model=S.GAP_GOTOH if gotoh else S.GAP_MERGED) as bank:
+        bank.set_penalties(*params)
+        bank.load_query(q)
+        got = bank.score_batch(res, offs, lens)
+        kern = bank.last_kernel()
+        monkeypatch.setenv("SWBANK_STREAM", "0")
+        ref = bank.score_batch(res, offs, lens)
+        monkeypatch.setenv("SWBANK_STREAM", "2")
+    assert "streamed=" in kern, kern
+    if case in ("u16", "gotoh-u16"):
+        assert kern.startswith("tile u16"), kern
+    if case == "lut-f16":
+        assert kern.startswith("tile f16 R=") and " pair " not in kern, kern
+    assert np.array_equal(got, ref), kern
+    sel = np.unique(np.concatenate([rng.choice(n, 500, replace=False), np.asarray(extra, int),
+                                    np.arange(n - 128, n)]))
+    sub = [res[int(offs[k]):int(offs[k]) + L] for k in sel]
+    want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(*params[:2]), *params[2:],
+                         O.GAP_GOTOH if gotoh else O.GAP_MERGED)
+    assert np.array_equal(got[sel], want), kern
+
+
+@pytest.mark.parametrize("where", ["first", "middle", "last"])
+@pytest.mark.parametrize("kind", ["code", "range"])
+def test_stream_errors(monkeypatch, where, kind):
+    """A code outside the alphabet or a target past the residues, in the first, a middle or the
+    last chunk: SW_ERR_ARG naming the target; the kernel drains (the chunks never sent are
+    released as aborted) and the next call on the bank scores correctly."""
+    monkeypatch.setenv("SWBANK_STREAM", "2")
+    rng = np.random.default_rng(5)
+    n, L = 30_000, 64
+    res, offs, lens = _uniform(rng, n, L)
+    k = {"first": 3, "middle": 17_000, "last": n - 2}[where]
+    bad_res, bad_offs = res.copy(), offs.copy()
+    if kind == "code":
+        bad_res[k * L + 5] = 9
+    else:
+        bad_offs[k] = res.size - L + 1
+    q = rng.integers(0, 4, 80, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        with pytest.raises(S.SwbankError) as ei:
+            bank.score_batch(bad_res, bad_offs, lens)
+        assert ei.value.status == S.ERR_ARG
+        assert f"target {k}" in str(ei.value), str(ei.value)
+        got = bank.score_batch(res, offs, lens)
+        assert "streamed=" in bank.last_kernel()
+    sel = rng.choice(n, 300, replace=False)
+    sub = [res[int(offs[j]):int(offs[j]) + L] for j in sel]
+    assert np.array_equal(got[sel], O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(), -12, -4))
+
+
+def test_stream_repeat_calls(monkeypatch):
+    """Back-to-back calls reuse the codes buffer, the layout words and the records (no stale
+    chunk from the previous call is read): different batches, different lengths."""
+    monkeypatch.setenv("SWBANK_STREAM", "2")
+    rng = np.random.default_rng(9)
+    q = rng.integers(0, 4, 90, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        for n, L in [(20_000, 100), (9_000, 40), (20_000, 100), (50_000, 7)]:
+            res, offs, lens = _uniform(rng, n, L, p_n=0.005 if L == 40 else 0.0)
+            got = bank.score_batch(res, offs, lens)
+            assert "streamed=" in bank.last_kernel()
+            sel = rng.choice(n, 300, replace=False)
+            sub = [res[int(offs[j]):int(offs[j]) + L] for j in sel]
+            assert np.array_equal(got[sel], O.score_batch(q, *S.pack_targets(sub),
+                                                          O.dna_matrix(), -12, -4))
+
+
+def test_stream_with_other_banks(monkeypatch):
+    """With several other banks (and their streams) open in the process, so streams share the
+    process's hardware queues, the streamed call still runs streamed (its kernel on a queue of
+    its own: no copy marker stuck behind it) and matches the chunked feeder."""
+    rng = np.random.default_rng(21)
+    q = rng.integers(0, 4, 100, dtype=np.uint8)
+    others = [S.ScoreBank() for _ in range(4)]
+    try:
+        small = _uniform(rng, 3000, 90)
+        for o in others:
+            o.set_penalties(*REF)
+            o.load_query(q)
+            o.score_batch(*small)
+        res, offs, lens = _uniform(rng, 300_000, 150)
+        with S.ScoreBank() as bank:
+            bank.set_penalties(*REF)
+            bank.load_query(q)
+            for _ in range(3):
+                got = bank.score_batch(res, offs, lens)
+                assert "streamed=" in bank.last_kernel(), bank.last_kernel()
+            monkeypatch.setenv("SWBANK_STREAM", "0")
+            ref = bank.score_batch(res, offs, lens)
+        assert np.array_equal(got, ref)
+    finally:
+        for o in others:
+            o.close()
