@@ -338,9 +338,8 @@ struct sw_bank {
   // streamed host batches (one kernel for the whole call, equal-length DNA): the batch's codes
   // (chunks 256-byte aligned: no cache line holds two chunks, and nothing of a chunk is read
   // before its layout word is set, so no line is cached before its copy landed), the chunks'
-  // device layout words (uncached device memory), the chunk records (device,
-  // staged in srec, which also takes the layout words back), the host layout words (coherent
-  // host memory), a copy event per chunk
+  // device layout words (uncached device memory), the chunk records (device, staged in srec),
+  // the host layout and abort words (coherent host memory), a copy event per chunk
   DevBuf<uint8_t> sbuf;
   UcBuf sflag;
   DevBuf<SwkStreamChunk> sdrec;
@@ -350,6 +349,7 @@ struct sw_bank {
   // shared with another stream
   hipStream_t kstream = nullptr;
   PinBuf srec, shflag{hipHostMallocCoherent};
+  PinBuf shscores{hipHostMallocCoherent};  // the streamed kernel writes the scores here
   std::vector<hipEvent_t> sev;
   std::unique_ptr<HostPool> pool;
 
@@ -635,6 +635,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->sctr.release();
   b->srec.release();
   b->shflag.release();
+  b->shscores.release();
   for (hipEvent_t e : b->sev) (void)hipEventDestroy(e);
   for (int i = 0; i < sw_bank::NSLOT; ++i) {
     if (b->h2d_done[i]) (void)hipEventDestroy(b->h2d_done[i]);
@@ -2012,11 +2013,10 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   HIPOK(b, b->sdrec.reserve(nsc));
   HIPOK(b, b->sctr.reserve(1));
   HIPOK(b, b->srec.reserve(nsc * sizeof(SwkStreamChunk)));
-  HIPOK(b, b->shflag.reserve(nsc * 4));
+  HIPOK(b, b->shflag.reserve(nsc * 8));  // layout words | abort words
   for (int i = 0; i < std::min<int>(sw_bank::NSLOT, (int)nsc); ++i)
     HIPOK(b, b->hslot[i].reserve(slot_bytes));
-  HIPOK(b, b->scores.reserve(n));
-  HIPOK(b, b->hscores.reserve(n * 4));
+  HIPOK(b, b->shscores.reserve(n * 4));
   while (b->sev.size() < nsc) {
     hipEvent_t e;
     HIPOK(b, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -2027,6 +2027,7 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   for (size_t i = 0; i < nsc; ++i) {
     rec[i] = SwkStreamChunk{(unsigned)tile0[i], (unsigned)roff[i], (unsigned)(roff[i] >> 32), 0u};
     __atomic_store_n(&hflag[i], 0u, __ATOMIC_RELAXED);
+    __atomic_store_n(&hflag[nsc + i], 0u, __ATOMIC_RELAXED);
   }
   std::atomic_thread_fence(std::memory_order_seq_cst);
 
@@ -2052,7 +2053,8 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                                (uint32_t)nsc, b->sctr.p,
                                pair ? b->qpair.p : use_f16 ? b->qtab16.p : b->qtab.p,
                                use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
-                               pair ? b->pair_bytes : 0, b->pad, b->segs[0].W, b->scores.p,
+                               pair ? b->pair_bytes : 0, b->pad, b->segs[0].W,
+                               reinterpret_cast<int32_t*>(b->shscores.p),
                                b->pS1, b->pS2, ks));
     HIPOK(b, hipEventRecord(b->ev_used, ks));
     if (b->timing) {
@@ -2187,30 +2189,22 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     (void)hipStreamSynchronize(b->copy_stream);
     return err;
   }
-  // the scores and the layout words back only now: a copy enqueued behind the kernel may hold
-  // the copy engine the chunks' copies need until the kernel ends (seen as chunks that never
-  // reach the kernel)
-  if (err == SW_OK) {
-    hipError_t e = hipMemcpyAsync(b->hscores.p, b->scores.p, n * 4, hipMemcpyDeviceToHost,
-                                  ks);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(rec, b->sflag.p, nsc * 4, hipMemcpyDeviceToHost, ks);
-    if (e != hipSuccess) err = fail(b, SW_ERR_HIP, "streamed scores: %s", hipGetErrorString(e));
-  }
+  // no copy follows the kernel: it writes the scores (and any abort word) straight to coherent
+  // host memory.  (A copy enqueued behind the running kernel may hold the copy engine the
+  // chunks' copies need until the kernel ends: chunks that never reach the kernel.)
   const hipError_t se = hipStreamSynchronize(ks);
   if (err != SW_OK) return err;
   if (se != hipSuccess) return fail(b, SW_ERR_HIP, "streamed batch: %s", hipGetErrorString(se));
   trace_mark("landed");
   // a chunk whose wait ran out (its copy held up past the kernel's bound, e.g. by other work on
   // the device's copy engines): the call runs again through the chunked feeder
-  const uint32_t* dflag = reinterpret_cast<const uint32_t*>(rec);
   for (size_t i = 0; i < nsc; ++i)
-    if (dflag[i] == SWK_STREAM_ABORT) {
+    if (__atomic_load_n(&hflag[nsc + i], __ATOMIC_ACQUIRE) == SWK_STREAM_ABORT) {
       used = false;
       return SW_OK;
     }
   // scores into the caller's buffer with the best hit (lowest index of the maximum)
-  const int32_t* hs = reinterpret_cast<const int32_t*>(b->hscores.p);
+  const int32_t* hs = reinterpret_cast<const int32_t*>(b->shscores.p);
   std::vector<size_t> pbest(PT, SIZE_MAX);
   const size_t ostep = (n + PT - 1) / PT;
   pool.run([&](unsigned p) {

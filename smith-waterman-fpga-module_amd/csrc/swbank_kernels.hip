@@ -637,9 +637,10 @@ __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens
 // Wave-uniform code layout of streamed chunk c, waiting until its copy landed.  Every wait
 // polls the device word; one poll in 16 (staggered by workgroup) also reads the host word over
 // PCIe, and the wave that sees it set copies it to the device word for the others.  Bounded
-// (2^20 polls, about a second): a wave that runs out marks the chunk SWK_STREAM_ABORT.
+// (2^20 polls, about a second): a wave that runs out marks the chunk SWK_STREAM_ABORT in the
+// device word and in the host's abort word hflag[nsc + c].
 __device__ __forceinline__ uint32_t stream_mode(const uint32_t* hflag, uint32_t* dflag, int c,
-                                                int lane) {
+                                                int nsc, int lane) {
   for (int it = 0; it < (1 << 20); ++it) {
     uint32_t v = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load(dflag + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
@@ -654,8 +655,11 @@ __device__ __forceinline__ uint32_t stream_mode(const uint32_t* hflag, uint32_t*
     }
     __builtin_amdgcn_s_sleep(16);
   }
-  if (lane == 0)
+  if (lane == 0) {
     __hip_atomic_store(dflag + c, SWK_STREAM_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(const_cast<uint32_t*>(hflag) + nsc + c, SWK_STREAM_ABORT,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   return SWK_STREAM_ABORT;
 }
 
@@ -728,7 +732,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
                      (size_t)st0 * SWB_TILE));
       sro_lo = __builtin_amdgcn_readfirstlane(ssc[c].res_off_lo);
       sro_hi = __builtin_amdgcn_readfirstlane(ssc[c].res_off_hi);
-      smode = stream_mode(a.lens, const_cast<uint32_t*>(a.nidx), c, lane) == SWK_PACK_NIBBLE
+      smode = stream_mode(a.lens, const_cast<uint32_t*>(a.nidx), c, snc, lane) == SWK_PACK_NIBBLE
                   ? SWK_PACK_NIBBLE
                   : SWK_PACK_STREAM;
     }
@@ -1138,6 +1142,12 @@ static int cached_occupancy(const void* fn, int threads, size_t lds, int dev, in
   return occ;
 }
 
+// (tuning) SWBANK_GRID_EVEN=0: every resident slot, the last round partial
+static bool env_flag_off(const char* name) {
+  const char* v = std::getenv(name);
+  return v && v[0] == '0' && v[1] == 0;
+}
+
 static unsigned persistent_grid(const void* fn, size_t ntiles, int threads, size_t lds) {
   int dev = 0, cus = 0;
   const char* env = std::getenv("SWBANK_GRID");
@@ -1149,6 +1159,7 @@ static unsigned persistent_grid(const void* fn, size_t ntiles, int threads, size
   if (cap > 0) occ = std::min(occ, cap);
   if (t_occ_cap > 0) occ = std::min(occ, t_occ_cap);
   const size_t slots = (size_t)cus * occ;
+  if (env_flag_off("SWBANK_GRID_EVEN")) return (unsigned)std::min(ntiles, slots);
   const size_t rounds = (ntiles + slots - 1) / slots;
   return (unsigned)((ntiles + rounds - 1) / rounds);
 }
