@@ -1,6 +1,6 @@
 #!/bin/bash
-# configs[4]: the wave kernel's split form for every pair (P = 2 / 4) against the default
-# policy (split tail only)
+# configs[4]: the wave kernel's split-tail policy (P = 2 / 4 for the tail, no split, every
+# pair split) against the default
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
 run() {
@@ -9,10 +9,11 @@ run() {
   python - "$*" <<'PY'
 import json, sys
 d = json.load(open("gpurun_out/psplit.json"))
-print(sys.argv[1] or "default", d["value"], d["ms_per_step"], d.get("config", {}).get("kernel", ""), d.get("parity", ""))
+print(sys.argv[1] or "default", d["value"], d["ms_per_step"], d.get("parity", ""))
 PY
 }
+for i in 1 2; do
 run X=0
-run SWBANK_WAVE_SPLIT=1000000 SWBANK_WAVE_SPLIT_P=2
-run SWBANK_WAVE_SPLIT=1000000 SWBANK_WAVE_SPLIT_P=4
-run X=0
+run SWBANK_WAVE_SPLIT_P=2
+run SWBANK_WAVE_SPLIT=0
+done

@@ -2072,11 +2072,15 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   std::vector<std::chrono::steady_clock::time_point> pub_t(nsc);  // (SWBANK_TRACE_FILE)
   std::atomic<size_t> issued{0};
   std::atomic<bool> stop{false};
+  // (tests) SWBANK_STREAM_HOLD_MS=t: chunk 1 is published t ms late, past the kernel's wait
+  // bound, to exercise the abort and the chunked re-run
+  const int hold_ms = env_int("SWBANK_STREAM_HOLD_MS", 0);
   std::thread publisher([&] {
     for (size_t i = 0; i < nsc; ++i) {
       while (issued.load(std::memory_order_acquire) <= i && !stop.load()) std::this_thread::yield();
       if (issued.load(std::memory_order_acquire) <= i) return;
       while (hipEventQuery(b->sev[i]) == hipErrorNotReady) std::this_thread::yield();
+      if (i == 1 && hold_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(hold_ms));
       __atomic_store_n(&hflag[i], mode[i], __ATOMIC_RELEASE);
       pub_t[i] = std::chrono::steady_clock::now();
     }

@@ -192,3 +192,32 @@ def test_stream_with_other_banks(monkeypatch):
     finally:
         for o in others:
             o.close()
+
+
+def test_stream_stalled_chunk_reruns(monkeypatch):
+    """A chunk published past the kernel's wait bound (SWBANK_STREAM_HOLD_MS): the waiting waves
+    mark it aborted, the kernel drains, and the call re-runs through the chunked feeder with
+    exact scores; the bank stays usable for a streamed call afterwards."""
+    import time
+    monkeypatch.setenv("SWBANK_STREAM", "2")
+    rng = np.random.default_rng(33)
+    n, L = 40_000, 100
+    res, offs, lens = _uniform(rng, n, L)
+    q = rng.integers(0, 4, 90, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        monkeypatch.setenv("SWBANK_STREAM_HOLD_MS", "8000")
+        t0 = time.perf_counter()
+        got = bank.score_batch(res, offs, lens)
+        dt = time.perf_counter() - t0
+        kern = bank.last_kernel()
+        monkeypatch.delenv("SWBANK_STREAM_HOLD_MS")
+        print(f"stalled call {dt:.2f} s, {kern}")
+        assert "streamed=" not in kern, kern  # the chunked re-run
+        again = bank.score_batch(res, offs, lens)
+        assert "streamed=" in bank.last_kernel()
+    assert np.array_equal(got, again)
+    sel = rng.choice(n, 300, replace=False)
+    sub = [res[int(offs[j]):int(offs[j]) + L] for j in sel]
+    assert np.array_equal(got[sel], O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(), -12, -4))
