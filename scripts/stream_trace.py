@@ -17,10 +17,18 @@ def main():
     from oracle import oracle as O
     n, L = 1021952, 128
     q = O.random_codes(1, 128, 4)
-    res = O.random_codes(2, n * L, 4)
-    offs = np.arange(n, dtype=np.uint64) * L
-    lens = np.full(n, L, np.uint32)
-    for mode in ("1", "0", "1"):
+    if "--ragged" in sys.argv:  # lengths 64-128, 0.1 % N
+        rng = np.random.default_rng(7)
+        lens = rng.integers(L // 2, L + 1, n).astype(np.uint32)
+        offs = np.zeros(n, np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        res = O.random_codes(2, int(lens.sum()), 4)
+        res[rng.random(res.size) < 0.001] = 4
+    else:
+        res = O.random_codes(2, n * L, 4)
+        offs = np.arange(n, dtype=np.uint64) * L
+        lens = np.full(n, L, np.uint32)
+    for mode in (("0",) if "--ragged" in sys.argv else ("1", "0", "1")):
         os.environ["SWBANK_STREAM"] = mode
         path = tempfile.mktemp()
         with S.ScoreBank() as bank:
