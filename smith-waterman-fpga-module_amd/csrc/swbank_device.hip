@@ -2017,9 +2017,9 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   for (int i = 0; i < std::min<int>(sw_bank::NSLOT, (int)nsc); ++i)
     HIPOK(b, b->hslot[i].reserve(slot_bytes));
   HIPOK(b, b->shscores.reserve(n * 4));
-  while (b->sev.size() < nsc) {
+  while (b->sev.size() < nsc) {  // blocking sync: the publisher sleeps in them
     hipEvent_t e;
-    HIPOK(b, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPOK(b, hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
     b->sev.push_back(e);
   }
   SwkStreamChunk* rec = reinterpret_cast<SwkStreamChunk*>(b->srec.p);
@@ -2067,22 +2067,32 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     return SW_OK;
   };
 
-  // the publisher: chunk i's layout word once its copy event completed (issued chunks only)
+  // the publisher: chunk i's layout word once its copy landed.  It sleeps in the copy event
+  // (blocking-sync events) and on a condition variable for the next issued chunk: spinning
+  // threads beside the 16 gather threads burnt the process's CPU quota (multi-ms stalls), and
+  // polling from this thread between gather pieces made the gather 3-4x slower
   std::vector<uint32_t> mode(nsc, 0);
-  std::vector<std::chrono::steady_clock::time_point> pub_t(nsc);  // (SWBANK_TRACE_FILE)
-  std::atomic<size_t> issued{0};
-  std::atomic<bool> stop{false};
+  size_t issued = 0;  // (under pm)
+  bool stop = false;
+  std::mutex pm;
+  std::condition_variable pcv;
   // (tests) SWBANK_STREAM_HOLD_MS=t: chunk 1 is published t ms late, past the kernel's wait
   // bound, to exercise the abort and the chunked re-run
   const int hold_ms = env_int("SWBANK_STREAM_HOLD_MS", 0);
+  std::vector<std::chrono::steady_clock::time_point> pub_t(nsc);  // (SWBANK_TRACE_FILE)
+  size_t published = 0;
   std::thread publisher([&] {
     for (size_t i = 0; i < nsc; ++i) {
-      while (issued.load(std::memory_order_acquire) <= i && !stop.load()) std::this_thread::yield();
-      if (issued.load(std::memory_order_acquire) <= i) return;
-      while (hipEventQuery(b->sev[i]) == hipErrorNotReady) std::this_thread::yield();
+      {
+        std::unique_lock<std::mutex> lk(pm);
+        pcv.wait(lk, [&] { return issued > i || stop; });
+        if (issued <= i) return;
+      }
+      (void)hipEventSynchronize(b->sev[i]);
       if (i == 1 && hold_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(hold_ms));
       __atomic_store_n(&hflag[i], mode[i], __ATOMIC_RELEASE);
       pub_t[i] = std::chrono::steady_clock::now();
+      published = i + 1;
     }
   });
 
@@ -2118,9 +2128,26 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       const size_t stepb = pass == 0 ? 8 : 16;  // bytes one 32-code vector step stores
       const swpack::PackFn fn = pass == 0 ? pack2fn : pack4fn;
       wide = 0;
+      // a part whose targets lie back to back in the residues (offsets k * L apart) and end on
+      // a byte boundary of the packed stream packs as ONE run: the per-target call overhead
+      // was most of the gather (SWBANK_STREAM_RUNS=0: per target)
+      const bool runs = (pass == 0 ? L % 4 == 0 : L % 2 == 0) &&
+                        env_int("SWBANK_STREAM_RUNS", 1) != 0;
       pool.run([&](unsigned p) {
         const size_t lo = std::min(cnt, p * step), hi = std::min(cnt, (p + 1) * step);
         uint32_t acc = 0;
+        if (runs && hi > lo && (hi - lo) * (size_t)L < 0x80000000ull) {
+          const uint64_t o0 = offsets[c0 + lo];
+          const size_t total = (hi - lo) * (size_t)L;
+          bool back = o0 <= nres && total <= nres - o0;
+          for (size_t j = lo + 1; back && j < hi; ++j)
+            back = offsets[c0 + j] == o0 + (j - lo) * (uint64_t)L;
+          if (back) {
+            acc = fn(residues + o0, (uint32_t)total, codes + lo * sb, total % 32 == 0);
+            if (pass == 0 ? acc > 3u : acc >= (uint32_t)SW_DNA_ALPHA) wide = 1;
+            return;
+          }
+        }
         for (size_t j = lo; j < hi; ++j) {
           const size_t k = c0 + j;
           if (offsets[k] > nres || L > nres - offsets[k]) {
@@ -2176,18 +2203,27 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       break;
     }
     mode[i] = md;
-    issued.store(i + 1, std::memory_order_release);
+    {
+      std::lock_guard<std::mutex> lk(pm);
+      issued = i + 1;
+    }
+    pcv.notify_one();
     trace_mark("launched");
     if (i == 0 && (err = start_kernel()) != SW_OK) break;
     started = i == 0 || started;
   }
-  // on failure the chunks never sent are released to the kernel as aborted (it reads whatever
-  // their range holds) so it drains; the call reports the error
-  stop.store(true);
+  // the issued chunks' words once their copies landed; on failure the chunks never sent are
+  // released to the kernel as aborted (it reads whatever their range holds) so it drains, and
+  // the call reports the error
+  {
+    std::lock_guard<std::mutex> lk(pm);
+    stop = true;
+  }
+  pcv.notify_one();
   publisher.join();
   if (g_trace)
-    for (size_t i = 0; i < issued.load(); ++i) g_trace->mark_at("published", pub_t[i]);
-  for (size_t i = issued.load(); i < nsc; ++i)
+    for (size_t i = 0; i < published; ++i) g_trace->mark_at("published", pub_t[i]);
+  for (size_t i = issued; i < nsc; ++i)
     __atomic_store_n(&hflag[i], SWK_STREAM_ABORT, __ATOMIC_RELEASE);
   if (!started) {  // nothing enqueued on the bank stream; chunk 0's copy may be in flight
     (void)hipStreamSynchronize(b->copy_stream);

@@ -221,3 +221,44 @@ def test_stream_stalled_chunk_reruns(monkeypatch):
     sel = rng.choice(n, 300, replace=False)
     sub = [res[int(offs[j]):int(offs[j]) + L] for j in sel]
     assert np.array_equal(got[sel], O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(), -12, -4))
+
+
+@pytest.mark.parametrize("layout", ["back-to-back", "reversed", "gaps", "partly"])
+def test_stream_runs(monkeypatch, layout):
+    """Parts whose targets lie back to back pack as one run; reversed order, gaps between
+    targets, or a batch only partly back to back go target by target: the same scores either
+    way (SWBANK_STREAM_RUNS=0 packs every target on its own), and the oracle's on a sample."""
+    monkeypatch.setenv("SWBANK_STREAM", "2")
+    rng = np.random.default_rng(len(layout))
+    n, L = 30_000, 128
+    seqs = rng.integers(0, 4, (n, L), dtype=np.uint8)
+    if layout == "back-to-back":
+        res, offs = seqs.reshape(-1), np.arange(n, dtype=np.uint64) * L
+    elif layout == "reversed":
+        res, offs = seqs[::-1].reshape(-1).copy(), (n - 1 - np.arange(n, dtype=np.uint64)) * L
+    else:
+        gap = 5 if layout == "gaps" else 0
+        res = np.full(n * (L + gap) + L + 64, 3, np.uint8)
+        offs = np.arange(n, dtype=np.uint64) * (L + gap)
+        if layout == "partly":  # back to back, except one target every 7000 moved to the end
+            for k in range(0, n, 7000):
+                offs[k] = n * L  # all share one copy at the end
+            res[n * L:n * L + L] = seqs[0]
+            for k in range(0, n, 7000):
+                seqs[k] = seqs[0]
+        for k in range(n):
+            if layout == "gaps" or offs[k] < n * L:
+                res[int(offs[k]):int(offs[k]) + L] = seqs[k]
+    lens = np.full(n, L, np.uint32)
+    q = rng.integers(0, 4, 100, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        got = bank.score_batch(res, offs, lens)
+        assert "streamed=" in bank.last_kernel()
+        monkeypatch.setenv("SWBANK_STREAM_RUNS", "0")
+        per = bank.score_batch(res, offs, lens)
+    assert np.array_equal(got, per)
+    sel = np.unique(np.concatenate([rng.choice(n, 300, replace=False), np.arange(0, n, 7000)]))
+    want = O.score_batch(q, *S.pack_targets([seqs[k] for k in sel]), O.dna_matrix(), -12, -4)
+    assert np.array_equal(got[sel], want)
