@@ -2003,9 +2003,19 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     slot_bytes = std::max(slot_bytes, roff[i + 1] - roff[i]);
   }
   HIPOK(b, hipSetDevice(b->device));
-  if (!b->kstream) {
-    std::vector<uint32_t> mask((std::max(b->cus, 1) + 31) / 32, 0xFFFFFFFFu);
-    HIPOK(b, hipExtStreamCreateWithCUMask(&b->kstream, (uint32_t)mask.size(), mask.data()));
+  if (!b->kstream) {  // (no queue of its own: the chunked feeder)
+    if (b->cus <= 0) {
+      used = false;
+      return SW_OK;
+    }
+    std::vector<uint32_t> mask(((size_t)b->cus + 31) / 32, 0xFFFFFFFFu);
+    if (hipExtStreamCreateWithCUMask(&b->kstream, (uint32_t)mask.size(), mask.data()) !=
+        hipSuccess) {
+      b->kstream = nullptr;
+      (void)hipGetLastError();
+      used = false;
+      return SW_OK;
+    }
   }
   hipStream_t ks = b->kstream;
   HIPOK(b, b->sbuf.reserve(roff[nsc]));
