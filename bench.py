@@ -469,18 +469,20 @@ def host_api_rate(wl, d_sc, iters=5):
                    f"{iters}"}
 
 
-def parity_sample(wl, per_rank, m=512):
-    """Every query's scores for the first and the last m/2 targets of every rank's batch (rank
-    0's own, and at N>1 the slices it gathered from the others, regenerated from their seeds;
-    the last ones are where the wave kernel's split tail runs), re-computed by the oracle (test
-    infrastructure) and compared: the bench's own bit-exactness evidence."""
+def parity_sample(wl, per_rank, m=4096):
+    """Every query's scores for the first and the last m/4 targets of every rank's batch and
+    m/2 seeded random ones between (rank 0's own, and at N>1 the slices it gathered from the
+    others, regenerated from their seeds; the last ones are where the wave kernel's split tail
+    runs), re-computed by the oracle (test infrastructure, the multi-threaded C restatement)
+    and compared: the bench's own bit-exactness evidence."""
     from oracle import oracle as O
     if wl.model == "gotoh":
         sub, go, ge, model = wl.sub, -11, -1, O.GAP_GOTOH
     else:
         sub, go, ge, model = O.dna_matrix(PEN[0], PEN[1]), PEN[2], PEN[3], O.GAP_MERGED
-    rows = np.unique(np.concatenate([np.arange(min(m // 2, wl.n)),
-                                     np.arange(max(0, wl.n - m // 2), wl.n)]))
+    pick = np.random.default_rng(12345).integers(0, wl.n, m // 2)
+    rows = np.unique(np.concatenate([np.arange(min(m // 4, wl.n)),
+                                     np.arange(max(0, wl.n - m // 4), wl.n), pick]))
     mism, checked = 0, 0
     for r, sc in enumerate(per_rank):
         gpu = sc.cpu().numpy()
