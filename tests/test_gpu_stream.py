@@ -262,3 +262,40 @@ def test_stream_runs(monkeypatch, layout):
     sel = np.unique(np.concatenate([rng.choice(n, 300, replace=False), np.arange(0, n, 7000)]))
     want = O.score_batch(q, *S.pack_targets([seqs[k] for k in sel]), O.dna_matrix(), -12, -4)
     assert np.array_equal(got[sel], want)
+
+
+def test_stream_concurrent_banks():
+    """Two banks streaming on the same device from two host threads at once (ctypes releases
+    the GIL): both kernels wait only on their own call's copies, so both finish, streamed or
+    through the chunked re-run, with exact scores."""
+    import threading
+    rng = np.random.default_rng(44)
+    qs = [rng.integers(0, 4, 100, dtype=np.uint8) for _ in range(2)]
+    batches = [_uniform(rng, 300_000, 128) for _ in range(2)]
+    out, kern, errs = [None, None], [None, None], []
+
+    def work(i):
+        try:
+            with S.ScoreBank() as bank:
+                bank.set_penalties(*REF)
+                bank.load_query(qs[i])
+                for _ in range(3):
+                    out[i] = bank.score_batch(*batches[i])
+                kern[i] = bank.last_kernel()
+        except Exception as e:  # reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in th), "a streamed call did not return"
+    assert not errs, errs
+    print("kernels:", kern)
+    for i in range(2):
+        res, offs, lens = batches[i]
+        sel = rng.choice(len(lens), 300, replace=False)
+        sub = [res[int(offs[j]):int(offs[j]) + 128] for j in sel]
+        want = O.score_batch(qs[i], *S.pack_targets(sub), O.dna_matrix(), -12, -4)
+        assert np.array_equal(out[i][sel], want)
