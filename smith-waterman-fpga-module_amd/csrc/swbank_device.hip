@@ -1966,10 +1966,16 @@ static bool scratch_free(const sw_bank* b, uint32_t max_len) {
 // One pipeline fill and drain per call instead of one per chunk, and no chunk kernel on half
 // the chip.  `used` = false when the batch does not qualify (the chunked feeder runs instead;
 // always for a multi-device bank's per-device parts, out == nullptr); SWBANK_STREAM=0 disables.
+// recs != nullptr: the batch is n CAPI records (sw_score_records) of length L (record 0's); each
+// chunk takes the first ceil(L/4) bytes of every record's 2-bit data field, so equal-length
+// records cross PCIe at half the record bytes.  A record of another length ends streaming:
+// found in chunk 0 (before the launch) it costs nothing; later, the kernel drains and the call
+// runs through the chunked feeder (`used` = false), which reports bad lengths.
 static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                              const uint64_t* offsets, size_t n, uint32_t L, int32_t* out,
-                             bool& used) {
+                             bool& used, const uint8_t* recs = nullptr) {
   used = false;
+  if (recs && (L == 0 || L > SWB_RECORD_MAX)) return SW_OK;
   const int mode_env = env_int("SWBANK_STREAM", 1);  // 2: also below the size threshold (tests)
   if (mode_env == 0 || !out || b->alpha != SW_DNA_ALPHA || b->prof || b->col0 || b->RB != 4 ||
       env_int("SWBANK_PACK2", 1) == 0 || env_int("SWBANK_UNIFORM", 1) == 0 ||
@@ -2115,7 +2121,8 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   std::atomic<size_t> oob{SIZE_MAX};
   std::atomic<uint32_t> wide{0};
   sw_status err = SW_OK;
-  bool started = false;  // the kernel is enqueued
+  bool started = false;     // the kernel is enqueued
+  bool nonuniform = false;  // (records) a record of another length: the chunked feeder
   for (size_t i = 0; i < nsc && err == SW_OK; ++i) {
     const int s = (int)(i % sw_bank::NSLOT);
     if (i >= (size_t)sw_bank::NSLOT) {
@@ -2133,7 +2140,30 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t md = 0;
     size_t sb = 0;
-    for (int pass = nib_mode ? 1 : 0; pass < 2 && md == 0; ++pass) {
+    if (recs) {  // 2-bit data bytes of every record; lengths must all be L
+      sb = (L + 3) / 4;
+      std::atomic<bool> other{false};
+      const size_t step = (cnt + PT - 1) / PT;
+      pool.run([&](unsigned p) {
+        const size_t lo = std::min(cnt, p * step), hi = std::min(cnt, (p + 1) * step);
+        for (size_t j = lo; j < hi; ++j) {
+          const uint8_t* r = recs + (c0 + j) * SWB_RECORD;
+          uint16_t l;
+          std::memcpy(&l, r + 4, 2);
+          if (l != L) {
+            other = true;
+            return;
+          }
+          std::memcpy(codes + j * sb, r + 6, sb);
+        }
+      });
+      if (other.load()) {
+        nonuniform = true;
+        break;
+      }
+      md = SWK_PACK_STREAM;
+    }
+    for (int pass = nib_mode ? 1 : 0; !recs && pass < 2 && md == 0; ++pass) {
       sb = pass == 0 ? (L + 3) / 4 : nib;
       const size_t stepb = pass == 0 ? 8 : 16;  // bytes one 32-code vector step stores
       const swpack::PackFn fn = pass == 0 ? pack2fn : pack4fn;
@@ -2237,6 +2267,7 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     __atomic_store_n(&hflag[i], SWK_STREAM_ABORT, __ATOMIC_RELEASE);
   if (!started) {  // nothing enqueued on the bank stream; chunk 0's copy may be in flight
     (void)hipStreamSynchronize(b->copy_stream);
+    if (nonuniform) used = false;
     return err;
   }
   // no copy follows the kernel: it writes the scores (and any abort word) straight to coherent
@@ -2244,6 +2275,10 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   // chunks' copies need until the kernel ends: chunks that never reach the kernel.)
   const hipError_t se = hipStreamSynchronize(ks);
   if (err != SW_OK) return err;
+  if (nonuniform) {  // the kernel drained on aborted chunks: the chunked feeder runs the call
+    used = false;
+    return SW_OK;
+  }
   if (se != hipSuccess) return fail(b, SW_ERR_HIP, "streamed batch: %s", hipGetErrorString(se));
   trace_mark("landed");
   // a chunk whose wait ran out (its copy held up past the kernel's bound, e.g. by other work on
@@ -2630,6 +2665,13 @@ static sw_status records_feed(sw_bank* b, const uint8_t* recs, size_t n, int32_t
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
   if ((st = feeder_init(b)) != SW_OK) return st;
+  if (n) {  // equal-length records: one streamed kernel (stream_feed), else the chunks below
+    uint16_t l0;
+    std::memcpy(&l0, recs + 4, 2);
+    bool used = false;
+    st = stream_feed(b, nullptr, 0, nullptr, n, l0, out, used, recs);
+    if (used) return st;
+  }
   const auto rlen = [&](size_t k) { return record_len(recs + k * SWB_RECORD); };
   // chunks in input order: records | lens | perm | count (longest-first order per chunk)
   std::vector<Chunk> chunks;

@@ -299,3 +299,59 @@ def test_stream_concurrent_banks():
         sub = [res[int(offs[j]):int(offs[j]) + 128] for j in sel]
         want = O.score_batch(qs[i], *S.pack_targets(sub), O.dna_matrix(), -12, -4)
         assert np.array_equal(out[i][sel], want)
+
+
+@pytest.mark.parametrize("L", [100, 232, 37, 1])
+def test_stream_records(monkeypatch, L):
+    """Equal-length CAPI records (sw_score_records) stream their 2-bit data bytes: the same
+    scores as the byte path and the oracle, and the batch best hit carries the record's ID."""
+    monkeypatch.setenv("SWBANK_STREAM", "2")
+    rng = np.random.default_rng(L)
+    n = 40_000
+    seqs = [rng.integers(0, 4, L, dtype=np.uint8) for _ in range(n)]
+    ids = rng.integers(0, 2**31, n)
+    recs = S.make_records(seqs, ids)
+    q = rng.integers(0, 4, 120, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        got = bank.score_records(recs)
+        assert "streamed=" in bank.last_kernel(), bank.last_kernel()
+        bid, bsc, bix = bank.best()
+        ref = bank.score_targets(seqs)
+    assert np.array_equal(got, ref)
+    top = int(np.argmax(got))
+    assert (bid, bsc, bix) == (int(ids[top]), int(got[top]), top)
+    sel = rng.choice(n, 300, replace=False)
+    want = O.score_batch(q, *S.pack_targets([seqs[k] for k in sel]), O.dna_matrix(), -12, -4)
+    assert np.array_equal(got[sel], want)
+
+
+@pytest.mark.parametrize("where", ["chunk0", "later", "too-long"])
+def test_stream_records_other_lengths(monkeypatch, where):
+    """A record of another length ends streaming: in chunk 0 before the launch, later after
+    the kernel drains; the chunked feeder then scores the call (exact), or reports a length
+    past 232 (SW_ERR_ARG)."""
+    monkeypatch.setenv("SWBANK_STREAM", "2")
+    rng = np.random.default_rng(len(where))
+    n, L = 40_000, 90
+    seqs = [rng.integers(0, 4, L, dtype=np.uint8) for _ in range(n)]
+    k = {"chunk0": 5, "later": 35_000, "too-long": 30_000}[where]
+    seqs[k] = rng.integers(0, 4, 50, dtype=np.uint8)
+    recs = S.make_records(seqs)
+    if where == "too-long":
+        recs[k, 4:6] = np.frombuffer(np.uint16(300).tobytes(), np.uint8)
+    q = rng.integers(0, 4, 80, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        if where == "too-long":
+            with pytest.raises(S.SwbankError) as ei:
+                bank.score_records(recs)
+            assert ei.value.status == S.ERR_ARG
+            return
+        got = bank.score_records(recs)
+        assert "streamed=" not in bank.last_kernel(), bank.last_kernel()
+    sel = np.unique(np.concatenate([rng.choice(n, 300, replace=False), [k]]))
+    want = O.score_batch(q, *S.pack_targets([seqs[j] for j in sel]), O.dna_matrix(), -12, -4)
+    assert np.array_equal(got[sel], want)
