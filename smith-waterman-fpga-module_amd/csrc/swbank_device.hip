@@ -1787,6 +1787,13 @@ std::vector<size_t> chunk_bounds(size_t total) {
   size_t sz = first_kb > 0 ? (size_t)first_kb << 10
               : env_int("SWBANK_CHUNK_MB", 0) > 0 ? cap : std::max<size_t>(1 << 20, cap / 4);
   for (size_t at = sz; at < total; at += sz, sz = std::min(cap, sz * 2)) bounds.push_back(at);
+  // SWBANK_CHUNK_TAIL=1: the last chunk as a half and two quarters, so the call's final
+  // launches (which nothing overlaps) are short
+  const size_t last = bounds.empty() ? 0 : bounds.back(), rem = total - last;
+  if (env_int("SWBANK_CHUNK_TAIL", 0) != 0 && rem >= ((size_t)4 << 20)) {
+    bounds.push_back(last + rem / 2);
+    bounds.push_back(last + rem / 2 + rem / 4);
+  }
   return bounds;
 }
 }  // namespace
