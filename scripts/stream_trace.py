@@ -28,7 +28,7 @@ def main():
         res = O.random_codes(2, n * L, 4)
         offs = np.arange(n, dtype=np.uint64) * L
         lens = np.full(n, L, np.uint32)
-    for mode in (("0",) if "--ragged" in sys.argv else ("1", "0", "1")):
+    for mode in ("1", "0", "1"):
         os.environ["SWBANK_STREAM"] = mode
         path = tempfile.mktemp()
         with S.ScoreBank() as bank:

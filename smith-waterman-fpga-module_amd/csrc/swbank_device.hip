@@ -1978,9 +1978,12 @@ static bool scratch_free(const sw_bank* b, uint32_t max_len) {
 // records cross PCIe at half the record bytes.  A record of another length ends streaming:
 // found in chunk 0 (before the launch) it costs nothing; later, the kernel drains and the call
 // runs through the chunked feeder (`used` = false), which reports bad lengths.
+// rlens != nullptr: a ragged batch (L = its longest target); each chunk's region carries the
+// chunk's code offsets, lengths and longest-first visiting order ahead of its codes.
 static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                              const uint64_t* offsets, size_t n, uint32_t L, int32_t* out,
-                             bool& used, const uint8_t* recs = nullptr) {
+                             bool& used, const uint8_t* recs = nullptr,
+                             const uint32_t* rlens = nullptr) {
   used = false;
   if (recs && (L == 0 || L > SWB_RECORD_MAX)) return SW_OK;
   const int mode_env = env_int("SWBANK_STREAM", 1);  // 2: also below the size threshold (tests)
@@ -2012,7 +2015,8 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   size_t slot_bytes = 0;
   for (size_t i = 0; i < nsc; ++i) {
     const size_t cnt = std::min(n, tile0[i + 1] * SWB_TILE) - tile0[i] * SWB_TILE;
-    roff[i + 1] = roff[i] + (cnt * nib + 64 + 255) / 256 * 256;
+    const size_t head = rlens ? align16(cnt * 16) : 0;  // ragged: offsets | lengths | order
+    roff[i + 1] = roff[i] + (head + cnt * nib + 64 + 255) / 256 * 256;
     slot_bytes = std::max(slot_bytes, roff[i + 1] - roff[i]);
   }
   HIPOK(b, hipSetDevice(b->device));
@@ -2072,7 +2076,8 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       HIPOK(b, hipEventRecord(ev.b, ks));
     }
     HIPOK(b, swk_launch_stream(b->R, b->gotoh() ? 1 : 0, use_f16 ? 1 : 0, pair ? 1 : 0, b->sbuf.p,
-                               n, L, b->sdrec.p, hflag, reinterpret_cast<uint32_t*>(b->sflag.p),
+                               n, rlens ? 0u : L, b->sdrec.p, hflag,
+                               reinterpret_cast<uint32_t*>(b->sflag.p),
                                (uint32_t)nsc, b->sctr.p,
                                pair ? b->qpair.p : use_f16 ? b->qtab16.p : b->qtab.p,
                                use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
@@ -2146,8 +2151,82 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     trace_mark("gather<");
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t md = 0;
-    size_t sb = 0;
-    if (recs) {  // 2-bit data bytes of every record; lengths must all be L
+    size_t sb = 0, bytes = 0;
+    if (rlens) {  // ragged: offsets | lengths | order, then the codes at the next 16 bytes
+      const size_t ca = align16(cnt * 16), step = (cnt + PT - 1) / PT;
+      uint64_t* so = reinterpret_cast<uint64_t*>(codes);
+      uint32_t* sl = reinterpret_cast<uint32_t*>(codes + cnt * 8);
+      uint32_t* sp = sl + cnt;
+      uint8_t* cb = codes + ca;
+      std::vector<size_t> p2(PT + 1, 0), p4(PT + 1, 0);
+      pool.run([&](unsigned p) {  // lengths, bounds, packed bytes per part
+        const size_t lo = std::min(cnt, p * step), hi = std::min(cnt, (p + 1) * step);
+        size_t a2 = 0, a4 = 0;
+        for (size_t j = lo; j < hi; ++j) {
+          const size_t k = c0 + j;
+          const uint32_t l = rlens[k];
+          if (offsets[k] > nres || l > nres - offsets[k]) {
+            size_t cur = oob.load();
+            while (k < cur && !oob.compare_exchange_weak(cur, k)) {
+            }
+            return;
+          }
+          sl[j] = l;
+          a2 += (l + 3) / 4;
+          a4 += (l + 1) / 2;
+        }
+        p2[p + 1] = a2;
+        p4[p + 1] = a4;
+      });
+      for (unsigned p = 0; p < PT; ++p) {
+        p2[p + 1] += p2[p];
+        p4[p + 1] += p4[p];
+      }
+      for (int pass = nib_mode ? 1 : 0; oob.load() == SIZE_MAX && pass < 2 && md == 0; ++pass) {
+        const bool two = pass == 0;
+        const std::vector<size_t>& pre = two ? p2 : p4;
+        const size_t stepb = two ? 8 : 16;
+        const swpack::PackFn fn = two ? pack2fn : pack4fn;
+        wide = 0;
+        pool.run([&](unsigned p) {
+          const size_t lo = std::min(cnt, p * step), hi = std::min(cnt, (p + 1) * step);
+          size_t at = pre[p];
+          uint32_t acc = 0;
+          for (size_t j = lo; j < hi; ++j) {
+            const size_t k = c0 + j;
+            const uint32_t l = sl[j];
+            const size_t st = (l + 31u) / 32u;
+            // full vector steps past the target's end stay inside this part's output and read
+            // inside the residues (later targets of the part rewrite those bytes)
+            const bool w = offsets[k] + st * 32 <= nres && at + st * stepb <= pre[p + 1];
+            const uint32_t v = fn(residues + offsets[k], l, cb + at, w);
+            acc = two ? (acc | v) : std::max(acc, v);
+            so[j] = at;
+            at += two ? (l + 3) / 4 : (l + 1) / 2;
+          }
+          if (two ? acc > 3u : acc >= (uint32_t)SW_DNA_ALPHA) wide = 1;
+        });
+        if (wide.load() == 0) md = two ? SWK_PACK_STREAM : SWK_PACK_NIBBLE;
+        else if (two) nib_mode = true;
+      }
+      if (oob.load() == SIZE_MAX && md == 0) {  // a code outside the alphabet
+        for (size_t j = 0; j < cnt && err == SW_OK; ++j)
+          for (uint32_t x = 0; x < rlens[c0 + j]; ++x)
+            if (residues[offsets[c0 + j] + x] >= (uint8_t)SW_DNA_ALPHA) {
+              fail(b, SW_ERR_ARG, "target %zu code %u outside alphabet", c0 + j,
+                   (unsigned)residues[offsets[c0 + j] + x]);
+              err = SW_ERR_ARG;
+              break;
+            }
+        if (err == SW_OK) err = fail(b, SW_ERR_ARG, "code outside alphabet");
+        break;
+      }
+      if (md != 0) {
+        if (!chunk_perm(pool, sl, cnt, sp))  // already longest first: the identity
+          for (size_t j = 0; j < cnt; ++j) sp[j] = (uint32_t)j;
+        bytes = ca + (md == SWK_PACK_STREAM ? p2[PT] : p4[PT]);
+      }
+    } else if (recs) {  // 2-bit data bytes of every record; lengths must all be L
       sb = (L + 3) / 4;
       std::atomic<bool> other{false};
       const size_t step = (cnt + PT - 1) / PT;
@@ -2170,7 +2249,7 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       }
       md = SWK_PACK_STREAM;
     }
-    for (int pass = nib_mode ? 1 : 0; !recs && pass < 2 && md == 0; ++pass) {
+    for (int pass = nib_mode ? 1 : 0; !recs && !rlens && pass < 2 && md == 0; ++pass) {
       sb = pass == 0 ? (L + 3) / 4 : nib;
       const size_t stepb = pass == 0 ? 8 : 16;  // bytes one 32-code vector step stores
       const swpack::PackFn fn = pass == 0 ? pack2fn : pack4fn;
@@ -2238,7 +2317,7 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       if (err == SW_OK) err = fail(b, SW_ERR_ARG, "code outside alphabet");
       break;
     }
-    const size_t bytes = cnt * sb;
+    if (!rlens) bytes = cnt * sb;
     std::memset(codes + bytes, 0, 16);  // the last targets' final step reads a few bytes past
     const hipError_t e1 = hipMemcpyAsync(b->sbuf.p + roff[i], codes, bytes + 16,
                                          hipMemcpyHostToDevice, b->copy_stream);
@@ -2362,6 +2441,12 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   if (max_len && *std::min_element(pmin.begin(), pmin.end()) == max_len) {
     bool used = false;
     st = stream_feed(b, residues, nres, offsets, n, max_len, out, used);
+    if (used) return st;
+  } else if (max_len && env_int("SWBANK_STREAM_RAGGED", 0) != 0) {
+    // ragged streamed (opt-in): exact, but slower than the chunked feeder on the ragged
+    // bench shape (host-side order per chunk on the gather's critical path)
+    bool used = false;
+    st = stream_feed(b, residues, nres, offsets, n, max_len, out, used, nullptr, lens);
     if (used) return st;
   }
   // slot: offsets u64 | lens | perm | count | ident (SlotTail) | codes at codes_at(cnt): one byte per

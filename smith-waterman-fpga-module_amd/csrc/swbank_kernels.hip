@@ -714,6 +714,12 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int snc = (int)a.qwords;
   int scur = -1, st0 = 0;
   uint32_t scn = 0, sro_lo = 0, sro_hi = 0, smode = SWK_PACK_STREAM;
+  // ragged streamed batches (ulen == 0): a chunk's region is offsets u64 | lengths u32 | visiting
+  // order u32 (scn each) | codes at the next 16-byte boundary; the order of the chunk of the tile
+  // this wave is scoring (wperm, its first tile wst0) maps score positions to targets
+  const uint32_t* cperm = nullptr;
+  const uint32_t* wperm = nullptr;
+  int wst0 = 0;
   const auto stream_tile = [&](int t, uint32_t& pk) -> Lane2 {
     if (t >= ntiles) {  // past the batch: reads nothing
       pk = SWK_PACK_STREAM;
@@ -737,8 +743,15 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
                   : SWK_PACK_STREAM;
     }
     pk = smode;
-    return lane_targets(a.res + ((size_t)sro_hi << 32 | sro_lo), nullptr, nullptr, scn, t - st0,
-                        lane, pk, nullptr, a.ulen,
+    const uint8_t* base = a.res + ((size_t)sro_hi << 32 | sro_lo);
+    if (a.ulen == 0) {  // ragged: the chunk's own offsets, lengths and order
+      const uint64_t* co = reinterpret_cast<const uint64_t*>(base);
+      const uint32_t* cl = reinterpret_cast<const uint32_t*>(base + 8 * (size_t)scn);
+      cperm = cl + scn;
+      return lane_targets(base + (((size_t)scn * 16 + 15) & ~(size_t)15), co, cl, scn, t - st0,
+                          lane, pk, cperm, 0u, 0u);
+    }
+    return lane_targets(base, nullptr, nullptr, scn, t - st0, lane, pk, nullptr, a.ulen,
                         pk == SWK_PACK_NIBBLE ? (a.ulen + 1) / 2 : (a.ulen + 3) / 4);
   };
 
@@ -754,8 +767,13 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     }
   }
   Lane2 cur;
-  if constexpr (STREAM) cur = stream_tile(tile, packed);
-  else cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen, a.ustride);
+  if constexpr (STREAM) {
+    cur = stream_tile(tile, packed);
+    wperm = cperm;
+    wst0 = st0;
+  } else {
+    cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen, a.ustride);
+  }
   int nch, nfull;
   tile_chunks(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
               nfull);
@@ -1073,8 +1091,15 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
             blo = f16_unscore((uint32_t)blo);
             bhi = f16_unscore((uint32_t)bhi);
           }
-          const size_t slo = idx && tlo < n ? idx[tlo] : tlo;
-          const size_t shi = idx && thi < n ? idx[thi] : thi;
+          size_t slo = idx && tlo < n ? idx[tlo] : tlo;
+          size_t shi = idx && thi < n ? idx[thi] : thi;
+          if constexpr (STREAM) {  // ragged: through the chunk's visiting order
+            if (wperm) {
+              const size_t b0 = (size_t)wst0 * SWB_TILE;
+              if (tlo < n) slo = b0 + wperm[tlo - b0];
+              if (thi < n) shi = b0 + wperm[thi - b0];
+            }
+          }
           int32_t* qsc = MQ ? a.scores + (size_t)q * a.sstride : a.scores;
           if (a.accum) {  // best over the previous query segments
             if (tlo < n) blo = max(blo, qsc[slo]);
@@ -1091,7 +1116,11 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         best = (u16x2){0, 0};
         prevUpH = H0;
         tile = ntile;
-        if constexpr (STREAM) packed = packed_n;
+        if constexpr (STREAM) {
+          packed = packed_n;
+          wperm = cperm;
+          wst0 = st0;
+        }
         if constexpr (MQ && PAIR) unit = nunit;
         if constexpr (MQ && !PAIR) {  // several queries: the next unit's row LUTs
           unit = nunit;
@@ -1884,7 +1913,7 @@ extern "C" hipError_t swk_launch_stream(int R, int gotoh, int f16, int pair, con
                                         uint32_t pad, int W, int32_t* scores, uint32_t pS1,
                                         uint32_t pS2, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (!sc || !hflag || !dflag || !tctr || nsc == 0 || ulen == 0) return hipErrorInvalidValue;
+  if (!sc || !hflag || !dflag || !tctr || nsc == 0) return hipErrorInvalidValue;
   swk::ScoreArgs a{res,  nullptr, nullptr, n, qtab, nv, S, O, E, PS, pad, scores, nullptr, nullptr,
                    0u, 0u, (uint32_t)SWK_PACK_STREAM, nullptr, nullptr, 0u, nullptr, pS1, pS2,
                    swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),

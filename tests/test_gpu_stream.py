@@ -355,3 +355,80 @@ def test_stream_records_other_lengths(monkeypatch, where):
     sel = np.unique(np.concatenate([rng.choice(n, 300, replace=False), [k]]))
     want = O.score_batch(q, *S.pack_targets([seqs[j] for j in sel]), O.dna_matrix(), -12, -4)
     assert np.array_equal(got[sel], want)
+
+
+def _ragged(rng, n, lo, hi, p_n=0.0, gap=0):
+    lens = rng.integers(lo, hi + 1, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gap)
+    res = rng.integers(0, 4, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    if p_n:
+        res[rng.random(res.size) < p_n] = 4
+    return res, offs, lens
+
+
+@pytest.mark.parametrize("case", ["2bit", "nibble", "empty", "gaps", "big", "u16", "gotoh"])
+def test_stream_ragged(monkeypatch, case):
+    """Ragged batches stream too when asked (SWBANK_STREAM_RAGGED=1): each chunk carries its
+    offsets, lengths and longest-first order ahead of its codes; scores equal the chunked
+    feeder's (SWBANK_STREAM_RAGGED=0) and the oracle's on a sample."""
+    if case != "big":
+        monkeypatch.setenv("SWBANK_STREAM", "2")
+    monkeypatch.setenv("SWBANK_STREAM_RAGGED", "1")  # opt-in
+    rng = np.random.default_rng(len(case) * 13)
+    n = 300_000 if case == "big" else 30_000
+    lo, hi = {"empty": (0, 40), "big": (64, 150)}.get(case, (20, 200))
+    res, offs, lens = _ragged(rng, n, lo, hi, p_n=0.002 if case in ("nibble", "big") else 0.0,
+                              gap=3 if case == "gaps" else 0)
+    gotoh = case == "gotoh"
+    params = (5, -4, -10, -1) if gotoh else REF
+    if case == "u16":
+        monkeypatch.setenv("SWBANK_F16", "0")
+    q = rng.integers(0, 4, 110, dtype=np.uint8)
+    with S.ScoreBank(gap_model=S.GAP_GOTOH if gotoh else S.GAP_MERGED) as bank:
+        bank.set_penalties(*params)
+        bank.load_query(q)
+        got = bank.score_batch(res, offs, lens)
+        kern = bank.last_kernel()
+        best = bank.best()
+        monkeypatch.setenv("SWBANK_STREAM_RAGGED", "0")
+        ref = bank.score_batch(res, offs, lens)
+    assert "streamed=" in kern, kern
+    assert np.array_equal(got, ref), kern
+    top = int(np.argmax(got))
+    assert best[1:] == (int(got[top]), top)
+    sel = np.unique(np.concatenate([rng.choice(n, 400, replace=False), np.arange(n - 130, n)]))
+    sub = [res[int(offs[k]):int(offs[k]) + int(lens[k])] for k in sel]
+    want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(*params[:2]), *params[2:],
+                         O.GAP_GOTOH if gotoh else O.GAP_MERGED)
+    assert np.array_equal(got[sel], want), kern
+
+
+@pytest.mark.parametrize("kind", ["code", "range"])
+def test_stream_ragged_errors(monkeypatch, kind):
+    """A bad code or a target past the residues in a ragged streamed batch: SW_ERR_ARG naming
+    the target, and the bank scores the next call."""
+    monkeypatch.setenv("SWBANK_STREAM", "2")
+    monkeypatch.setenv("SWBANK_STREAM_RAGGED", "1")  # opt-in
+    rng = np.random.default_rng(71)
+    res, offs, lens = _ragged(rng, 30_000, 10, 120)
+    k = 21_000
+    bad_res, bad_offs = res.copy(), offs.copy()
+    if kind == "code":
+        bad_res[int(offs[k]) + 2] = 7
+        lens[k] = max(lens[k], 5)
+    else:
+        bad_offs[k] = res.size - 1
+        lens[k] = max(lens[k], 5)
+    q = rng.integers(0, 4, 70, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        with pytest.raises(S.SwbankError) as ei:
+            bank.score_batch(bad_res, bad_offs, lens)
+        assert ei.value.status == S.ERR_ARG and f"target {k}" in str(ei.value), str(ei.value)
+        got = bank.score_batch(res, offs, lens)
+        assert "streamed=" in bank.last_kernel()
+    sel = rng.choice(len(lens), 300, replace=False)
+    sub = [res[int(offs[j]):int(offs[j]) + int(lens[j])] for j in sel]
+    assert np.array_equal(got[sel], O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(), -12, -4))
