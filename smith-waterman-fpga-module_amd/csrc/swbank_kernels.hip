@@ -574,8 +574,8 @@ struct ScoreArgs {
   // query q - 1's, its scores sstride entries after; edge rows are per unit.  nq <= 1: one query
   uint32_t nq, qwords;
   size_t sstride;
-  // streamed batch (STREAM variants, the host feeder): equal-length targets (ulen codes) in
-  // chunks of whole tiles that land in HBM while the kernel runs; chunk c's record sc[c] (nsc
+  // streamed batch (STREAM variants, the host feeder): equal-length targets (ulen codes; 0:
+  // ragged, see stream_tile) in chunks of whole tiles that land in HBM while the kernel runs; chunk c's record sc[c] (nsc
   // records) gives its first tile and its codes (res + res_off); its layout word is hflag[c]
   // in host memory (set by the host once the copy landed) and dflag[c] in uncached device
   // memory (set by the first wave that saw hflag[c], polled by the others); tiles past the
@@ -1901,7 +1901,8 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
   return hipErrorInvalidValue;
 }
 
-// Streamed host batch (the feeder's one-launch path): equal-length targets (ulen codes), the
+// Streamed host batch (the feeder's one-launch path): equal-length targets (ulen codes), or
+// ragged ones (ulen = 0: each chunk's region starts with its offsets, lengths and order), the
 // chunk records `sc` and layout words dflag (device) / hflag (host), the codes in the device
 // buffer `res`; row-LUT or
 // pair-table variants without the column-0 rule, one query segment.
