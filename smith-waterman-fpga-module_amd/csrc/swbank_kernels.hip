@@ -1301,6 +1301,9 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
 // generated row blocks as the tile kernel with the lane's own LUT words / profile words in
 // VGPRs.  K = 4: one 4-row block; K = 8, 16: 8-row blocks.
 #define SWK_CLAMP(x, n) ((x) < (n) ? (x) : (n) - 1)
+#ifndef SWK_RING_PF
+#define SWK_RING_PF 0  // wave kernel, f16 profile: read the code ring one step ahead (A/B)
+#endif
 #define SWK_W_HT(B)                                                                           \
   [h0] "+v"(Hl[B]), [h1] "+v"(Hl[SWK_CLAMP(B + 1, K)]), [h2] "+v"(Hl[SWK_CLAMP(B + 2, K)]),    \
       [h3] "+v"(Hl[SWK_CLAMP(B + 3, K)]), [h4] "+v"(Hl[SWK_CLAMP(B + 4, K)]),                  \
@@ -1422,12 +1425,20 @@ __device__ __forceinline__ uint32_t dpp_shr1_zero(uint32_t v) {  // lane 0 reads
 // hold 256 columns each, and the waves of the block run nph + 2(P - 1) phases of 64 steps
 // with one barrier each, segment s two phases behind segment s - 1: its first step of a phase
 // loads 64 ring columns that the segment above finished writing by the previous barrier.
+// cring (f16 profile, main waves): the wave's 256-byte LDS code ring.  Instead of shifting a
+// code word one lane down per step (readlane + move + DPP add + two extracts), every 64 steps
+// each lane writes the letter codes of its column of the previous and of the next 64 columns
+// into ring bytes l and 64 + l (target A; target B 128 bytes on); at step T + j lane l reads
+// column T + j - l at ring position 64 + j - l and forms its two profile addresses with one
+// mad each.
 template <int K, bool COL0, bool PROF, bool GOTOH, bool F16, bool SPLIT = false>
 __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* prof,
                                            const uint32_t* qtab, uint32_t nv, uint32_t PSb,
                                            size_t pair, int lane, const uint2* lin = nullptr,
                                            uint2* lout = nullptr, int nph = 0, int seg = 0,
-                                           int P = 1) {
+                                           int P = 1, uint8_t* cring = nullptr) {
+  constexpr bool RING = F16 && PROF && !SPLIT;
+  constexpr bool PF = SWK_RING_PF != 0;  // ring letters read one step ahead
   const size_t tA = 2 * pair, tB = tA + 1;
   const size_t n = a.n;
   const bool packed = a.packed != SWK_PACK_BYTES, rec = a.packed == SWK_PACK_RECORDS;
@@ -1488,6 +1499,7 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
   u16x2 prevUpH = H0;
   uint32_t botH = as_u32(H0), botX = as_u32(X0), buf = padsel;
   uint32_t let = F16 && PROF ? padsel + lane * hop : padsel;
+  uint32_t ringprev = pad | pad << 8;  // RING: this lane's codes of the previous 64 columns
   // query segments (queries longer than 64K rows): lane 0 reads row -1 of this segment (the
   // previous segment's bottom row) from edge_in, lane 63 writes this segment's bottom row;
   // layout [pair][column] {H, G/T/F} of both targets
@@ -1501,25 +1513,48 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
   // two steps per iteration (the loop-carried values alternate registers instead of being
   // copied back); an odd count gets one extra all-padding step, which changes no score
   const int nsteps = Lmax + 63;
+  // the codes of column c of both targets (pad past the end): RING as {A, B << 8}, else the
+  // code word
+  const auto load_codes = [&](const uint32_t c) __attribute__((always_inline)) -> uint32_t {
+    uint32_t x = pad, y = pad;
+    if (nib) {
+      if (c < LA) x = (pA[c >> 1] >> (4 * (c & 1))) & 15u;
+      if (c < LB) y = (pB[c >> 1] >> (4 * (c & 1))) & 15u;
+    } else if (packed) {
+      if (c < LA) x = (pA[c >> 2] >> (2 * (c & 3))) & 3u;
+      if (c < LB) y = (pB[c >> 2] >> (2 * (c & 3))) & 3u;
+    } else {
+      if (c < LA) x = pA[c];
+      if (c < LB) y = pB[c];
+    }
+    if constexpr (RING) return min(x, pad) | (min(y, pad) << 8);
+    else return code_word(min(x, pad), min(y, pad));
+  };
+  const auto ring_write = [&](const uint32_t nc) __attribute__((always_inline)) {
+    cring[lane] = (uint8_t)ringprev;  // letters of target A at [0, 128), B at [128, 256)
+    cring[64 + lane] = (uint8_t)nc;
+    cring[128 + lane] = (uint8_t)(ringprev >> 8);
+    cring[192 + lane] = (uint8_t)(nc >> 8);
+    ringprev = nc;
+  };
+  uint32_t nra = 0, nrb = 0;  // RING && PF: the letters of the next step's column
+  if constexpr (RING && PF) {
+    ring_write(load_codes((uint32_t)lane));
+    nra = cring[64 - lane];
+    nrb = cring[192 - lane];
+  }
   const auto step = [&](const int t, const bool even, auto segc) __attribute__((always_inline)) {
     constexpr bool SEG = decltype(segc)::value;  // query segment: row -1 from edge_in
     if (even && (t & 63) == 0) {  // next 64 columns of both targets, one code pair per lane
       const uint32_t c = (uint32_t)t + lane;
-      uint32_t x = pad, y = pad;
-      if (nib) {
-        if (c < LA) x = (pA[c >> 1] >> (4 * (c & 1))) & 15u;
-        if (c < LB) y = (pB[c >> 1] >> (4 * (c & 1))) & 15u;
-      } else if (packed) {
-        if (c < LA) x = (pA[c >> 2] >> (2 * (c & 3))) & 3u;
-        if (c < LB) y = (pB[c >> 2] >> (2 * (c & 3))) & 3u;
-      } else {
-        if (c < LA) x = pA[c];
-        if (c < LB) y = pB[c];
-      }
-      buf = code_word(min(x, pad), min(y, pad));
+      if constexpr (RING && !PF) ring_write(load_codes(c));
+      else if constexpr (!RING) buf = load_codes(c);
       if (SEG) ebuf = c < (uint32_t)Lmax ? ein[c & rmask] : make_uint2(as_u32(H0), as_u32(X0));
     }
-    const uint32_t inj = __builtin_amdgcn_readlane(buf, t & 63);
+    // prefetching ring: the next block's codes go in before step T + 64's codes are read
+    if constexpr (RING && PF)
+      if (!even && (t & 63) == 63) ring_write(load_codes((uint32_t)t + 1 + lane));
+    const uint32_t inj = RING ? 0u : __builtin_amdgcn_readlane(buf, t & 63);
     u16x2 upH, upX;
     if constexpr (SEG) {
       upH = as_u16x2(dpp_shr1(__builtin_amdgcn_readlane(ebuf.x, t & 63), botH));
@@ -1528,7 +1563,16 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
       upH = as_u16x2(as_u32(H0) == 0 ? dpp_shr1_zero(botH) : dpp_shr1(as_u32(H0), botH));
       upX = as_u16x2(as_u32(X0) == 0 ? dpp_shr1_zero(botX) : dpp_shr1(as_u32(X0), botX));
     }
-    if constexpr (F16 && PROF) {  // shift down one lane and add the lane's row offset
+    uint32_t rca = 0, rcb = 0;  // RING: the two letters of column t - lane
+    if constexpr (RING && PF) {
+      rca = nra;
+      rcb = nrb;
+    } else if constexpr (RING) {
+      // (t & 62) is shared by the two steps of an iteration: one address add per two steps
+      const uint8_t* rp = cring + (64 - lane) + (t & 62);
+      rca = rp[even ? 0 : 1];
+      rcb = rp[even ? 128 : 129];
+    } else if constexpr (F16 && PROF) {  // shift down one lane and add the lane's row offset
       uint32_t nl = inj;
       asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
                    : "+v"(nl) : "v"(let), "v"(hop));
@@ -1543,8 +1587,9 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
       const bool z = COL0 && t == lane;
       if constexpr (PROF) {
         ProfLookupK16<K> lk;
-        const uint8_t* lds = prof;
-        const uint32_t olo = let & 0xFFFFu, ohi = let >> 16;
+        const uint8_t* lds = RING ? prof + lane * 2 * K : prof;
+        const uint32_t olo = RING ? __umul24(rca, PSb) : let & 0xFFFFu;
+        const uint32_t ohi = RING ? __umul24(rcb, PSb) : let >> 16;
         if constexpr (K == 2) {
           lk.lo[0] = *reinterpret_cast<const uint32_t*>(lds + olo);
           lk.hi[0] = *reinterpret_cast<const uint32_t*>(lds + ohi);
@@ -1562,6 +1607,11 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
             lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z;
             lk.hi[4 * q + 3] = y.w;
           }
+        }
+        if constexpr (RING && PF) {  // the next step's letters (block start: the new block)
+          const uint8_t* np = cring + (64 - lane) + (even ? (t & 62) + 1 : ((t + 1) & 63));
+          nra = np[0];
+          nrb = np[128];
         }
         if constexpr (COL0)
           column_merged_f16_mask<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, z);
@@ -1778,7 +1828,10 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
   const size_t tA = 2 * pair, tB = tA + 1;
   const size_t n = a.n;
   if (tA >= n || pair >= a.main_pairs) return;  // whole wave
-  uint2 b = wave_pair<K, COL0, PROF, GOTOH, F16>(a, prof, a.qtab, a.nv, a.PS, pair, lane);
+  // f16 profile: each wave's code ring follows the profile in LDS
+  uint8_t* cring = F16 && PROF ? prof + (a.pad + 1) * a.PS + 256 * (threadIdx.x >> 6) : nullptr;
+  uint2 b = wave_pair<K, COL0, PROF, GOTOH, F16>(a, prof, a.qtab, a.nv, a.PS, pair, lane,
+                                                 nullptr, nullptr, 0, 0, 1, cring);
   if constexpr (F16) {
     // optimistic f16: a pair above 2048 - max(s) may have rounded; re-score it in u16 now
     // (the profile from HBM: rare, and no LDS for a second table)
@@ -1808,6 +1861,7 @@ static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream
                                        : 4u;
   const size_t blocks = a.split_blocks + ((size_t)a.main_pairs + wpb - 1) / wpb;
   size_t lds = PROF ? prof_bytes : 0;
+  if (F16 && PROF) lds += 256 * wpb;  // the waves' code rings
   if (a.split_blocks)  // every segment's profile, or the 8 words of the segment combine
     lds = std::max<size_t>(lds, PROF ? (size_t)a.split_words * 4 * a.split_P : 64);
   auto fn = &score_wave<K, COL0, PROF, GOTOH, F16>;
