@@ -1301,8 +1301,11 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
 // generated row blocks as the tile kernel with the lane's own LUT words / profile words in
 // VGPRs.  K = 4: one 4-row block; K = 8, 16: 8-row blocks.
 #define SWK_CLAMP(x, n) ((x) < (n) ? (x) : (n) - 1)
+#ifndef SWK_RING_SPLIT
+#define SWK_RING_SPLIT 0  // the split tail's segment waves use the code ring too (A/B)
+#endif
 #ifndef SWK_RING_PF
-#define SWK_RING_PF 0  // wave kernel, f16 profile: read the code ring one step ahead (A/B)
+#define SWK_RING_PF 1  // wave kernel, f16 profile: read the code ring one step ahead
 #endif
 #define SWK_W_HT(B)                                                                           \
   [h0] "+v"(Hl[B]), [h1] "+v"(Hl[SWK_CLAMP(B + 1, K)]), [h2] "+v"(Hl[SWK_CLAMP(B + 2, K)]),    \
@@ -1437,7 +1440,7 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
                                            size_t pair, int lane, const uint2* lin = nullptr,
                                            uint2* lout = nullptr, int nph = 0, int seg = 0,
                                            int P = 1, uint8_t* cring = nullptr) {
-  constexpr bool RING = F16 && PROF && !SPLIT;
+  constexpr bool RING = F16 && PROF && SWK_RING_SPLIT >= (SPLIT ? 1 : 0);
   constexpr bool PF = SWK_RING_PF != 0;  // ring letters read one step ahead
   const size_t tA = 2 * pair, tB = tA + 1;
   const size_t n = a.n;
@@ -1756,8 +1759,10 @@ __device__ __forceinline__ void wave_split_block(const ScoreArgs& a, uint32_t* s
   }
   const uint8_t* sprof = PROF ? prof + (size_t)seg * a.split_words * 4 : nullptr;
   const uint32_t* sq = a.split_qtab + (size_t)seg * a.split_words;
+  uint8_t* cring = F16 && PROF && SWK_RING_SPLIT
+                       ? prof + (size_t)P * a.split_words * 4 + 256 * wave : nullptr;
   uint2 b = wave_pair<KS, COL0, PROF, GOTOH, F16, true>(a, sprof, sq, a.nv, a.split_PS, p, lane,
-                                                         lin, lout, nph, seg, P);
+                                                         lin, lout, nph, seg, P, cring);
   // LDS is free again (the last phase ended with a barrier): combine the pair's segments
   uint32_t blockmax = 0;
   const auto combine = [&](uint2 v) -> uint2 {
@@ -1863,7 +1868,9 @@ static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream
   size_t lds = PROF ? prof_bytes : 0;
   if (F16 && PROF) lds += 256 * wpb;  // the waves' code rings
   if (a.split_blocks)  // every segment's profile, or the 8 words of the segment combine
-    lds = std::max<size_t>(lds, PROF ? (size_t)a.split_words * 4 * a.split_P : 64);
+    lds = std::max<size_t>(lds, PROF ? (size_t)a.split_words * 4 * a.split_P +
+                                           (F16 && SWK_RING_SPLIT ? 256 * 4 : 0)
+                                     : 64);
   auto fn = &score_wave<K, COL0, PROF, GOTOH, F16>;
   static bool attr_set = false;
   if (!attr_set) {
