@@ -207,6 +207,7 @@ class Workload:
             self.params = {"matrix": "BLOSUM62", "gap_open": -11, "gap_extend": -1,
                            "gap_model": "gotoh (ssearch36)"}
         n = self.n
+        self.Lmin = int(self.lens.min())
         self.d_res = torch.from_numpy(self.res).to(dev)
         self.d_offs = torch.from_numpy(self.offs.view(np.int64)).to(dev)
         self.d_lens = torch.from_numpy(self.lens.view(np.int32)).to(dev)
@@ -260,16 +261,18 @@ class Workload:
         if len(self.queries) > 1:
             self.bank.score_batch_device(self.d_res.data_ptr(), self.d_offs.data_ptr(),
                                          self.d_lens.data_ptr(), self.n, self.L,
-                                         d_sc.data_ptr(), stream)
+                                         d_sc.data_ptr(), stream, min_len=self.Lmin)
             return
         for k, q in enumerate(self.queries):
             if self.d_rec is not None:
                 self.bank.score_records_device(self.d_rec.data_ptr(), self.n,
                                                d_sc[k].data_ptr(), stream)
                 continue
+            # the caller's length range (sw_score_batch_device_range): a fixed-length batch
+            # needs no visiting order, a ragged one is sorted longest first on the device
             self.bank.score_batch_device(self.d_res.data_ptr(), self.d_offs.data_ptr(),
                                          self.d_lens.data_ptr(), self.n, self.L,
-                                         d_sc[k].data_ptr(), stream)
+                                         d_sc[k].data_ptr(), stream, min_len=self.Lmin)
 
 
 def main():

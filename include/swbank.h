@@ -51,8 +51,9 @@ extern "C" {
 #endif
 
 /* ABI 2: ids on the batch calls and the batch best hit (ScoreBank_v2.v:39-43), multi-device
- * banks (sw_config.n_devices / devices[]), scores past the 16-bit lanes (int32 re-score). */
-#define SWBANK_ABI_VERSION 2
+ * banks (sw_config.n_devices / devices[]), scores past the 16-bit lanes (int32 re-score).
+ * ABI 3: sw_score_batch_device_range (caller length range) and sw_bank_counters. */
+#define SWBANK_ABI_VERSION 3
 
 typedef int32_t sw_status;
 enum {
@@ -157,6 +158,16 @@ sw_status sw_score_batch_device(sw_bank *bank, const uint8_t *d_residues,
                                 const uint64_t *d_ids, size_t n, uint32_t max_len,
                                 int32_t *d_scores, void *stream);
 
+/* The same with the caller's length range: every d_lens[k] lies in [min_len, max_len].  The
+ * RTL's feeder takes each target's LEN as given (SM_Feeder3.v:135-140) and feeds in arrival
+ * order (ScoreBank_v2.v:142-148); when the range holds one length (a fixed-length read batch,
+ * min_len == max_len) no visiting order is built on the device at all, as there.
+ * sw_score_batch_device is this call with min_len = 0. */
+sw_status sw_score_batch_device_range(sw_bank *bank, const uint8_t *d_residues,
+                                      const uint64_t *d_offsets, const uint32_t *d_lens,
+                                      const uint64_t *d_ids, size_t n, uint32_t min_len,
+                                      uint32_t max_len, int32_t *d_scores, void *stream);
+
 /* Best hit of the last batch call (≙ the bank's max / vld_max outputs, ScoreBank_v2.v:42-43):
  * the lowest input index with the maximum score, its id (ids[index], the record's ID for
  * sw_score_records, else the index) and score.  Waits for a device call's stream.
@@ -202,6 +213,21 @@ sw_status sw_bank_set_timing(sw_bank *bank, int32_t enable);
  * the feeder (pack: host gather / packing time of the host-buffer calls) and of the score
  * kernels (device time) since the previous call. */
 sw_status sw_bank_timing(sw_bank *bank, uint64_t *launches, double *pack_ms, double *score_ms);
+/* Feeder / fallback counters since the bank was created (a multi-device bank sums its
+ * devices'), so silent slow paths show: host calls that ran as one streamed kernel, streamed
+ * calls re-run through the chunked feeder because a chunk's wait ran out, streamed calls
+ * declined for the memory cap (SWBANK_STREAM_MB) or a failed allocation, chunked host calls,
+ * device-side length sorts, and multi-device gathers abandoned after their time limit. */
+typedef struct sw_counters {
+  uint64_t stream_calls;
+  uint64_t stream_reruns;
+  uint64_t stream_declined;
+  uint64_t chunked_calls;
+  uint64_t device_sorts;
+  uint64_t gather_timeouts;
+} sw_counters;
+sw_status sw_bank_counters(const sw_bank *bank, sw_counters *out);
+
 /* Which kernel the last score call ran, e.g. "tile f16 R=32 W=4 segs=1 grid=998" or
  * "wave u16 K=4" (empty before the first call).  No reference counterpart: the RTL has one
  * datapath; this lets tests and profiles confirm the path taken. */

@@ -127,6 +127,8 @@ int main(int argc, char **argv) {
           if (end == p || (*end && *end != ',')) return usage(argv[0]), 1;
           p = *end ? end + 1 : end;
         }
+        /* an empty list, or more devices than a bank holds */
+        if (ndev == 0 || *p) return usage(argv[0]), 1;
         device = devs[0];
         break;
       }

@@ -390,6 +390,9 @@ struct sw_bank {
   hipEvent_t ev_ready = nullptr, ev_used = nullptr;
   PinBuf stage;
 
+  // feeder / fallback counters (sw_bank_counters)
+  sw_counters ctr{};
+
   // profiling
   bool timing = false;
   struct Ev { hipEvent_t a, b, c; };
@@ -667,6 +670,20 @@ extern "C" int32_t sw_bank_devices(const sw_bank* b, int32_t* devices, int32_t c
 extern "C" const char* sw_last_error(const sw_bank* b) { return b ? b->err : "null bank"; }
 
 extern "C" const char* sw_last_kernel(const sw_bank* b) { return b ? b->last_kernel : ""; }
+
+extern "C" sw_status sw_bank_counters(const sw_bank* b, sw_counters* out) {
+  if (!b || !out) return SW_ERR_ARG;
+  *out = b->ctr;
+  for (const sw_bank* k : b->kids) {
+    out->stream_calls += k->ctr.stream_calls;
+    out->stream_reruns += k->ctr.stream_reruns;
+    out->stream_declined += k->ctr.stream_declined;
+    out->chunked_calls += k->ctr.chunked_calls;
+    out->device_sorts += k->ctr.device_sorts;
+    out->gather_timeouts += k->ctr.gather_timeouts;
+  }
+  return SW_OK;
+}
 
 static void copy_kernel_name(sw_bank* b, const char* gather) {
   snprintf(b->last_kernel, sizeof(b->last_kernel), "multi[%zu] gather=%s: %s", b->kids.size(),
@@ -1214,6 +1231,16 @@ static sw_status prepare_i32(sw_bank* b) {
   return SW_OK;
 }
 
+// True when every length in [min_len, max_len] falls in the device sort's first length bin
+// (swk_sort_lens: bins of 2^shift lengths below max_len, at most 2048 of them): the caller's
+// order is then already longest first, and the sort kernels are not launched at all.
+static bool one_len_bin(uint32_t min_len, uint32_t max_len) {
+  if (min_len > max_len) return false;
+  uint32_t shift = 0;
+  while ((max_len >> shift) >= 2048u) ++shift;
+  return ((max_len - min_len) >> shift) == 0;
+}
+
 // packed (SWK_PACK_*): RECORDS: d_res holds n 64-byte CAPI records (2-bit codes), d_offs and
 // d_lens are unused; STREAM: 2-bit codes, d_offs in bytes (the host feeder's DNA chunks).
 // perm/perm_n (optional, tile kernel): pass 0 visits the targets in the order perm[0..n)
@@ -1224,7 +1251,8 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
                         const uint32_t* perm = nullptr,
                         const uint32_t* perm_n = nullptr, bool dsort = false,
                         bool wait_prev = true, uint32_t* sort_out = nullptr,
-                        uint32_t* sort_scr = nullptr, uint32_t ulen = 0, uint32_t ustride = 0) {
+                        uint32_t* sort_scr = nullptr, uint32_t ulen = 0, uint32_t ustride = 0,
+                        uint32_t min_len = 0) {
   // Past the 16-bit lanes (min(|q|, max|t|) * max(s) + max(s) > 65535) the 16-bit passes are
   // still exact for every pair scoring <= 65535 - max(s); the pairs above are re-scored by the
   // int32 kernel through an index list (swk_launch_i32).
@@ -1383,7 +1411,7 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
   // (the host feeder passes a chunk's own order (n + 2 words in its slot) and sort scratch, so
   // chunks on two streams do not share them)
   if (dsort && !use_wave && !perm && packed != SWK_PACK_RECORDS && ntiles > 1 &&
-      n <= 0xFFFFFFFFull && env_int("SWBANK_DSORT", 1) != 0) {
+      n <= 0xFFFFFFFFull && !one_len_bin(min_len, max_len) && env_int("SWBANK_DSORT", 1) != 0) {
     uint32_t* order = sort_out;
     if (!order) {
       HIPOK(b, b->dperm.reserve(n + 2));
@@ -1399,6 +1427,11 @@ static sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs
       scr = b->dsort.p;
     }
     HIPOK(b, swk_sort_lens(d_lens, n, max_len, order, order + n, order + n + 1, scr, st));
+    ++b->ctr.device_sorts;
+    if (!sort_out) {  // (the host feeder's chunks sort too: not named per chunk)
+      const size_t L = strlen(b->last_kernel);
+      snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " dsort");
+    }
     perm = order;
     perm_n = order + n;
     ident = order + n + 1;
@@ -1514,7 +1547,7 @@ static sw_status track_best_device(sw_bank* b, const int32_t* d_scores, const ui
 // optimistic f16, int32 re-scores, a wave-kernel shape; SWBANK_MQ=0) the queries run one after
 // the other through launch().
 static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
-                            const uint32_t* d_lens, size_t n, uint32_t max_len,
+                            const uint32_t* d_lens, size_t n, uint32_t min_len, uint32_t max_len,
                             int32_t* d_scores, hipStream_t st) {
   const size_t nq = b->qset.size();
   const uint64_t smax = (uint64_t)std::max(0, b->smax);
@@ -1537,7 +1570,7 @@ static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_
       rs = prepare(b);
       if (rs == SW_OK)
         rs = launch(b, d_res, d_offs, d_lens, n, max_len, d_scores + i * n, st, SWK_PACK_BYTES,
-                    nullptr, nullptr, true);
+                    nullptr, nullptr, true, true, nullptr, nullptr, 0, 0, min_len);
     }
     b->query = longest;
     b->dirty = true;
@@ -1571,7 +1604,7 @@ static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_
   const uint32_t ecols = (max_len + 7) / 8 * 8;
   // longest-first order of a ragged batch (shared by every query)
   const uint32_t *perm = nullptr, *perm_n = nullptr, *ident = nullptr;
-  if (ntiles > 1 && env_int("SWBANK_DSORT", 1) != 0) {
+  if (ntiles > 1 && !one_len_bin(min_len, max_len) && env_int("SWBANK_DSORT", 1) != 0) {
     HIPOK(b, b->dperm.reserve(n + 2));
     const size_t sw = swk_sort_scratch_bytes() / 4;
     if (b->dsort.cap < sw) {
@@ -1580,6 +1613,7 @@ static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_
     }
     HIPOK(b, swk_sort_lens(d_lens, n, max_len, b->dperm.p, b->dperm.p + n, b->dperm.p + n + 1,
                            b->dsort.p, st));
+    ++b->ctr.device_sorts;
     perm = b->dperm.p;
     perm_n = b->dperm.p + n;
     ident = b->dperm.p + n + 1;
@@ -1636,7 +1670,17 @@ extern "C" sw_status sw_score_batch_device(sw_bank* b, const uint8_t* d_res,
                                            const uint64_t* d_offs, const uint32_t* d_lens,
                                            const uint64_t* d_ids, size_t n, uint32_t max_len,
                                            int32_t* d_scores, void* stream) {
+  return sw_score_batch_device_range(b, d_res, d_offs, d_lens, d_ids, n, 0, max_len, d_scores,
+                                     stream);
+}
+
+extern "C" sw_status sw_score_batch_device_range(sw_bank* b, const uint8_t* d_res,
+                                                 const uint64_t* d_offs, const uint32_t* d_lens,
+                                                 const uint64_t* d_ids, size_t n,
+                                                 uint32_t min_len, uint32_t max_len,
+                                                 int32_t* d_scores, void* stream) {
   if (!b) return SW_ERR_ARG;
+  if (min_len > max_len) return fail(b, SW_ERR_ARG, "min_len %u > max_len %u", min_len, max_len);
   if (b->is_multi())
     return fail(b, SW_ERR_UNSUPPORTED, "device buffers need a single-device bank");
   b->best_kind = 0;
@@ -1648,10 +1692,10 @@ extern "C" sw_status sw_score_batch_device(sw_bank* b, const uint8_t* d_res,
   hipStream_t hs = stream ? reinterpret_cast<hipStream_t>(stream) : b->stream;
   if (b->qset.size() > 1) {  // a query set: nq x n scores; the best hit is not tracked
     if (d_ids) return fail(b, SW_ERR_UNSUPPORTED, "best hit over a query set");
-    return launch_set(b, d_res, d_offs, d_lens, n, max_len, d_scores, hs);
+    return launch_set(b, d_res, d_offs, d_lens, n, min_len, max_len, d_scores, hs);
   }
   if ((st = launch(b, d_res, d_offs, d_lens, n, max_len, d_scores, hs, SWK_PACK_BYTES, nullptr,
-                   nullptr, true)) != SW_OK)
+                   nullptr, true, true, nullptr, nullptr, 0, 0, min_len)) != SW_OK)
     return st;
   return d_ids ? track_best_device(b, d_scores, d_ids, n, hs) : SW_OK;
 }
@@ -1837,6 +1881,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
                       ScoreF score, int32_t* out, bool overlap) {
   sw_status st = feeder_init(b);
   if (st != SW_OK) return st;
+  ++b->ctr.chunked_calls;
   size_t slot_bytes = 0;
   for (const Chunk& c : chunks) slot_bytes = std::max(slot_bytes, c.bytes);
   for (int i = 0; i < std::min<int>(sw_bank::NSLOT, (int)chunks.size()); ++i) {
@@ -2001,7 +2046,6 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                        std::min<uint64_t>(b->query.size(), L) * smax + smax <= 2048u;
   const bool pair = use_f16 && b->pair_bytes != 0 && env_int("SWBANK_PAIR", 1) != 0;
   if (!(b->R == 16 || (b->R == 32 && !b->gotoh()))) return SW_OK;  // streamed variants
-  used = true;
 
   // chunks of whole tiles: 1/64 of the batch first, doubling up to 1/8
   std::vector<size_t> tile0;
@@ -2019,36 +2063,50 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     roff[i + 1] = roff[i] + (head + cnt * nib + 64 + 255) / 256 * 256;
     slot_bytes = std::max(slot_bytes, roff[i + 1] - roff[i]);
   }
+  // Memory the streamed call keeps for the bank's lifetime: the batch's 4-bit codes on the
+  // device (sbuf), NSLOT pinned host slots of the largest chunk (<= 1/8 of it each) and the
+  // batch's scores in coherent host memory.  Past SWBANK_STREAM_MB (default 4096 MiB of device
+  // codes + host scores), or when any of it cannot be allocated, the call runs through the
+  // chunked feeder, whose slots are bounded by chunk_target() (counted: stream_declined).
+  const size_t cap_bytes = (size_t)std::max(1, env_int("SWBANK_STREAM_MB", 4096)) << 20;
+  if (roff[nsc] + n * 4 > cap_bytes) {
+    ++b->ctr.stream_declined;
+    return SW_OK;
+  }
   HIPOK(b, hipSetDevice(b->device));
   if (!b->kstream) {  // (no queue of its own: the chunked feeder)
-    if (b->cus <= 0) {
-      used = false;
-      return SW_OK;
-    }
+    if (b->cus <= 0) return SW_OK;
     std::vector<uint32_t> mask(((size_t)b->cus + 31) / 32, 0xFFFFFFFFu);
     if (hipExtStreamCreateWithCUMask(&b->kstream, (uint32_t)mask.size(), mask.data()) !=
         hipSuccess) {
       b->kstream = nullptr;
       (void)hipGetLastError();
-      used = false;
       return SW_OK;
     }
   }
   hipStream_t ks = b->kstream;
-  HIPOK(b, b->sbuf.reserve(roff[nsc]));
-  HIPOK(b, b->sflag.reserve(nsc * 4));
-  HIPOK(b, b->sdrec.reserve(nsc));
-  HIPOK(b, b->sctr.reserve(1));
-  HIPOK(b, b->srec.reserve(nsc * sizeof(SwkStreamChunk)));
-  HIPOK(b, b->shflag.reserve(nsc * 8));  // layout words | abort words
-  for (int i = 0; i < std::min<int>(sw_bank::NSLOT, (int)nsc); ++i)
-    HIPOK(b, b->hslot[i].reserve(slot_bytes));
-  HIPOK(b, b->shscores.reserve(n * 4));
-  while (b->sev.size() < nsc) {  // blocking sync: the publisher sleeps in them
-    hipEvent_t e;
-    HIPOK(b, hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
-    b->sev.push_back(e);
+  {
+    bool ok = b->sbuf.reserve(roff[nsc]) == hipSuccess && b->sflag.reserve(nsc * 4) == hipSuccess &&
+              b->sdrec.reserve(nsc) == hipSuccess && b->sctr.reserve(1) == hipSuccess &&
+              b->srec.reserve(nsc * sizeof(SwkStreamChunk)) == hipSuccess &&
+              b->shflag.reserve(nsc * 8) == hipSuccess &&  // layout words | abort words
+              b->shscores.reserve(n * 4) == hipSuccess;
+    for (int i = 0; ok && i < std::min<int>(sw_bank::NSLOT, (int)nsc); ++i)
+      ok = b->hslot[i].reserve(slot_bytes) == hipSuccess;
+    while (ok && b->sev.size() < nsc) {  // blocking sync: the publisher sleeps in them
+      hipEvent_t e;
+      ok = hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync) == hipSuccess;
+      if (ok) b->sev.push_back(e);
+    }
+    if (!ok) {  // out of device or pinned memory: the chunked feeder (bounded slots) instead
+      (void)hipGetLastError();
+      b->sbuf.release();
+      b->shscores.release();
+      ++b->ctr.stream_declined;
+      return SW_OK;
+    }
   }
+  used = true;
   SwkStreamChunk* rec = reinterpret_cast<SwkStreamChunk*>(b->srec.p);
   uint32_t* hflag = reinterpret_cast<uint32_t*>(b->shflag.p);
   for (size_t i = 0; i < nsc; ++i) {
@@ -2109,6 +2167,9 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   const int hold_ms = env_int("SWBANK_STREAM_HOLD_MS", 0);
   std::vector<std::chrono::steady_clock::time_point> pub_t(nsc);  // (SWBANK_TRACE_FILE)
   size_t published = 0;
+  // a copy that failed is never published as landed: the chunk and every later one are released
+  // to the kernel as aborted (it drains), and the call fails with SW_ERR_HIP
+  hipError_t pub_err = hipSuccess;
   std::thread publisher([&] {
     for (size_t i = 0; i < nsc; ++i) {
       {
@@ -2116,7 +2177,12 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
         pcv.wait(lk, [&] { return issued > i || stop; });
         if (issued <= i) return;
       }
-      (void)hipEventSynchronize(b->sev[i]);
+      const hipError_t e = hipEventSynchronize(b->sev[i]);
+      if (e != hipSuccess) {
+        pub_err = e;
+        for (size_t j = i; j < nsc; ++j) __atomic_store_n(&hflag[j], SWK_STREAM_ABORT, __ATOMIC_RELEASE);
+        return;
+      }
       if (i == 1 && hold_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(hold_ms));
       __atomic_store_n(&hflag[i], mode[i], __ATOMIC_RELEASE);
       pub_t[i] = std::chrono::steady_clock::now();
@@ -2361,6 +2427,8 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   // chunks' copies need until the kernel ends: chunks that never reach the kernel.)
   const hipError_t se = hipStreamSynchronize(ks);
   if (err != SW_OK) return err;
+  if (pub_err != hipSuccess)
+    return fail(b, SW_ERR_HIP, "streamed chunk copy: %s", hipGetErrorString(pub_err));
   if (nonuniform) {  // the kernel drained on aborted chunks: the chunked feeder runs the call
     used = false;
     return SW_OK;
@@ -2372,8 +2440,10 @@ static sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   for (size_t i = 0; i < nsc; ++i)
     if (__atomic_load_n(&hflag[nsc + i], __ATOMIC_ACQUIRE) == SWK_STREAM_ABORT) {
       used = false;
+      ++b->ctr.stream_reruns;
       return SW_OK;
     }
+  ++b->ctr.stream_calls;
   // scores into the caller's buffer with the best hit (lowest index of the maximum)
   const int32_t* hs = reinterpret_cast<const int32_t*>(b->shscores.p);
   std::vector<size_t> pbest(PT, SIZE_MAX);

@@ -644,12 +644,18 @@ __device__ __forceinline__ uint32_t stream_mode(const uint32_t* hflag, uint32_t*
   for (int it = 0; it < (1 << 20); ++it) {
     uint32_t v = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load(dflag + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
-    if (v) return v;
+    if (v) {
+      // the chunk's codes were written by a host-to-device copy, not by the wave that set the
+      // device word: a system-scope acquire, so no cache line of the reused buffer (an earlier
+      // call's codes) is read stale on this wave's XCD (once per chunk and wave)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      return v;
+    }
     if (((it + (int)blockIdx.x) & 15) == 0) {
       v = __builtin_amdgcn_readfirstlane(
           __hip_atomic_load(hflag + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
       if (v) {
-        if (lane == 0) __hip_atomic_store(dflag + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(dflag + c, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         return v;
       }
     }

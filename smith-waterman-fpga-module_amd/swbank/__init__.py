@@ -41,9 +41,11 @@ EXPORTS = (
     "sw_unpack_2bit", "sw_fill_matrix", "sw_bank_set_timing", "sw_bank_timing",
     "sw_last_kernel", "sw_load_query_record", "sw_score_records", "sw_score_records_device",
     "sw_best_hit_device", "sw_batch_best", "sw_bank_devices", "sw_load_queries",
-    "sw_query_count",
+    "sw_query_count", "sw_score_batch_device_range", "sw_bank_counters",
 )
-ABI_VERSION = 2
+ABI_VERSION = 3
+COUNTERS = ("stream_calls", "stream_reruns", "stream_declined", "chunked_calls", "device_sorts",
+            "gather_timeouts")
 MAX_DEVICES = 16
 RECORD_BYTES, RECORD_MAX_BASES = 64, 232
 
@@ -99,6 +101,8 @@ def lib() -> ctypes.CDLL:
         "sw_load_query": (i32, [P, u64, P, u32]),
         "sw_score_batch": (i32, [P, P, sz, P, P, P, sz, P]),
         "sw_score_batch_device": (i32, [P, P, P, P, P, sz, u32, P, P]),
+        "sw_score_batch_device_range": (i32, [P, P, P, P, P, sz, u32, u32, P, P]),
+        "sw_bank_counters": (i32, [P, P]),
         "sw_batch_best": (i32, [P, P, P, P]),
         "sw_bank_devices": (i32, [P, P, i32]),
         "sw_best_hit": (i32, [P, P, P, sz, P, P]),
@@ -353,11 +357,26 @@ class ScoreBank:
         return self.score_batch(*pack_targets(list(seqs)))
 
     def score_batch_device(self, d_res: int, d_offs: int, d_lens: int, n: int, max_len: int,
-                           d_scores: int, stream: int = 0, d_ids: int = 0):
+                           d_scores: int, stream: int = 0, d_ids: int = 0,
+                           min_len: Optional[int] = None):
         """Device pointers (ints, e.g. torch.Tensor.data_ptr()); async on `stream`.  With d_ids
-        the call also records the batch best hit on the device (best())."""
-        self._check(lib().sw_score_batch_device(self._h, d_res, d_offs, d_lens, d_ids or None,
-                                                n, max_len, d_scores, stream or None))
+        the call also records the batch best hit on the device (best()).  With min_len (every
+        length in [min_len, max_len]) the call is sw_score_batch_device_range: a range of one
+        length skips the on-device length sort."""
+        if min_len is None:
+            self._check(lib().sw_score_batch_device(self._h, d_res, d_offs, d_lens,
+                                                    d_ids or None, n, max_len, d_scores,
+                                                    stream or None))
+        else:
+            self._check(lib().sw_score_batch_device_range(self._h, d_res, d_offs, d_lens,
+                                                          d_ids or None, n, min_len, max_len,
+                                                          d_scores, stream or None))
+
+    def counters(self) -> dict:
+        """sw_bank_counters: feeder / fallback counts since the bank was created."""
+        c = (ctypes.c_uint64 * len(COUNTERS))()
+        self._check(lib().sw_bank_counters(self._h, ctypes.byref(c)))
+        return dict(zip(COUNTERS, (int(x) for x in c)))
 
     # CAPI record path (sequence_t arrays, 2-bit codes)
     def load_query_record(self, record: np.ndarray):

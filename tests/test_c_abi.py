@@ -29,6 +29,15 @@ def test_c_client_host_checks(client):
     assert r.stdout.strip() == "host ok"
 
 
+@pytest.mark.parametrize("arg", ["", ",", "0,x", ",".join(["0"] * 17)])
+def test_cli_bad_device_list(arg):
+    """-d with an empty list, a bad entry, or more devices than a bank holds is a usage error
+    (exit 1), never a read of an unset device ordinal."""
+    q, lib = O.golden_fasta("query1.fa"), O.golden_fasta("data1.fa")
+    r = subprocess.run([S.CLI_PATH, "-q", q, "-l", lib, "-d", arg], capture_output=True, text=True)
+    assert r.returncode == 1 and "usage" in r.stderr, (r.returncode, r.stderr)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("lib", ["data500.fa", "data100.fa", "data10.fa"])
 def test_c_client_scores_golden(client, lib):

@@ -189,6 +189,43 @@ def test_device_sort_ragged(lo, hi, monkeypatch):
     assert (out["1"] == want).all() and (out["0"] == want).all()
 
 
+@pytest.mark.parametrize("lo,hi", [(128, 128), (100, 101), (64, 150), (0, 3000)])
+def test_device_range_skips_sort_on_one_length(lo, hi):
+    """sw_score_batch_device_range: with the caller's length range the sort kernels run only
+    when the lengths span more than one sort bin (last_kernel names " dsort", the bank counts
+    it); a fixed-length batch keeps the caller's order with no sort launch at all.  Scores equal
+    the oracle's either way."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(lo + 7 * hi)
+    q = _codes(rng, 128)
+    n = 40000
+    lens0 = rng.integers(lo, hi + 1, n)
+    seqs = [_codes(rng, int(l)) for l in lens0]
+    res, offs, lens = O.pack_residues(seqs)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    d_sc = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    mn, mx = int(lens.min()), max(int(lens.max()), 1)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, mx,
+                                d_sc.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                                min_len=mn)
+        torch.cuda.synchronize()
+        kern, c = bank.last_kernel(), bank.counters()
+        with pytest.raises(S.SwbankError) as e:  # an empty range
+            bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n,
+                                    mx, d_sc.data_ptr(), 0, min_len=mx + 1)
+        assert e.value.status == S.ERR_ARG
+    sorted_ = mx - mn >= 1  # max_len < 2048: one length per bin
+    assert (" dsort" in kern) == sorted_ and c["device_sorts"] == int(sorted_), (kern, c)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)
+    assert (d_sc.cpu().numpy() == want).all()
+
+
 # ---- device records with a corrupt length field --------------------------------------------
 def test_device_records_clamp_corrupt_lengths():
     """A device record whose length field exceeds 232 is read as 232 bases (the kernels clamp

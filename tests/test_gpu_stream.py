@@ -166,6 +166,46 @@ def test_stream_repeat_calls(monkeypatch):
                                                           O.dna_matrix(), -12, -4))
 
 
+def test_stream_same_shape_new_data(monkeypatch):
+    """Two streamed calls of the same shape (the same chunk ranges of the reused device buffer)
+    with different codes: the second call's scores are all exact (no line of the first call's
+    codes is read stale), against the chunked feeder on every target."""
+    rng = np.random.default_rng(5)
+    q = rng.integers(0, 4, 120, dtype=np.uint8)
+    n, L = 300_000, 128
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        first = _uniform(rng, n, L)
+        bank.score_batch(*first)
+        res, offs, lens = _uniform(rng, n, L)
+        res[: 100 * L] = np.tile(q[:L], 100)[: 100 * L]  # a different best hit
+        got = bank.score_batch(res, offs, lens)
+        assert "streamed=" in bank.last_kernel(), bank.last_kernel()
+        monkeypatch.setenv("SWBANK_STREAM", "0")
+        ref = bank.score_batch(res, offs, lens)
+    assert np.array_equal(got, ref)
+
+
+def test_stream_memory_cap_falls_back(monkeypatch):
+    """A batch past the streamed path's memory cap (SWBANK_STREAM_MB) runs through the bounded
+    chunked feeder with the same scores; the decline is counted (sw_bank_counters)."""
+    rng = np.random.default_rng(6)
+    q = rng.integers(0, 4, 100, dtype=np.uint8)
+    res, offs, lens = _uniform(rng, 300_000, 150)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        ref = bank.score_batch(res, offs, lens)
+        assert "streamed=" in bank.last_kernel()
+        monkeypatch.setenv("SWBANK_STREAM_MB", "1")
+        got = bank.score_batch(res, offs, lens)
+        assert "streamed=" not in bank.last_kernel(), bank.last_kernel()
+        c = bank.counters()
+    assert c["stream_declined"] == 1 and c["stream_calls"] == 1 and c["chunked_calls"] == 1, c
+    assert np.array_equal(got, ref)
+
+
 def test_stream_with_other_banks(monkeypatch):
     """With several other banks (and their streams) open in the process, so streams share the
     process's hardware queues, the streamed call still runs streamed (its kernel on a queue of
@@ -215,8 +255,11 @@ def test_stream_stalled_chunk_reruns(monkeypatch):
         monkeypatch.delenv("SWBANK_STREAM_HOLD_MS")
         print(f"stalled call {dt:.2f} s, {kern}")
         assert "streamed=" not in kern, kern  # the chunked re-run
+        c = bank.counters()
+        assert c["stream_reruns"] == 1 and c["chunked_calls"] == 1 and c["stream_calls"] == 0, c
         again = bank.score_batch(res, offs, lens)
         assert "streamed=" in bank.last_kernel()
+        assert bank.counters()["stream_calls"] == 1
     assert np.array_equal(got, again)
     sel = rng.choice(n, 300, replace=False)
     sub = [res[int(offs[j]):int(offs[j]) + L] for j in sel]
