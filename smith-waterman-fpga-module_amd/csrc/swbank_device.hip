@@ -2764,7 +2764,11 @@ static sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       const size_t sw = swk_sort_scratch_bytes() / 4;
       if (b->sortscr[slot].cap < sw) {
         HIPOK(b, b->sortscr[slot].reserve(sw));
-        HIPOK(b, hipMemset(b->sortscr[slot].p, 0, sw * 4));
+        // on the chunk's own stream: a hipMemset is ordered on the null stream only, which
+        // does not order the bank's non-blocking streams, so the zeroing could land while the
+        // chunk's sort kernels were already counting (a corrupt visiting order: some targets
+        // scored twice, others never written)
+        HIPOK(b, hipMemsetAsync(b->sortscr[slot].p, 0, sw * 4, ks));
       }
       scr = b->sortscr[slot].p;
     }

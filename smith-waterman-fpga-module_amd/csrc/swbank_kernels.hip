@@ -575,17 +575,23 @@ struct ScoreArgs {
   uint32_t nq, qwords;
   size_t sstride;
   // streamed batch (STREAM variants, the host feeder): equal-length targets (ulen codes; 0:
-  // ragged, see stream_tile) in chunks of whole tiles that land in HBM while the kernel runs; chunk c's record sc[c] (nsc
-  // records) gives its first tile and its codes (res + res_off); its layout word is hflag[c]
-  // in host memory (set by the host once the copy landed) and dflag[c] in uncached device
-  // memory (set by the first wave that saw hflag[c], polled by the others); tiles past the
-  // first G go to workgroups dynamically (tctr: tiles taken, zeroed by the host), so a
-  // workgroup that waited on a late chunk takes fewer tiles.  These travel in fields the
-  // streamed variants never read (no target arrays, no re-score list, one query): sc = offs,
-  // hflag = lens, dflag = nidx, tctr = ident, nsc = qwords -- the argument block keeps its
-  // size (with 40 more bytes here, later launches of every variant read wrong arguments now
-  // and then on MI355X: scores of other targets, or none written)
+  // ragged, see stream_tile) in chunks of whole tiles that land in HBM while the kernel runs;
+  // chunk c's record sc[c] (nsc records) gives its first tile and its codes (res + res_off);
+  // its layout word is hflag[c] in host memory (set by the host once the copy landed) and
+  // dflag[c] in uncached device memory (set by the first wave that saw hflag[c], polled by the
+  // others); tiles past the first G go to workgroups dynamically (tctr: tiles taken, zeroed by
+  // the host), so a workgroup that waited on a late chunk takes fewer tiles.
+  // (Round 2 carried these in fields the streamed variants never read, after a build with
+  // them appended had other launches score wrong targets now and then.  That was the host
+  // feeder's sort scratch zeroed by a null-stream hipMemset racing the chunk's sort kernels on
+  // a non-blocking stream -- a corrupt visiting order -- not the argument block)
+  const SwkStreamChunk* sc;
+  const uint32_t* hflag;
+  uint32_t* dflag;
+  uint32_t* tctr;
+  uint32_t nsc;
 };
+static_assert(sizeof(ScoreArgs) == 296, "ScoreArgs layout (kernel argument block) changed");
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) void* glob_void_ptr;
@@ -716,8 +722,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   // STREAM: the chunk of this wave's current tile (tiles only grow), its first tile, target
   // count, code offset and layout
   // (wave-uniform, kept in SGPRs)
-  const SwkStreamChunk* const ssc = reinterpret_cast<const SwkStreamChunk*>(a.offs);
-  const int snc = (int)a.qwords;
+  const SwkStreamChunk* const ssc = a.sc;
+  const int snc = (int)a.nsc;
   int scur = -1, st0 = 0;
   uint32_t scn = 0, sro_lo = 0, sro_hi = 0, smode = SWK_PACK_STREAM;
   // ragged streamed batches (ulen == 0): a chunk's region is offsets u64 | lengths u32 | visiting
@@ -744,7 +750,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
                      (size_t)st0 * SWB_TILE));
       sro_lo = __builtin_amdgcn_readfirstlane(ssc[c].res_off_lo);
       sro_hi = __builtin_amdgcn_readfirstlane(ssc[c].res_off_hi);
-      smode = stream_mode(a.lens, const_cast<uint32_t*>(a.nidx), c, snc, lane) == SWK_PACK_NIBBLE
+      smode = stream_mode(a.hflag, a.dflag, c, snc, lane) == SWK_PACK_NIBBLE
                   ? SWK_PACK_NIBBLE
                   : SWK_PACK_STREAM;
     }
@@ -897,7 +903,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         if (last) {
           if (wave == 0) {
             int nt = 0;
-            if (lane == 0) nt = G + (int)atomicAdd(const_cast<uint32_t*>(a.ident), 1u);
+            if (lane == 0) nt = G + (int)atomicAdd(a.tctr, 1u);
             nt = min(__builtin_amdgcn_readfirstlane(nt), ntiles);
             if (lane == 0) {
               sq[(k + 1) % W] = nt;
@@ -1547,14 +1553,24 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
     ringprev = nc;
   };
   uint32_t nra = 0, nrb = 0;  // RING && PF: the letters of the next step's column
+  // RING && PF: this lane's ring position of step 0 (step T + j reads ring byte 64 + j - lane),
+  // and the codes of the next 64-column block, loaded one block ahead (global latency off the
+  // block boundary, where every wave of a SIMD would wait on it at about the same time)
+  const uint8_t* const cring_l = RING && PF ? cring + 64 - lane : nullptr;
+  uint32_t ncode = 0;
   if constexpr (RING && PF) {
     ring_write(load_codes((uint32_t)lane));
-    nra = cring[64 - lane];
-    nrb = cring[192 - lane];
+    ncode = load_codes(64u + lane);
+    nra = cring_l[0];
+    nrb = cring_l[128];
   }
-  const auto step = [&](const int t, const bool even, auto segc) __attribute__((always_inline)) {
+  // step t of the lane pipeline; J = t % 8 when the caller runs groups of 8 steps (RING && PF:
+  // the ring reads take immediate offsets from the group's base gb), else -1
+  const auto step = [&](const int t, const bool even, auto segc, auto jc,
+                        const uint8_t* gb) __attribute__((always_inline)) {
     constexpr bool SEG = decltype(segc)::value;  // query segment: row -1 from edge_in
-    if (even && (t & 63) == 0) {  // next 64 columns of both targets, one code pair per lane
+    constexpr int J = decltype(jc)::value;
+    if ((J < 0 ? even : J == 0) && (t & 63) == 0) {  // next 64 columns, one code pair per lane
       const uint32_t c = (uint32_t)t + lane;
       if constexpr (RING && !PF) ring_write(load_codes(c));
       else if constexpr (!RING) buf = load_codes(c);
@@ -1562,7 +1578,10 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
     }
     // prefetching ring: the next block's codes go in before step T + 64's codes are read
     if constexpr (RING && PF)
-      if (!even && (t & 63) == 63) ring_write(load_codes((uint32_t)t + 1 + lane));
+      if ((J < 0 ? !even : J == 7) && (t & 63) == 63) {
+        ring_write(ncode);
+        ncode = load_codes((uint32_t)t + 65 + lane);
+      }
     const uint32_t inj = RING ? 0u : __builtin_amdgcn_readlane(buf, t & 63);
     u16x2 upH, upX;
     if constexpr (SEG) {
@@ -1618,7 +1637,7 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
           }
         }
         if constexpr (RING && PF) {  // the next step's letters (block start: the new block)
-          const uint8_t* np = cring + (64 - lane) + (even ? (t & 62) + 1 : ((t + 1) & 63));
+          const uint8_t* np = J >= 0 && J < 7 ? gb + (J + 1) : cring_l + ((t + 1) & 63);
           nra = np[0];
           nrb = np[128];
         }
@@ -1679,6 +1698,20 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
     if (seg_out && lane == 63 && t >= 63 && t - 63 < Lmax)
       eout[(uint32_t)(t - 63) & rmask] = make_uint2(botH, botX);
   };
+  using JN = std::integral_constant<int, -1>;
+  // RING && PF: groups of 8 steps (a ring read's offset is an immediate from the group's base;
+  // up to 7 trailing all-padding steps change no score)
+  const auto group8 = [&](const int t, auto segc) __attribute__((always_inline)) {
+    const uint8_t* gb = cring_l + (t & 63);
+    step(t, true, segc, std::integral_constant<int, 0>{}, gb);
+    step(t + 1, false, segc, std::integral_constant<int, 1>{}, gb);
+    step(t + 2, true, segc, std::integral_constant<int, 2>{}, gb);
+    step(t + 3, false, segc, std::integral_constant<int, 3>{}, gb);
+    step(t + 4, true, segc, std::integral_constant<int, 4>{}, gb);
+    step(t + 5, false, segc, std::integral_constant<int, 5>{}, gb);
+    step(t + 6, true, segc, std::integral_constant<int, 6>{}, gb);
+    step(t + 7, false, segc, std::integral_constant<int, 7>{}, gb);
+  };
   if constexpr (SPLIT) {
     // every wave of the block takes part in every phase's barrier (wave-uniform branches)
     const int lag = 2 * seg;
@@ -1687,27 +1720,33 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
       if (blk >= 0 && blk < nph) {
         if (seg_in) {
           for (int t = 64 * blk; t < 64 * blk + 64; t += 2) {
-            step(t, true, std::true_type{});
-            step(t + 1, false, std::true_type{});
+            step(t, true, std::true_type{}, JN{}, nullptr);
+            step(t + 1, false, std::true_type{}, JN{}, nullptr);
           }
         } else {
           for (int t = 64 * blk; t < 64 * blk + 64; t += 2) {
-            step(t, true, std::false_type{});
-            step(t + 1, false, std::false_type{});
+            step(t, true, std::false_type{}, JN{}, nullptr);
+            step(t + 1, false, std::false_type{}, JN{}, nullptr);
           }
         }
       }
       __syncthreads();
     }
+  } else if constexpr (RING && PF) {
+    if (seg_in) {
+      for (int t = 0; t < nsteps; t += 8) group8(t, std::true_type{});
+    } else {
+      for (int t = 0; t < nsteps; t += 8) group8(t, std::false_type{});
+    }
   } else if (seg_in) {
     for (int t = 0; t < nsteps; t += 2) {
-      step(t, true, std::true_type{});
-      step(t + 1, false, std::true_type{});
+      step(t, true, std::true_type{}, JN{}, nullptr);
+      step(t + 1, false, std::true_type{}, JN{}, nullptr);
     }
   } else {
     for (int t = 0; t < nsteps; t += 2) {
-      step(t, true, std::false_type{});
-      step(t + 1, false, std::false_type{});
+      step(t, true, std::false_type{}, JN{}, nullptr);
+      step(t + 1, false, std::false_type{}, JN{}, nullptr);
     }
   }
   // max over the wave's rows, per target (f16: non-negative integers -> int)
@@ -1987,11 +2026,11 @@ extern "C" hipError_t swk_launch_stream(int R, int gotoh, int f16, int pair, con
                    swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
                    swk::f16_pair(-(int)O), nullptr, 0u, 0u, 0};
   a.ulen = ulen;
-  a.offs = reinterpret_cast<const uint64_t*>(sc);  // (see ScoreArgs: the streamed fields)
-  a.lens = hflag;
-  a.nidx = dflag;
-  a.ident = tctr;
-  a.qwords = nsc;
+  a.sc = sc;
+  a.hflag = hflag;
+  a.dflag = dflag;
+  a.tctr = tctr;
+  a.nsc = nsc;
   if (pair) {
     if (R == 32 && f16 && !gotoh)
       return swk::launch_score<32, 4, false, false, false, true, true, false, true>(a, W, 0, st);

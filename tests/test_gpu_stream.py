@@ -171,7 +171,7 @@ def test_stream_same_shape_new_data(monkeypatch):
     with different codes: the second call's scores are all exact (no line of the first call's
     codes is read stale), against the chunked feeder on every target."""
     rng = np.random.default_rng(5)
-    q = rng.integers(0, 4, 120, dtype=np.uint8)
+    q = rng.integers(0, 4, 128, dtype=np.uint8)
     n, L = 300_000, 128
     with S.ScoreBank() as bank:
         bank.set_penalties(*REF)
