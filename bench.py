@@ -302,33 +302,19 @@ def main():
 
     wl = Workload(args, rank, dev, S, torch)
     gdev = dev if backend == "nccl" else torch.device("cpu")
-    gather = ([torch.empty_like(wl.d_sc, device=gdev) for _ in range(world)]
-              if (world > 1 and rank == 0) else None)
     stream = torch.cuda.current_stream()
-    # Two score buffers: step i scores into bufs[i % 2] while the RCCL gather of step i-1
-    # (async, on RCCL's stream) still reads the other one; a buffer is rewritten only after
-    # the gather that read it has completed (work.wait() orders the compute stream after it).
-    bufs = [wl.d_sc, torch.empty_like(wl.d_sc)]
-    pending = [None, None]
-    nstep = [0]
+    # Two score buffers: step i scores into one while the async gather of step i-1 (RCCL's
+    # stream) still reads the other (swbank.dist.StepGather; gloo gathers a host copy).  The
+    # CPU tests run this same class under gloo (tests/test_dist.py).
+    from swbank.dist import StepGather
+    sg = StepGather(wl.d_sc, dst=0, stage_cpu=backend != "nccl")
 
     def step():
-        b = nstep[0] % 2
-        if pending[b] is not None:
-            pending[b].wait()
-            pending[b] = None
-        wl.run(stream.cuda_stream, bufs[b])
-        if world > 1 and backend == "nccl":
-            pending[b] = dist.gather(bufs[b], gather_list=gather, dst=0, async_op=True)
-        elif world > 1:
-            dist.gather(bufs[b].cpu(), gather_list=gather, dst=0)
-        nstep[0] += 1
+        wl.run(stream.cuda_stream, sg.buffer())
+        sg.submit()
 
     def drain():
-        for b in (0, 1):
-            if pending[b] is not None:
-                pending[b].wait()
-                pending[b] = None
+        sg.drain()
 
     for _ in range(args.warmup):
         step()
@@ -437,7 +423,8 @@ def main():
         "cpu_baseline": None,
     }
 
-    last = bufs[(nstep[0] - 1) % 2]
+    last = sg.last()
+    gather = sg.gathered
     if rank == 0 and world == 1 and wl.d_rec is None and len(wl.queries) == 1:
         out["pcie_inclusive"] = host_api_rate(wl, last)
     if rank == 0 and world == 1 and args.cpu_seconds > 0 and wl.kind == "q100xdata500":

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build libswbank with extra compile flags into lib/libswbank_NAME.so (A/B of kernel variants on
+# one box with SWBANK_LIB=...):   scripts/build_variant.sh NAME "-DSWK_PROF_AHEAD=0 ..."
+set -eu
+NAME=$1; FLAGS=${2:-}
+cd "$(dirname "$0")/../smith-waterman-fpga-module_amd"
+B=build/var_$NAME; mkdir -p $B lib
+H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -munsafe-fp-atomics -I../include -Icsrc $FLAGS"
+$H -c csrc/swbank_kernels.hip -o $B/k.o &
+$H -c csrc/swbank_device.hip -o $B/d.o &
+cc -O2 -fPIC -Wall -Wextra -std=c11 -I../include -Icsrc -c csrc/swbank_host.c -o $B/h.o
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/libswbank_$NAME.so $B/h.o $B/d.o $B/k.o
+echo "lib/libswbank_$NAME.so"

@@ -374,6 +374,7 @@ struct sw_bank {
   std::vector<sw_bank*> kids;
   std::unique_ptr<HostPool> dpool;
   std::vector<void*> comms;  // ncclComm_t per device (RCCL gather), empty -> copy gather
+  bool rccl_gather = false;  // comms wanted (re-created after an aborted gather)
   unsigned pool_threads = 0; // feeder threads (0: host_threads(); children share the host)
   DevBuf<int32_t> grecv;
   PinBuf hrecv;
@@ -440,6 +441,8 @@ struct Rccl {
   decltype(&ncclCommDestroy) commDestroy = nullptr;
   decltype(&ncclGather) gather = nullptr;
   decltype(&ncclGetErrorString) errorString = nullptr;
+  decltype(&ncclCommAbort) commAbort = nullptr;
+  decltype(&ncclCommGetAsyncError) asyncError = nullptr;
 };
 const Rccl& rccl() {
   static Rccl r;
@@ -455,8 +458,14 @@ const Rccl& rccl() {
     r.commDestroy = reinterpret_cast<decltype(&ncclCommDestroy)>(dlsym(h, "ncclCommDestroy"));
     r.gather = reinterpret_cast<decltype(&ncclGather)>(dlsym(h, "ncclGather"));
     r.errorString = reinterpret_cast<decltype(&ncclGetErrorString)>(dlsym(h, "ncclGetErrorString"));
-    r.ok = r.commInitAll && r.commDestroy && r.gather && r.errorString;
-    if (!r.ok) snprintf(r.err, sizeof(r.err), "librccl.so.1 lacks ncclCommInitAll/ncclGather");
+    r.commAbort = reinterpret_cast<decltype(&ncclCommAbort)>(dlsym(h, "ncclCommAbort"));
+    r.asyncError =
+        reinterpret_cast<decltype(&ncclCommGetAsyncError)>(dlsym(h, "ncclCommGetAsyncError"));
+    r.ok = r.commInitAll && r.commDestroy && r.gather && r.errorString && r.commAbort &&
+           r.asyncError;
+    if (!r.ok)
+      snprintf(r.err, sizeof(r.err),
+               "librccl.so.1 lacks ncclCommInitAll/ncclGather/ncclCommAbort/ncclCommGetAsyncError");
   });
   return r;
 }
@@ -535,6 +544,7 @@ extern "C" sw_status sw_bank_create(sw_bank** out, const sw_config* cfg_in) {
         nr = r.commInitAll(comms.data(), cfg.n_devices, cfg.devices);
         if (nr == ncclSuccess) b->comms.assign(comms.begin(), comms.end());
       }
+      b->rccl_gather = !b->comms.empty();
       if (b->comms.empty() && force_rccl) {
         sw_bank_destroy(b);
         return SW_ERR_UNSUPPORTED;
@@ -2941,20 +2951,97 @@ static sw_status multi_gather(sw_bank* b, const std::vector<size_t>& cnt, FeedF 
   HIPOK(b, hipSetDevice(root->device));
   HIPOK(b, b->grecv.reserve(D * cmax));
   HIPOK(b, b->hrecv.reserve(D * cmax * 4));
+  const Rccl& r = rccl();
+  if (b->rccl_gather && b->comms.empty()) {  // re-created after an aborted gather
+    std::vector<ncclComm_t> comms(D);
+    std::vector<int> devs(D);
+    for (size_t d = 0; d < D; ++d) devs[d] = b->kids[d]->device;
+    const ncclResult_t nr = r.commInitAll(comms.data(), (int)D, devs.data());
+    if (nr != ncclSuccess)
+      return fail(b, SW_ERR_HIP, "ncclCommInitAll after an aborted gather: %s", r.errorString(nr));
+    b->comms.assign(comms.begin(), comms.end());
+    HIPOK(b, hipSetDevice(root->device));
+  }
   if (!b->comms.empty()) {
-    const Rccl& r = rccl();
-    std::vector<int> nst(D, 0);
+    // One host thread per device issues its ncclGather and then watches it: done, an async
+    // RCCL error, a failure on another device, or SWBANK_GATHER_TIMEOUT_MS (default 60 s)
+    // without completion.  Any of the latter aborts every communicator (ncclCommAbort ends the
+    // collective kernels still waiting for a peer), the call fails with SW_ERR_HIP, and the next
+    // call creates the communicators again, so a device that dropped out of one gather does not
+    // leave the others blocked or the bank unusable.  (SWBANK_GATHER_FAULT=d, tests: device d
+    // reports a failure instead of joining the gather.)
+    const int timeout_ms = std::max(1, env_int("SWBANK_GATHER_TIMEOUT_MS", 60000));
+    const int fault_dev = env_int("SWBANK_GATHER_FAULT", -1);
+    std::vector<int> nst(D, 0);  // 0 ok, > 0 ncclResult_t, -1 HIP, -2 timeout, -3 peer failed
+    std::atomic<bool> failed{false};
     b->dpool->run([&](unsigned d) {
       sw_bank* k = b->kids[d];
-      if (hipSetDevice(k->device) != hipSuccess) { nst[d] = -1; return; }
+      const ncclComm_t comm = static_cast<ncclComm_t>(b->comms[d]);
+      if (hipSetDevice(k->device) != hipSuccess || (int)d == fault_dev) {
+        nst[d] = -1;
+        failed = true;
+        return;
+      }
       const ncclResult_t e = r.gather(k->scores.p, d == 0 ? b->grecv.p : nullptr, cmax, ncclInt32, 0,
-                                      static_cast<ncclComm_t>(b->comms[d]), k->stream);
-      nst[d] = e != ncclSuccess ? (int)e : hipStreamSynchronize(k->stream) != hipSuccess ? -1 : 0;
+                                      comm, k->stream);
+      if (e != ncclSuccess) {
+        nst[d] = (int)e;
+        failed = true;
+        return;
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      for (unsigned it = 0;; ++it) {
+        const hipError_t q = hipStreamQuery(k->stream);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) {
+          nst[d] = -1;
+          break;
+        }
+        ncclResult_t ae = ncclSuccess;
+        if (r.asyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+          nst[d] = (int)ae;
+          break;
+        }
+        if (failed.load()) {
+          nst[d] = -3;
+          break;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
+          nst[d] = -2;
+          break;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(it < 1000 ? 20 : 500));
+      }
+      failed = true;
     });
-    for (size_t d = 0; d < D; ++d)
-      if (nst[d] != 0)
-        return fail(b, SW_ERR_HIP, "ncclGather on device %d failed (%s)", b->kids[d]->device,
-                    nst[d] > 0 ? r.errorString((ncclResult_t)nst[d]) : "HIP");
+    if (failed.load()) {
+      bool timed_out = false;
+      for (size_t d = 0; d < D; ++d) timed_out |= nst[d] == -2;
+      for (size_t d = 0; d < D; ++d) {
+        (void)hipSetDevice(b->kids[d]->device);
+        (void)r.commAbort(static_cast<ncclComm_t>(b->comms[d]));
+      }
+      b->comms.clear();
+      for (sw_bank* k : b->kids) {  // the aborted collectives have left the streams
+        (void)hipSetDevice(k->device);
+        (void)hipStreamSynchronize(k->stream);
+        (void)hipGetLastError();
+      }
+      (void)hipSetDevice(b->device);
+      if (timed_out) ++b->ctr.gather_timeouts;
+      size_t d0 = 0;
+      while (d0 + 1 < D && nst[d0] == 0) ++d0;
+      for (size_t d = 0; d < D; ++d)  // the first device that failed on its own, not by a peer
+        if (nst[d] != 0 && nst[d] != -3) {
+          d0 = d;
+          break;
+        }
+      return fail(b, SW_ERR_HIP, "ncclGather on device %d failed (%s); communicators aborted",
+                  b->kids[d0]->device,
+                  nst[d0] > 0    ? r.errorString((ncclResult_t)nst[d0])
+                  : nst[d0] == -2 ? "timed out (SWBANK_GATHER_TIMEOUT_MS)"
+                                  : "HIP or device fault");
+    }
     HIPOK(b, hipSetDevice(root->device));
   } else {
     for (size_t d = 0; d < D; ++d) {

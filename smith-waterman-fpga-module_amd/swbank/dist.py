@@ -10,6 +10,9 @@ only exchange is one gather of the int32 score vector to rank 0 (SURVEY §8 e).
 * ``gather_scores(...)``      rank 0 receives every rank's scores (padded to equal counts for
                               the collective) and scatters them back to input order.
 * ``score_sharded(...)``      the whole path for one batch held on every rank's host.
+* ``StepGather``              bench.py's per-step gather: double-buffered score vectors and an
+                              async ``dist.gather`` to rank 0, so step i's gather overlaps step
+                              i+1's kernel (the same code under RCCL and, in the CPU tests, gloo).
 
 The backend is whatever process group is initialised: "nccl" (= RCCL over xGMI) on GPUs,
 "gloo" in the CPU tests.
@@ -75,3 +78,58 @@ def score_sharded(bank, residues: np.ndarray, offsets: np.ndarray, lens: np.ndar
     if device is not None:
         t = t.to(device)
     return gather_scores(t, idx, len(lens), group=group)
+
+
+class StepGather:
+    """Double-buffered score vectors with an asynchronous gather to rank ``dst`` per step.
+
+    Step i writes ``buffer()`` (= bufs[i % 2]) and calls ``submit()``, which starts
+    ``dist.gather(..., async_op=True)`` of it; the gather of step i-1 may still be reading the
+    other buffer, and a buffer is handed out again only after the gather that read it has
+    completed (``work.wait()``, which on RCCL orders the compute stream after the collective).
+    ``stage_cpu``: gather a host copy (gloo cannot gather device tensors); the copy is kept
+    until its gather completes.  On rank ``dst``, ``gathered`` holds every rank's vector of the
+    last completed step after ``drain()``."""
+
+    def __init__(self, like, dst: int = 0, group=None, stage_cpu: bool = False):
+        import torch
+        import torch.distributed as dist
+
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.group, self.dst, self.stage_cpu = group, dst, stage_cpu
+        self.bufs = [like, torch.empty_like(like)]
+        gdev = torch.device("cpu") if stage_cpu else like.device
+        self.gathered = ([torch.empty_like(like, device=gdev) for _ in range(self.world)]
+                         if self.world > 1 and self.rank == dst else None)
+        self.pending = [None, None]  # (work, staged tensor) per buffer
+        self.steps = 0
+
+    def buffer(self):
+        """The buffer this step scores into (waits for the gather still reading it)."""
+        b = self.steps % 2
+        if self.pending[b] is not None:
+            self.pending[b][0].wait()
+            self.pending[b] = None
+        return self.bufs[b]
+
+    def submit(self):
+        import torch.distributed as dist
+
+        b = self.steps % 2
+        if self.world > 1:
+            t = self.bufs[b].cpu() if self.stage_cpu else self.bufs[b]
+            work = dist.gather(t, gather_list=self.gathered, dst=self.dst, group=self.group,
+                               async_op=True)
+            self.pending[b] = (work, t)
+        self.steps += 1
+
+    def drain(self):
+        for b in (0, 1):
+            if self.pending[b] is not None:
+                self.pending[b][0].wait()
+                self.pending[b] = None
+
+    def last(self):
+        """The buffer of the last submitted step."""
+        return self.bufs[(self.steps - 1) % 2]

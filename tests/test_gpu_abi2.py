@@ -316,6 +316,32 @@ def test_multi_device_bank_bad_input_leaves_bank_usable(monkeypatch):
     assert (got == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
 
 
+def test_multi_device_rccl_gather_failure_leaves_bank_usable(monkeypatch):
+    """A device that fails inside the RCCL gather phase (SWBANK_GATHER_FAULT=d: it reports a
+    failure instead of joining ncclGather): the call returns SW_ERR_HIP, every communicator is
+    aborted (ncclCommAbort) rather than left waiting for the missing rank, and the next call
+    creates them again and returns exact scores.  (The box has one GPU, so this is the real
+    ncclCommInitAll / ncclGather / ncclCommAbort on a 1-rank communicator; the timeout path for a
+    peer that never arrives needs two devices.)"""
+    monkeypatch.setenv("SWBANK_GATHER", "rccl")
+    q, seqs = _ragged_batch(4, 3000)
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)
+    with S.ScoreBank(devices=[0]) as multi:
+        multi.set_penalties(*REF)
+        multi.load_query(q)
+        assert (multi.score_batch(res, offs, lens) == want).all()
+        monkeypatch.setenv("SWBANK_GATHER_FAULT", "0")
+        with pytest.raises(S.SwbankError) as e:
+            multi.score_batch(res, offs, lens)
+        assert e.value.status == S.ERR_HIP and "aborted" in str(e.value), str(e.value)
+        monkeypatch.delenv("SWBANK_GATHER_FAULT")
+        got = multi.score_batch(res, offs, lens)
+        assert multi.last_kernel().startswith("multi[1] gather=rccl"), multi.last_kernel()
+        assert multi.counters()["gather_timeouts"] == 0
+    assert (got == want).all()
+
+
 def test_cli_device_list(tmp_path, monkeypatch):
     """swbank -d 0,0: the CLI's multi-device bank reproduces the single-device transcript."""
     import subprocess

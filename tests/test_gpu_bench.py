@@ -49,13 +49,23 @@ def test_bench_two_ranks_gathered_parity(workload):
     assert ps["ranks"] == 2 and ps["mismatches"] == 0 and ps["targets"] >= 2 * 256
 
 
-@pytest.mark.parametrize("workload", ["ragged", "data500"])
+@pytest.mark.parametrize("workload", ["ragged", "data500", "reads150x1k", "protein512x1k"])
 def test_bench_workloads_one_gpu(workload):
+    """Every bench workload the driver does not run itself, at reduced size: configs[3] (the
+    query-set path, 4 x 1-kbp queries) and configs[4] (protein, the wave kernel with its split
+    tail: 2,500 targets = 1,250 pairs, 226 past one wave per SIMD)."""
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
-           "--reps", "64", "--cpu-seconds", "0", "--workload", workload]
+           "--reps", "64", "--reads", "8192", "--slice", "4", "--ptargets", "2500",
+           "--cpu-seconds", "0", "--workload", workload]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 1 and d["parity_sample"]["mismatches"] == 0
-    assert d["pcie_inclusive"]["matches_device_api"] is True
+    assert d["parity_sample"]["targets"] > 0
+    if workload != "reads150x1k":  # (one query: the host API runs beside it)
+        assert d["pcie_inclusive"]["matches_device_api"] is True
     assert 0 < d["roofline"]["frac"] <= 1.0
+    if workload == "reads150x1k":
+        assert "queries=4" in d["kernel"], d["kernel"]
+    if workload == "protein512x1k":
+        assert d["kernel"].startswith("wave") and "split=" in d["kernel"], d["kernel"]
