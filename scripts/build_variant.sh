@@ -7,8 +7,9 @@ cd "$(dirname "$0")/../smith-waterman-fpga-module_amd"
 B=build/var_$NAME; mkdir -p $B lib
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -munsafe-fp-atomics -I../include -Icsrc $FLAGS"
 $H -c csrc/swbank_kernels.hip -o $B/k.o &
-$H -c csrc/swbank_device.hip -o $B/d.o &
+for u in bank launch feeder stream multi; do $H -c csrc/swbank_$u.hip -o $B/$u.o & done
 cc -O2 -fPIC -Wall -Wextra -std=c11 -I../include -Icsrc -c csrc/swbank_host.c -o $B/h.o
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/libswbank_$NAME.so $B/h.o $B/d.o $B/k.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/libswbank_$NAME.so $B/h.o \
+  $B/bank.o $B/launch.o $B/feeder.o $B/stream.o $B/multi.o $B/k.o
 echo "lib/libswbank_$NAME.so"

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Measure tile vs wave kernel GCUPS over (query length, target length, gap model, alphabet)
-to calibrate the host's kernel choice (csrc/swbank_device.hip, launch()).  One process,
+to calibrate the host's kernel choice (csrc/swbank_launch.hip, launch()).  One process,
 interleaved, device buffers resident; prints one JSON line per case.
 usage: python scripts/kernel_choice.py [--cells 2e10]"""
 import argparse

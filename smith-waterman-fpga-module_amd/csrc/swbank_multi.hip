@@ -1,0 +1,263 @@
+// swbank_multi.hip — multi-device banks: one child bank per device, the RCCL score gather.
+// 
+// SURVEY §8 e: pairs shard with no data-path collective; one ncclGather (rccl.h:745) over
+// communicators from ncclCommInitAll (rccl.h:236); librccl is dlopen-ed on first use.
+#include "swbank_bank.h"
+
+// RCCL for the multi-device score gather (SURVEY §8 e: ncclCommInitAll, rccl.h:236, and
+// ncclGather, rccl.h:745).  Loaded on first use so single-device users never map it; in a
+// process where PyTorch already mapped its librccl.so.1 that copy is reused (same SONAME).
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      snprintf(r.err, sizeof(r.err), "dlopen librccl.so.1: %s", dlerror());
+      return;
+    }
+    r.commInitAll = reinterpret_cast<decltype(&ncclCommInitAll)>(dlsym(h, "ncclCommInitAll"));
+    r.commDestroy = reinterpret_cast<decltype(&ncclCommDestroy)>(dlsym(h, "ncclCommDestroy"));
+    r.gather = reinterpret_cast<decltype(&ncclGather)>(dlsym(h, "ncclGather"));
+    r.errorString = reinterpret_cast<decltype(&ncclGetErrorString)>(dlsym(h, "ncclGetErrorString"));
+    r.commAbort = reinterpret_cast<decltype(&ncclCommAbort)>(dlsym(h, "ncclCommAbort"));
+    r.asyncError =
+        reinterpret_cast<decltype(&ncclCommGetAsyncError)>(dlsym(h, "ncclCommGetAsyncError"));
+    r.ok = r.commInitAll && r.commDestroy && r.gather && r.errorString && r.commAbort &&
+           r.asyncError;
+    if (!r.ok)
+      snprintf(r.err, sizeof(r.err),
+               "librccl.so.1 lacks ncclCommInitAll/ncclGather/ncclCommAbort/ncclCommGetAsyncError");
+  });
+  return r;
+}
+
+// ---- multi-device banks (≙ MODULES ScoringModules behind the PrioEncoder,
+//      ScoreBank_v2.v:76-148; SURVEY §8 e) ---------------------------------------------------
+// A batch is dealt over the child banks (phase 1: every device scores its share, scores stay on
+// the device), then gathered on the first device (phase 2: one ncclGather of equal, padded
+// counts over RCCL/xGMI, or device copies), copied back once and scattered to input order on
+// the host.  The collective is issued only after every share was accepted, so a bad input on
+// one device cannot leave the others blocked inside the gather.
+template <class FeedF>
+static sw_status multi_gather(sw_bank* b, const std::vector<size_t>& cnt, FeedF feed_kid) {
+  const size_t D = b->kids.size();
+  const size_t cmax = *std::max_element(cnt.begin(), cnt.end());
+  for (size_t d = 0; d < D; ++d) {  // padded send buffers, sized before any score lands
+    sw_bank* k = b->kids[d];
+    HIPOK(b, hipSetDevice(k->device));
+    HIPOK(b, k->scores.reserve(std::max<size_t>(cmax, 1)));
+  }
+  std::vector<sw_status> st(D, SW_OK);
+  b->dpool->run([&](unsigned d) {
+    sw_bank* k = b->kids[d];
+    if (hipSetDevice(k->device) != hipSuccess) st[d] = SW_ERR_HIP;
+    else if (cnt[d]) st[d] = feed_kid(d);
+  });
+  for (size_t d = 0; d < D; ++d)
+    if (st[d] != SW_OK) {
+      for (sw_bank* k : b->kids) {
+        (void)hipSetDevice(k->device);
+        (void)hipStreamSynchronize(k->stream);
+      }
+      (void)hipSetDevice(b->device);
+      return fail(b, st[d], "device %d: %s", b->kids[d]->device, b->kids[d]->err);
+    }
+  sw_bank* root = b->kids[0];
+  HIPOK(b, hipSetDevice(root->device));
+  HIPOK(b, b->grecv.reserve(D * cmax));
+  HIPOK(b, b->hrecv.reserve(D * cmax * 4));
+  const Rccl& r = rccl();
+  if (b->rccl_gather && b->comms.empty()) {  // re-created after an aborted gather
+    std::vector<ncclComm_t> comms(D);
+    std::vector<int> devs(D);
+    for (size_t d = 0; d < D; ++d) devs[d] = b->kids[d]->device;
+    const ncclResult_t nr = r.commInitAll(comms.data(), (int)D, devs.data());
+    if (nr != ncclSuccess)
+      return fail(b, SW_ERR_HIP, "ncclCommInitAll after an aborted gather: %s", r.errorString(nr));
+    b->comms.assign(comms.begin(), comms.end());
+    HIPOK(b, hipSetDevice(root->device));
+  }
+  if (!b->comms.empty()) {
+    // One host thread per device issues its ncclGather and then watches it: done, an async
+    // RCCL error, a failure on another device, or SWBANK_GATHER_TIMEOUT_MS (default 60 s)
+    // without completion.  Any of the latter aborts every communicator (ncclCommAbort ends the
+    // collective kernels still waiting for a peer), the call fails with SW_ERR_HIP, and the next
+    // call creates the communicators again, so a device that dropped out of one gather does not
+    // leave the others blocked or the bank unusable.  (SWBANK_GATHER_FAULT=d, tests: device d
+    // reports a failure instead of joining the gather.)
+    const int timeout_ms = std::max(1, env_int("SWBANK_GATHER_TIMEOUT_MS", 60000));
+    const int fault_dev = env_int("SWBANK_GATHER_FAULT", -1);
+    std::vector<int> nst(D, 0);  // 0 ok, > 0 ncclResult_t, -1 HIP, -2 timeout, -3 peer failed
+    std::atomic<bool> failed{false};
+    b->dpool->run([&](unsigned d) {
+      sw_bank* k = b->kids[d];
+      const ncclComm_t comm = static_cast<ncclComm_t>(b->comms[d]);
+      if (hipSetDevice(k->device) != hipSuccess || (int)d == fault_dev) {
+        nst[d] = -1;
+        failed = true;
+        return;
+      }
+      const ncclResult_t e = r.gather(k->scores.p, d == 0 ? b->grecv.p : nullptr, cmax, ncclInt32, 0,
+                                      comm, k->stream);
+      if (e != ncclSuccess) {
+        nst[d] = (int)e;
+        failed = true;
+        return;
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      for (unsigned it = 0;; ++it) {
+        const hipError_t q = hipStreamQuery(k->stream);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) {
+          nst[d] = -1;
+          break;
+        }
+        ncclResult_t ae = ncclSuccess;
+        if (r.asyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+          nst[d] = (int)ae;
+          break;
+        }
+        if (failed.load()) {
+          nst[d] = -3;
+          break;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
+          nst[d] = -2;
+          break;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(it < 1000 ? 20 : 500));
+      }
+      failed = true;
+    });
+    if (failed.load()) {
+      bool timed_out = false;
+      for (size_t d = 0; d < D; ++d) timed_out |= nst[d] == -2;
+      for (size_t d = 0; d < D; ++d) {
+        (void)hipSetDevice(b->kids[d]->device);
+        (void)r.commAbort(static_cast<ncclComm_t>(b->comms[d]));
+      }
+      b->comms.clear();
+      for (sw_bank* k : b->kids) {  // the aborted collectives have left the streams
+        (void)hipSetDevice(k->device);
+        (void)hipStreamSynchronize(k->stream);
+        (void)hipGetLastError();
+      }
+      (void)hipSetDevice(b->device);
+      if (timed_out) ++b->ctr.gather_timeouts;
+      size_t d0 = 0;
+      while (d0 + 1 < D && nst[d0] == 0) ++d0;
+      for (size_t d = 0; d < D; ++d)  // the first device that failed on its own, not by a peer
+        if (nst[d] != 0 && nst[d] != -3) {
+          d0 = d;
+          break;
+        }
+      return fail(b, SW_ERR_HIP, "ncclGather on device %d failed (%s); communicators aborted",
+                  b->kids[d0]->device,
+                  nst[d0] > 0    ? r.errorString((ncclResult_t)nst[d0])
+                  : nst[d0] == -2 ? "timed out (SWBANK_GATHER_TIMEOUT_MS)"
+                                  : "HIP or device fault");
+    }
+    HIPOK(b, hipSetDevice(root->device));
+  } else {
+    for (size_t d = 0; d < D; ++d) {
+      sw_bank* k = b->kids[d];
+      if (!cnt[d]) continue;
+      HIPOK(b, hipSetDevice(k->device));
+      HIPOK(b, hipMemcpyPeerAsync(b->grecv.p + d * cmax, root->device, k->scores.p, k->device,
+                                  cnt[d] * 4, k->stream));
+      HIPOK(b, hipStreamSynchronize(k->stream));
+    }
+    HIPOK(b, hipSetDevice(root->device));
+  }
+  HIPOK(b, hipMemcpyAsync(b->hrecv.p, b->grecv.p, D * cmax * 4, hipMemcpyDeviceToHost,
+                          root->stream));
+  HIPOK(b, hipStreamSynchronize(root->stream));
+  copy_kernel_name(b, b->comms.empty() ? "copy" : "rccl");
+  return SW_OK;
+}
+
+// The lowest index with the maximum score over scores[0, n), in parallel on the pool.
+static void host_best(sw_bank* b, const int32_t* scores, size_t n) {
+  const unsigned T = b->pool->size();
+  std::vector<size_t> pi(T, SIZE_MAX);
+  const size_t step = (n + T - 1) / T;
+  b->pool->run([&](unsigned p) {
+    const size_t lo = std::min(n, p * step), hi = std::min(n, lo + step);
+    size_t bi = lo;
+    for (size_t k = lo + 1; k < hi; ++k)
+      if (scores[k] > scores[bi]) bi = k;
+    if (lo < hi) pi[p] = bi;
+  });
+  size_t bi = SIZE_MAX;
+  for (size_t x : pi)
+    if (x != SIZE_MAX && (bi == SIZE_MAX || scores[x] > scores[bi])) bi = x;
+  b->best_index = bi;
+  b->best_id = bi;
+  b->best_score = scores[bi];
+  b->best_kind = 1;
+}
+
+sw_status multi_batch(sw_bank* b, const uint8_t* residues, size_t nres,
+                             const uint64_t* offsets, const uint32_t* lens, size_t n,
+                             int32_t* scores_out) {
+  const size_t D = b->kids.size();
+  // length-balanced deal (SURVEY §8 e): longest first, round robin -> each device gets every
+  // D-th target of the sorted order, itself already longest first (its feeder skips the sort)
+  std::vector<uint32_t> order(n);
+  if (!chunk_perm(*b->pool, lens, n, order.data())) std::iota(order.begin(), order.end(), 0u);
+  std::vector<size_t> cnt(D);
+  for (size_t d = 0; d < D; ++d) cnt[d] = n > d ? (n - d + D - 1) / D : 0;
+  std::vector<std::vector<uint64_t>> offs(D);
+  std::vector<std::vector<uint32_t>> lns(D), idx(D);
+  for (size_t d = 0; d < D; ++d) {
+    offs[d].resize(cnt[d]);
+    lns[d].resize(cnt[d]);
+    idx[d].resize(cnt[d]);
+  }
+  parallel_for(*b->pool, n, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      const uint32_t t = order[k];
+      const size_t d = k % D, i = k / D;
+      idx[d][i] = t;
+      offs[d][i] = offsets[t];
+      lns[d][i] = lens[t];
+    }
+  });
+  sw_status st = multi_gather(b, cnt, [&](unsigned d) {
+    return batch_feed(b->kids[d], residues, nres, offs[d].data(), lns[d].data(), cnt[d], nullptr);
+  });
+  if (st != SW_OK) return st;
+  const size_t cmax = cnt[0];
+  const int32_t* hr = reinterpret_cast<const int32_t*>(b->hrecv.p);
+  parallel_for(*b->pool, n, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      const size_t d = k % D, i = k / D;
+      scores_out[idx[d][i]] = hr[d * cmax + i];
+    }
+  });
+  host_best(b, scores_out, n);
+  return SW_OK;
+}
+
+sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_t* scores_out) {
+  // records are at most 232 bases: contiguous ranges (no copy of the 64-byte records)
+  const size_t D = b->kids.size();
+  std::vector<size_t> cnt(D), first(D);
+  for (size_t d = 0; d < D; ++d) {
+    first[d] = n * d / D;
+    cnt[d] = n * (d + 1) / D - first[d];
+  }
+  sw_status st = multi_gather(b, cnt, [&](unsigned d) {
+    return records_feed(b->kids[d], recs + first[d] * SWB_RECORD, cnt[d], nullptr);
+  });
+  if (st != SW_OK) return st;
+  const size_t cmax = *std::max_element(cnt.begin(), cnt.end());
+  const int32_t* hr = reinterpret_cast<const int32_t*>(b->hrecv.p);
+  for (size_t d = 0; d < D; ++d)
+    std::memcpy(scores_out + first[d], hr + d * cmax, cnt[d] * 4);
+  host_best(b, scores_out, n);
+  return SW_OK;
+}
+
