@@ -274,10 +274,11 @@ struct sw_bank {
   bool mq_ready = false;               // mqtab / mqtab16 match qset and the penalties
   DevBuf<uint32_t> mqtab, mqtab16;     // [query][the single-query LUT layout] (u16, f16)
   size_t mq_words = 0;                 // words per query
-  // letter-pair tables of a DNA merged f16 set: [128-row segment][query][mq_pair_words]
+  // letter-pair tables of a DNA merged f16 set: [segment][query][mq_pair_words], segments of
+  // mq_pair_rows rows (512: 16 waves of 32 rows, 4-column chunks; 128: 4 waves, 8 columns)
   DevBuf<uint32_t> mqpair;
   size_t mq_pair_words = 0;
-  int mq_pair_segs = 0;
+  int mq_pair_segs = 0, mq_pair_rows = 0;
   uint32_t mq_pS1 = 0, mq_pS2 = 0;
 
   // derived per (penalties, query)

@@ -704,13 +704,16 @@ sw_status prepare_multi(sw_bank* b) {
       }
     }
   }
-  // letter-pair tables (DNA merged f16 without the column-0 rule): 128-row segments (4 waves of
-  // 32 rows: the pair kernel's layout), one table per (segment, query)
+  // letter-pair tables (DNA merged f16 without the column-0 rule), one per (segment, query):
+  // 512-row segments (16 waves of 32 rows with 4-column chunks: a 1-kbp query is 2 segments,
+  // one bottom-row hand-off through HBM instead of 7 with 128-row segments) unless
+  // SWBANK_MQ_PAIR_ROWS=128 (4 waves, 8-column chunks, 4 workgroups per CU)
   std::vector<uint32_t> tp;
   b->mq_pair_segs = 0;
   if (b->f16 && !b->prof && !b->gotoh() && !b->col0 && A == SW_DNA_ALPHA &&
       env_int("SWBANK_MQ_PAIR", 1) != 0) {
-    const uint32_t NR = 128;
+    const uint32_t NR = env_int("SWBANK_MQ_PAIR_ROWS", 512) == 128 ? 128 : 512;
+    b->mq_pair_rows = (int)NR;
     pair_strides(NR, b->mq_pS1, b->mq_pS2);
     const int qmax = (int)b->query.size();
     b->mq_pair_segs = std::max(1, (qmax + (int)NR - 1) / (int)NR);

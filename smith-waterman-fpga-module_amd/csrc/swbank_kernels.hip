@@ -398,8 +398,57 @@ __device__ __forceinline__ uint32_t record_len(const uint8_t* rec) {
   return min((uint32_t)load_u<uint16_t>(rec + 4), SWB_RECORD_MAX);
 }
 
+// C = 4 (the 16-wave query-set kernel's 4-column chunks): codes [4c, 4c+4) in lo.x / hi.x.
+__device__ __forceinline__ uint32_t pad_tail4(uint32_t w, uint32_t j0, uint32_t len, uint32_t pad) {
+  const uint32_t n = len > j0 ? min(len - j0, 4u) : 0u;
+  const uint32_t keep = n >= 4 ? ~0u : ((1u << (8 * n)) - 1);
+  return (w & keep) | ((pad * 0x01010101u) & ~keep);
+}
+
+template <int C = 8>
 __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint32_t pad,
                                          uint32_t packed, uint2& lo, uint2& hi) {
+  static_assert(C == 8 || C == 4, "chunks of 8 or 4 columns");
+  if constexpr (C == 4) {
+    const uint32_t j0 = (uint32_t)c * 4;
+    uint32_t x, y;
+    if (packed == SWK_PACK_NIBBLE) {  // 2 bytes per 4 codes, chunk clamped to the target's last
+      const uint32_t cl = min((uint32_t)c, max((t.llo + 3) / 4, 1u) - 1);
+      const uint32_t ch = min((uint32_t)c, max((t.lhi + 3) / 4, 1u) - 1);
+      x = unpack8n(load_u<uint16_t>(t.plo + 2 * cl)).x;
+      y = unpack8n(load_u<uint16_t>(t.phi + 2 * ch)).x;
+    } else if (packed) {  // 1 byte per 4 codes (records: inside the data field)
+      uint32_t cl = (uint32_t)c, ch = (uint32_t)c;
+      if (packed == SWK_PACK_STREAM) {
+        cl = min(cl, max((t.llo + 3) / 4, 1u) - 1);
+        ch = min(ch, max((t.lhi + 3) / 4, 1u) - 1);
+      }
+      x = unpack8(t.plo[cl]).x;
+      y = unpack8(t.phi[ch]).x;
+    } else if (full) {
+      x = load_u<uint32_t>(t.plo + j0);
+      y = load_u<uint32_t>(t.phi + j0);
+    } else {
+      uint32_t b[2][4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // branch-free: clamped address, then select
+        const uint32_t j = j0 + k;
+        const uint32_t av = t.plo[j < t.llo ? j : 0];
+        const uint32_t hv = t.phi[j < t.lhi ? j : 0];
+        b[0][k] = j < t.llo ? av : pad;
+        b[1][k] = j < t.lhi ? hv : pad;
+      }
+      x = b[0][0] | b[0][1] << 8 | b[0][2] << 16 | b[0][3] << 24;
+      y = b[1][0] | b[1][1] << 8 | b[1][2] << 16 | b[1][3] << 24;
+    }
+    if (packed && !full) {
+      x = pad_tail4(x, j0, t.llo, pad);
+      y = pad_tail4(y, j0, t.lhi, pad);
+    }
+    lo = make_uint2(x, 0u);
+    hi = make_uint2(y, 0u);
+    return;
+  }
   const uint32_t j0 = (uint32_t)c * 8;
   if (packed == SWK_PACK_NIBBLE) {  // 4-bit stream, 4 bytes per 8 codes, clamped like below
     const uint32_t cl = min((uint32_t)c, max((t.llo + 7) / 8, 1u) - 1);
@@ -499,7 +548,8 @@ __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t
   return t;
 }
 
-// Chunk counts of a tile (uniform): nch = ceil(max len / 8) (>= 1), nfull = min len / 8.
+// Chunk counts of a tile (uniform): nch = ceil(max len / C) (>= 1), nfull = min len / C.
+template <int C = 8>
 __device__ __forceinline__ void tile_chunks(const Lane2& t, size_t tlo, size_t thi, size_t n,
                                             int& nch, int& nfull) {
   uint32_t Lmax = max(t.llo, t.lhi);
@@ -509,9 +559,9 @@ __device__ __forceinline__ void tile_chunks(const Lane2& t, size_t tlo, size_t t
     Lmax = max(Lmax, (uint32_t)__shfl_xor((int)Lmax, off));
     Lmin = min(Lmin, (uint32_t)__shfl_xor((int)Lmin, off));
   }
-  nch = max(1, (int)((__builtin_amdgcn_readfirstlane(Lmax) + 7) / 8));
+  nch = max(1, (int)((__builtin_amdgcn_readfirstlane(Lmax) + C - 1) / C));
   const uint32_t lm = __builtin_amdgcn_readfirstlane(Lmin);
-  nfull = lm == ~0u ? 0 : (int)(lm / 8);  // no valid lane (a tile past the end): no full loads
+  nfull = lm == ~0u ? 0 : (int)(lm / C);  // no valid lane (a tile past the end): no full loads
 }
 
 // Kernel arguments (one struct, passed by value).
@@ -596,16 +646,18 @@ static_assert(sizeof(ScoreArgs) == 296, "ScoreArgs layout (kernel argument block
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) void* glob_void_ptr;
 
-// 4 KB (8 columns x 64 lanes x uint2) global -> LDS by one wave: 4 LDS-DMA instructions of
-// 16 B per lane, lane-linear (the source layout is already [col][lane]).
+// C columns x 64 lanes x uint2 (4 KB for C = 8) global -> LDS by one wave: C / 2 LDS-DMA
+// instructions of 16 B per lane, lane-linear (the source layout is already [col][lane]).
+template <int C = 8>
 __device__ __forceinline__ void dma_edge_chunk(const uint2* src, uint2* dst, int lane) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < C / 2; ++q)
     __builtin_amdgcn_global_load_lds((glob_void_ptr)(src + q * 128 + lane * 2),
                                      (lds_void_ptr)(dst + q * 128), 16, 0, 0);
 }
 
 // Chunk count of a tile (uniform), from the lengths alone.
+template <int C = 8>
 __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens, size_t n,
                                         int tile, int lane, uint32_t packed, const uint32_t* idx,
                                         uint32_t ulen, uint32_t ustride) {
@@ -619,7 +671,7 @@ __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens
   uint32_t L = max(len(a), len(b));
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) L = max(L, (uint32_t)__shfl_xor((int)L, off));
-  return max(1, (int)((__builtin_amdgcn_readfirstlane(L) + 7) / 8));
+  return max(1, (int)((__builtin_amdgcn_readfirstlane(L) + C - 1) / C));
 }
 
 // Score kernel (persistent pipeline).  A workgroup of W waves x R rows holds the query (or
@@ -675,12 +727,14 @@ __device__ __forceinline__ uint32_t stream_mode(const uint32_t* hflag, uint32_t*
   return SWK_STREAM_ABORT;
 }
 
+// C: columns per chunk (one barrier per chunk); 4 for the 16-wave query-set pair kernel, whose
+// hand-off ring would not fit LDS beside a 512-row pair table at 8.
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
-          bool MQ = false, bool STREAM = false>
+          bool MQ = false, bool STREAM = false, int C = 8>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
   static_assert(!MQ || !PROF, "several queries: row-LUT or pair-table variants");
   static_assert(!STREAM || (!MQ && !PROF), "streamed batches: single-query LUT / pair variants");
-  constexpr int C = 8;
+  static_assert(C == 8 || (C == 4 && PAIR && MQ && !STREAM), "4-column chunks: MQ pair only");
   static_assert(!PAIR || (R == 32 && F16 && !PROF && !GOTOH && !COL0), "PAIR: f16 merged R=32");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
@@ -716,7 +770,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     total = (int)blockIdx.x < ntiles ? (1 << 30) : 0;
   } else {
     for (int u = blockIdx.x; u < nunits; u += G)  // (the unit's tile: see the MQ order below)
-      total += tile_nch(a.res, a.lens, n, !MQ ? u : PAIR ? u / (int)a.nq : u % ntiles, lane,
+      total += tile_nch<C>(a.res, a.lens, n, !MQ ? u : PAIR ? u / (int)a.nq : u % ntiles, lane,
                         packed, idx, a.ulen, a.ustride);
   }
   // STREAM: the chunk of this wave's current tile (tiles only grow), its first tile, target
@@ -787,7 +841,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen, a.ustride);
   }
   int nch, nfull;
-  tile_chunks(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
+  tile_chunks<C>(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
               nfull);
   const uint32_t S = a.S;
 
@@ -800,7 +854,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     bnd[lane] = F16 ? make_uint2(0u, GOTOH ? 0u : as_u32(as_u16x2(NOE2)))
                     : make_uint2(S | (S << 16), 0u);
     if (seg_in)  // the previous segment's bottom row of chunk 0
-      dma_edge_chunk(a.edge_in + (size_t)(MQ ? unit : tile) * a.ecols * 64, ein, lane);
+      dma_edge_chunk<C>(a.edge_in + (size_t)(MQ ? unit : tile) * a.ecols * 64, ein, lane);
   }
   uint32_t nv = a.nv;
   uint32_t tab[PROF || PAIR ? 1 : R];
@@ -840,7 +894,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   u16x2 best = {0, 0};
   u16x2 prevUpH = H0;  // H(row above, column -1)
   uint2 rlo, rhi;      // raw codes of the next chunk (prefetched one phase ahead)
-  load_raw(cur, 0, nfull > 0, a.pad, packed, rlo, rhi);
+  load_raw<C>(cur, 0, nfull > 0, a.pad, packed, rlo, rhi);
   if (STREAM && threadIdx.x == 0) sq[W] = total;
   __syncthreads();
 
@@ -930,20 +984,20 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         }
       }
       if (!last) {
-        load_raw(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
+        load_raw<C>(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
       } else if (nunit < nunits) {  // first chunk of the next tile
         if constexpr (STREAM) cur = stream_tile(ntile, packed_n);
         else
           cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed, idx, a.ulen,
                              a.ustride);
-        tile_chunks(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
+        tile_chunks<C>(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
                     n, nch_n, nfull_n);
-        load_raw(cur, 0, nfull_n > 0, a.pad, STREAM ? packed_n : packed, rlo, rhi);
+        load_raw<C>(cur, 0, nfull_n > 0, a.pad, STREAM ? packed_n : packed, rlo, rhi);
       }
       const int slot = g & 1;
       // next chunk's boundary row (never past the last unit's edge rows)
       if (seg_in && wave == 0 && (last ? nunit < nunits : (MQ ? unit : tile) < nunits))
-        dma_edge_chunk(a.edge_in + ((size_t)(last ? nunit : MQ ? unit : tile) * a.ecols +
+        dma_edge_chunk<C>(a.edge_in + ((size_t)(last ? nunit : MQ ? unit : tile) * a.ecols +
                                     (size_t)(last ? 0 : c + 1) * C) * 64,
                        ein + (size_t)((g + 1) & 1) * C * 64, lane);
       const uint2* rin = wave > 0 ? ring + ((size_t)((wave - 1) * 2 + slot) * C) * 64 + lane
@@ -1206,14 +1260,14 @@ static unsigned persistent_grid(const void* fn, size_t ntiles, int threads, size
 }
 
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
-          bool MQ = false, bool STREAM = false>
+          bool MQ = false, bool STREAM = false, int C = 8>
 static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st) {
   const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE * (MQ ? a.nq : 1);  // units
   const size_t lds = (size_t)W * SWB_TILE * 4 +
-                     (size_t)(64 + (a.edge_out ? 8 * 64 : 64) + (a.edge_in ? 2 * 8 * 64 : 0) +
-                              (W > 1 ? W - 1 : 0) * 2 * 8 * 64) * 8 +
+                     (size_t)(64 + (a.edge_out ? C * 64 : 64) + (a.edge_in ? 2 * C * 64 : 0) +
+                              (W > 1 ? W - 1 : 0) * 2 * C * 64) * 8 +
                      (PROF ? prof_bytes : 0) + (PAIR ? a.PS : 0) + (STREAM ? 256 : 0);
-  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR, MQ, STREAM>;
+  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR, MQ, STREAM, C>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -2082,6 +2136,9 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
   a.sstride = sstride;
   const uint32_t prof_bytes = (pad + 1) * PS;
   if (nq > 1 && pair) {  // several queries, pair tables (PS = one table's bytes)
+    // more than 4 waves (a 512-row table): 4-column chunks, so the ring fits beside the table
+    if (R == 32 && f16 && !prof && !gotoh && !col0 && W > 4)
+      return swk::launch_score<32, 4, false, false, false, true, true, true, false, 4>(a, W, 0, st);
     if (R == 32 && f16 && !prof && !gotoh && !col0)
       return swk::launch_score<32, 4, false, false, false, true, true, true>(a, W, 0, st);
     return hipErrorInvalidValue;

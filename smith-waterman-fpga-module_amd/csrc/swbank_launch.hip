@@ -354,13 +354,16 @@ static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_
   // pair tables (5.5 instead of 6.5 VALU per row) when the set has them, the batch is f16-exact
   // and a grid that is a multiple of nq (one query per workgroup) loses at most 1/8 of the
   // resident slots
-  const size_t slots = 4 * (size_t)std::max(b->cus, 1);
+  // (resident workgroups: 4 per CU for 128-row tables, 1 for the 16-wave 512-row ones)
+  const int prow = std::max(b->mq_pair_rows, 32);
+  const size_t slots = (prow > 128 ? 1 : 4) * (size_t)std::max(b->cus, 1);
   const bool mpair = b->mq_pair_segs > 0 && use_f16 && nq <= slots &&
                      8 * (slots - slots / nq * nq) <= slots;
   const size_t nseg = mpair ? (size_t)b->mq_pair_segs : b->segs.size();
   snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=%zu queries=%zu",
            use_f16 ? "f16" : "u16", mpair ? " pair" : "", b->R,
-           mpair ? std::min(4, (int)(b->query.size() + 31) / 32) : b->segs[0].W, nseg, nq);
+           mpair ? std::min(prow / 32, (int)(b->query.size() + 31) / 32) : b->segs[0].W, nseg,
+           nq);
   HIPOK(b, hipStreamWaitEvent(st, b->ev_ready, 0));  // the query tables are uploaded
   HIPOK(b, hipStreamWaitEvent(st, b->ev_used, 0));   // bank scratch is free
   sw_bank::Ev ev{};
@@ -408,8 +411,8 @@ static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_
     for (size_t sg = 0; sg < nseg; ++sg) {
       const void* ein = sg > 0 ? b->edge[(sg - 1) & 1].p : nullptr;
       void* eout = sg + 1 < nseg ? b->edge[sg & 1].p : nullptr;
-      if (mpair) {  // 128-row segments, 4 waves of 32 rows (fewer for a short last one)
-        const int rows = std::min(128, (int)b->query.size() - (int)sg * 128);
+      if (mpair) {  // prow-row segments, waves of 32 rows (fewer for a short last one)
+        const int rows = std::min(prow, (int)b->query.size() - (int)sg * prow);
         const int Wp = std::max(1, (rows + 31) / 32);
         HIPOK(b, swk_launch_score(32, 4, 0, 0, 0, 1, d_res, offs, lens, np,
                                   b->mqpair.p + sg * nq * b->mq_pair_words, b->nv16, b->S, b->O,

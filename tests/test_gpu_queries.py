@@ -162,14 +162,17 @@ def test_query_set_api_rules():
     assert np.array_equal(got, O.score_batch(queries[1], res, offs, lens, O.dna_matrix(), -12, -4))
 
 
+@pytest.mark.parametrize("rows", [512, 128])
 @pytest.mark.parametrize("nq", [2, 5, 16, 33])
-def test_query_set_pair_tables(monkeypatch, nq):
-    """DNA merged f16 sets run on letter-pair tables in 128-row segments, one query per
-    workgroup (the grid a multiple of nq): equal to the row-LUT variant (SWBANK_MQ_PAIR=0) and
-    the oracle, for set sizes that do and do not divide the resident slots."""
+def test_query_set_pair_tables(monkeypatch, nq, rows):
+    """DNA merged f16 sets run on letter-pair tables, one query per workgroup (the grid a
+    multiple of nq): 512-row segments (16 waves, 4-column chunks; the default) or 128-row ones
+    (4 waves, 8-column chunks), equal to the row-LUT variant (SWBANK_MQ_PAIR=0) and the oracle,
+    for set sizes that do and do not divide the resident slots, queries of 1-3 segments."""
     monkeypatch.setenv("SWBANK_KERNEL", "tile")
+    monkeypatch.setenv("SWBANK_MQ_PAIR_ROWS", str(rows))
     rng = np.random.default_rng(nq)
-    queries = [rng.integers(0, 4, int(rng.integers(60, 700)), dtype=np.uint8) for _ in range(nq)]
+    queries = [rng.integers(0, 4, int(rng.integers(60, 1100)), dtype=np.uint8) for _ in range(nq)]
     seqs = _targets(rng, 900, 0, 150, 4, queries, p_n=0.01)
     with S.ScoreBank() as bank:
         bank.set_penalties(5, -4, -12, -4)
@@ -177,6 +180,7 @@ def test_query_set_pair_tables(monkeypatch, nq):
         got = _score_set(bank, queries, seqs)
         kern = bank.last_kernel()
         assert " pair " in kern and f"queries={nq}" in kern, kern
+        assert f" W={min(rows, max(len(q) for q in queries) + 31) // 32} " in kern, kern
         monkeypatch.setenv("SWBANK_MQ_PAIR", "0")
         bank.load_queries(queries)  # the tables are rebuilt without pair tables
         lut = _score_set(bank, queries, seqs)
