@@ -47,7 +47,7 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
                                       int packed, const uint32_t* fb_qtab, uint32_t fb_nv,
                                       uint32_t fb_PS, int32_t fb_thresh,
                                       const SwkWaveSplit* split, uint32_t ulen,
-                                      uint32_t ustride, hipStream_t st);
+                                      uint32_t ustride, int half, hipStream_t st);
 extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int gotoh, int f16,
                                        const uint8_t* res, const uint64_t* offs,
                                        const uint32_t* lens, size_t n, const uint32_t* qtab,

@@ -2085,6 +2085,210 @@ static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream
   return hipGetLastError();
 }
 
+// Two pairs per wave (f16 profile, one query segment of <= 512 rows: configs[4]'s protein
+// shape).  Lanes 0-31 score pair p0, lanes 32-63 pair p0 + 1, lane l owning rows
+// [16 (l % 32), 16 (l % 32) + 16) of the same 512-row profile as the one-pair kernel's K = 8
+// layout (32 B per lane per letter).  Against one pair per wave at 8 rows per lane:
+// * the per-step work besides the column (two DPP moves of the bottom row, two profile
+//   addresses, the ring letters) is shared by 16 rows instead of 8;
+// * the lane pipeline is 32 deep: a pair's fill and drain skew is 31 steps, not 63;
+// * each half's lane 0 takes the row -1 boundary (lane 32 would otherwise read lane 31's
+//   bottom row through wave_shr): one v_cndmask per moved value.
+// Each half keeps its own 128-byte code ring (targets A, B: [previous 32 | next 32] columns).
+// Returns the half's two bests (every lane of the half).
+template <bool GOTOH>
+__device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_t* prof,
+                                                uint8_t* cring, int lane, size_t p0) {
+  constexpr int K = 16;
+  const int h = lane >> 5, hl = lane & 31;
+  const size_t pair = p0 + (size_t)h;
+  const size_t n = a.n;
+  const bool have = pair < a.main_pairs;
+  const size_t tA = 2 * pair, tB = tA + 1;
+  const bool packed = a.packed != SWK_PACK_BYTES, rec = a.packed == SWK_PACK_RECORDS;
+  const bool nib = a.packed == SWK_PACK_NIBBLE;
+  const bool uni = a.ustride != 0;
+  uint32_t LA = 0, LB = 0;
+  const uint8_t* pA = a.res;
+  const uint8_t* pB = a.res;
+  if (have) {
+    LA = rec ? record_len(a.res + tA * SWB_RECORD) : uni ? a.ulen : a.lens[tA];
+    LB = tB >= n ? 0u : rec ? record_len(a.res + tB * SWB_RECORD) : uni ? a.ulen : a.lens[tB];
+    pA = rec ? a.res + tA * SWB_RECORD + 6 : uni ? a.res + tA * a.ustride
+                                                 : a.res + (LA ? a.offs[tA] : 0);
+    const size_t tb = tB < n ? tB : tA;
+    pB = rec ? a.res + tb * SWB_RECORD + 6 : uni ? a.res + tb * a.ustride
+                                                 : a.res + (LB ? a.offs[tB] : 0);
+  }
+  uint32_t Lh = max(LA, LB);
+  Lh = max(Lh, (uint32_t)__shfl_xor((int)Lh, 32));
+  const int Lmax = (int)__builtin_amdgcn_readfirstlane(Lh);
+  const uint32_t pad = a.pad, PSb = a.PS;
+  const f16x2 NOE2 = as_f16x2(as_u16x2(a.f16_noe)), NE2 = as_f16x2(as_u16x2(a.f16_ne)),
+              NO2 = as_f16x2(as_u16x2(a.f16_no));
+  const uint32_t noe = as_u32(as_u16x2(NOE2)), ne = as_u32(as_u16x2(NE2)),
+                 no = as_u32(as_u16x2(NO2));
+  (void)NO2;
+  const u16x2 H0 = {0, 0};
+  const u16x2 X0 = GOTOH ? (u16x2){0, 0} : as_u16x2(NOE2);  // F / T of row -1
+  u16x2 Hl[K], Xl[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    Hl[k] = H0;
+    Xl[k] = X0;
+  }
+  u16x2 best = {0, 0}, prevUpH = H0;
+  uint32_t botH = as_u32(H0), botX = as_u32(X0);
+  const bool top = hl == 0;  // row -1 of this half's pair
+  // the codes of column c of this half's targets (pad past the end) as {A, B << 8}
+  const auto load_codes = [&](const uint32_t c) __attribute__((always_inline)) -> uint32_t {
+    uint32_t x = pad, y = pad;
+    if (nib) {
+      if (c < LA) x = (pA[c >> 1] >> (4 * (c & 1))) & 15u;
+      if (c < LB) y = (pB[c >> 1] >> (4 * (c & 1))) & 15u;
+    } else if (packed) {
+      if (c < LA) x = (pA[c >> 2] >> (2 * (c & 3))) & 3u;
+      if (c < LB) y = (pB[c >> 2] >> (2 * (c & 3))) & 3u;
+    } else {
+      if (c < LA) x = pA[c];
+      if (c < LB) y = pB[c];
+    }
+    return min(x, pad) | (min(y, pad) << 8);
+  };
+  // ring entries are 32-bit profile offsets (letter x PSb): a byte entry read in one step and
+  // used in the next would be masked again in every basic block it crosses
+  uint32_t* ring = reinterpret_cast<uint32_t*>(cring) + 128 * h;
+  const uint32_t* ring_l = ring + 32 - hl;  // step T + j reads ring_l[j] (A), ring_l[64 + j] (B)
+  uint32_t ringprev = pad | pad << 8;
+  const auto ring_write = [&](const uint32_t nc) __attribute__((always_inline)) {
+    ring[hl] = __umul24(ringprev & 0xFFu, PSb);
+    ring[32 + hl] = __umul24(nc & 0xFFu, PSb);
+    ring[64 + hl] = __umul24(ringprev >> 8, PSb);
+    ring[96 + hl] = __umul24(nc >> 8, PSb);
+    ringprev = nc;
+  };
+  ring_write(load_codes((uint32_t)hl));
+  uint32_t ncode = load_codes(32u + hl);  // the next block's codes, one block ahead
+  uint32_t nra = ring_l[0], nrb = ring_l[64];
+  const uint8_t* plds = prof + hl * 2 * K;
+  const auto step = [&](const int t, const bool even) __attribute__((always_inline)) {
+    if (!even && (t & 31) == 31) {  // the next 32 columns go in before step t + 1 reads them
+      ring_write(ncode);
+      // (t through an opaque copy: no per-step pointer increments for these loads)
+      uint32_t tt = (uint32_t)t;
+      asm volatile("" : "+s"(tt));
+      ncode = load_codes(tt + 33 + hl);
+    }
+    u16x2 upH = as_u16x2(dpp_shr1_zero(botH));
+    u16x2 upX = as_u16x2(GOTOH ? dpp_shr1_zero(botX) : dpp_shr1(as_u32(X0), botX));
+    upH = top ? H0 : upH;
+    upX = top ? X0 : upX;
+    const uint32_t rca = nra, rcb = nrb;
+    u16x2 diag = prevUpH;
+    prevUpH = upH;
+    __builtin_amdgcn_sched_barrier(0);
+    ProfLookupK16<K> lk;
+    const uint8_t* la = plds + rca;
+    const uint8_t* lb = plds + rcb;
+#pragma unroll
+    for (int q = 0; q < K / 8; ++q) {
+      const uint4 x = reinterpret_cast<const uint4*>(la)[q];
+      const uint4 y = reinterpret_cast<const uint4*>(lb)[q];
+      lk.lo[4 * q] = x.x; lk.lo[4 * q + 1] = x.y; lk.lo[4 * q + 2] = x.z; lk.lo[4 * q + 3] = x.w;
+      lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z; lk.hi[4 * q + 3] = y.w;
+    }
+    const uint32_t* np = ring_l + ((t + 1) & 31);  // the next step's profile offsets
+    nra = np[0];
+    nrb = np[64];
+    column_f16_lane_asm<K, GOTOH>(lk, diag, upX, Hl, Xl, best, noe, ne, no);
+    asm volatile("" : "+v"(best));
+    botH = as_u32(Hl[K - 1]);
+    botX = as_u32(upX);
+  };
+  const int nsteps = Lmax + 31;
+  for (int t = 0; t < nsteps; t += 2) {
+    step(t, true);
+    step(t + 1, false);
+  }
+  uint32_t bx = (uint32_t)f16_unscore(best.x), by = (uint32_t)f16_unscore(best.y);
+#pragma unroll
+  for (int off = 16; off >= 1; off >>= 1) {  // within the half
+    bx = max(bx, (uint32_t)__shfl_xor((int)bx, off));
+    by = max(by, (uint32_t)__shfl_xor((int)by, off));
+  }
+  return make_uint2(bx, by);
+}
+
+// configs[4]'s kernel: the wave kernel's split tail (blocks [0, split_blocks), as in
+// score_wave<8>) and main blocks of 4 waves scoring two pairs each (wave_two_pairs).  A pair
+// above the optimistic f16 threshold is re-scored in u16 by the whole wave with the one-pair
+// K = 8 code and table (rare).
+template <bool GOTOH>
+__global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
+  const int lane = threadIdx.x & 63;
+  if (blockIdx.x < a.split_blocks) {  // block-uniform
+    if (a.split_P == 4) wave_split_block<2, 4, false, true, GOTOH, true>(a, smem, lane);
+    else wave_split_block<4, 2, false, true, GOTOH, true>(a, smem, lane);
+    return;
+  }
+  {
+    const uint32_t words = (a.pad + 1) * a.PS / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+      reinterpret_cast<uint4*>(prof)[i] = src[i];
+    __syncthreads();
+  }
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t p0 = 2 * ((size_t)(blockIdx.x - a.split_blocks) * (blockDim.x >> 6) + wave);
+  const size_t n = a.n;
+  if (p0 >= a.main_pairs || 2 * p0 >= n) return;  // whole wave
+  uint8_t* cring = prof + (a.pad + 1) * a.PS + 1024 * wave;
+  uint2 b = wave_two_pairs<GOTOH>(a, prof, cring, lane, p0);
+  if (a.fb_qtab) {  // optimistic f16: re-score a flagged pair in u16 (whole wave, K = 8)
+    const uint32_t m0 = __builtin_amdgcn_readlane(max(b.x, b.y), 0);
+    const uint32_t m1 = __builtin_amdgcn_readlane(max(b.x, b.y), 32);
+    const uint8_t* fp = reinterpret_cast<const uint8_t*>(a.fb_qtab);
+    uint2 f0 = make_uint2(0u, 0u), f1 = make_uint2(0u, 0u);
+    if ((int32_t)m0 > a.fb_thresh)
+      f0 = wave_pair<8, false, true, GOTOH, false>(a, fp, a.fb_qtab, a.fb_nv, a.fb_PS, p0, lane);
+    if ((int32_t)m1 > a.fb_thresh && p0 + 1 < a.main_pairs)
+      f1 = wave_pair<8, false, true, GOTOH, false>(a, fp, a.fb_qtab, a.fb_nv, a.fb_PS, p0 + 1,
+                                                   lane);
+    if ((int32_t)m0 > a.fb_thresh && lane < 32) b = f0;
+    if ((int32_t)m1 > a.fb_thresh && lane >= 32) b = f1;
+  }
+  if ((lane & 31) == 0) {
+    const size_t pair = p0 + (size_t)(lane >> 5);
+    const size_t tA = 2 * pair, tB = tA + 1;
+    if (pair < a.main_pairs && tA < n) {
+      a.scores[tA] = (int32_t)b.x;
+      if (tB < n) a.scores[tB] = (int32_t)b.y;
+    }
+  }
+}
+
+template <bool GOTOH>
+static hipError_t launch_wave_half(const ScoreArgs& a, uint32_t prof_bytes, hipStream_t st) {
+  // 4 waves per block = 8 pairs, sharing one LDS copy of the profile; the split tail's blocks
+  // hold every segment's profile
+  const size_t blocks = a.split_blocks + ((size_t)a.main_pairs + 7) / 8;
+  size_t lds = (size_t)prof_bytes + 1024 * 4;  // + each wave's code rings (2 x 128 u32)
+  if (a.split_blocks) lds = std::max<size_t>(lds, (size_t)a.split_words * 4 * a.split_P);
+  auto fn = &score_wave_half<GOTOH>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(256), (unsigned)lds, st, a);
+  return hipGetLastError();
+}
+
 }  // namespace swk
 
 // Variants compiled in: (R, RB, COL0, PROF, GOTOH, F16).  The host picks R from the query
@@ -2302,7 +2506,7 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
                                       int packed, const uint32_t* fb_qtab, uint32_t fb_nv,
                                       uint32_t fb_PS, int32_t fb_thresh,
                                       const SwkWaveSplit* split, uint32_t ulen,
-                                      uint32_t ustride, hipStream_t st) {
+                                      uint32_t ustride, int half, hipStream_t st) {
   if (n == 0) return hipSuccess;
   swk::ScoreArgs a{res, offs, lens, n, qtab, nv, S, O, E, PS, pad, scores,
                    static_cast<const uint2*>(edge_in), static_cast<uint2*>(edge_out), ecols,
@@ -2331,6 +2535,13 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
     a.split_ring = static_cast<uint2*>(split->ring);
   }
   const uint32_t prof_bytes = (pad + 1) * PS;
+  // two pairs per wave: f16 profile, K = 8 tables (a <= 512-row query), one segment
+  if (half) {
+    if (K != 8 || col0 || !prof || !f16 || edge_in || edge_out || accum)
+      return hipErrorInvalidValue;
+    return gotoh ? swk::launch_wave_half<true>(a, prof_bytes, st)
+                 : swk::launch_wave_half<false>(a, prof_bytes, st);
+  }
 #define SWK_WCASE(KK, C0, PF, GT)                                                         \
   if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                                 \
     return f16 ? swk::launch_wave<KK, (C0 != 0), (PF != 0), (GT != 0), true>(a, prof_bytes, st) \

@@ -107,8 +107,12 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   const bool use_pair = use_f16 && b->pair_bytes != 0 && env_int("SWBANK_PAIR", 1) != 0;
   bool wave_fb = false;  // the wave kernel re-scores its own flagged pairs
   if (use_wave) {
-    snprintf(b->last_kernel, sizeof(b->last_kernel), "wave %s%s K=%d segs=%d", arith,
-             b->prof ? "-profile" : "", b->wK, b->wsegs);
+    // f16 profile, one segment of <= 512 rows (configs[4]): two pairs per wave, 16 rows per
+    // lane (swk wave_two_pairs); SWBANK_WAVE_HALF=0 keeps one pair per wave
+    const bool half = use_f16 && b->prof && !b->col0 && b->wK == 8 && b->wsegs == 1 &&
+                      env_int("SWBANK_WAVE_HALF", 1) != 0 && env_int("SWBANK_WAVE_BLOCK", 4) == 4;
+    snprintf(b->last_kernel, sizeof(b->last_kernel), "wave %s%s K=%d segs=%d%s", arith,
+             b->prof ? "-profile" : "", b->wK, b->wsegs, half ? " pairs/wave=2" : "");
     // segments hand the bottom row on through HBM: pairs x ecols x 8 B per edge buffer,
     // in position ranges under SWBANK_EDGE_MB like the tile kernel
     size_t wspan = n;
@@ -134,9 +138,10 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
     if (b->sK[0] && b->wsegs == 1 && n == wspan && env_int("SWBANK_WAVE_BLOCK", 4) == 4 &&
         pairs <= 0xFFFFFFFFull) {
       const size_t simds = 4 * (size_t)std::max(b->cus, 1);
+      const size_t units = half ? 2 * simds : simds;  // pairs per layer of one wave per SIMD
       size_t T = 0;
       if (sforce >= 0) T = std::min(pairs, (size_t)sforce);
-      else if (pairs >= simds && pairs % simds <= simds / 2) T = pairs % simds;
+      else if (pairs >= units && pairs % units <= units / 2) T = pairs % units;
       const int pforce = env_int("SWBANK_WAVE_SPLIT_P", 0);
       const int i = pforce == 2 ? 0 : pforce == 4 ? 1 : (4 * T <= simds ? 1 : 0);
       if (T && b->sK[i]) {
@@ -168,7 +173,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                      use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
                      use_f16 && b->prof ? b->wPS16 : b->wPS, b->pad, d_scores + p0,
                      (int)packed, wave_fb ? b->wtab.p : nullptr, b->nv, b->wPS,
-                     2048 - std::max(0, b->smax), &sp, ulen, ustride, st));
+                     2048 - std::max(0, b->smax), &sp, ulen, ustride, half ? 1 : 0, st));
       }
     }
   } else {

@@ -53,9 +53,9 @@ def test_bench_two_ranks_gathered_parity(workload):
 def test_bench_workloads_one_gpu(workload):
     """Every bench workload the driver does not run itself, at reduced size: configs[3] (the
     query-set path, 4 x 1-kbp queries) and configs[4] (protein, the wave kernel with its split
-    tail: 2,500 targets = 1,250 pairs, 226 past one wave per SIMD)."""
+    tail: 4,300 targets = 2,150 pairs, 102 past two pairs per SIMD)."""
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
-           "--reps", "64", "--reads", "8192", "--slice", "4", "--ptargets", "2500",
+           "--reps", "64", "--reads", "8192", "--slice", "4", "--ptargets", "4300",
            "--cpu-seconds", "0", "--workload", workload]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]

@@ -104,16 +104,18 @@ def test_split_records(monkeypatch):
 
 
 def test_split_auto_policy(arith):
-    """Without the override a batch of SIMDs x k + r pairs (r <= SIMDs / 2) splits its last r
-    pairs; the scores match the unsplit run (SWBANK_WAVE_SPLIT=0) and a sample of them the
-    oracle."""
+    """Without the override a batch of U x k + r pairs (r <= U / 2) splits its last r pairs,
+    U = the pairs of one wave per SIMD: SIMDs, or 2 x SIMDs for the f16 profile kernel's two
+    pairs per wave; the scores match the unsplit run (SWBANK_WAVE_SPLIT=0) and a sample of
+    them the oracle."""
     import os
 
     import torch
     simds = 4 * torch.cuda.get_device_properties(0).multi_processor_count
     rng = np.random.default_rng(99)
     q = rng.integers(0, 20, 512, dtype=np.uint8)
-    n = 2 * (simds + 37)
+    units = 2 * simds if arith.startswith("f16") else simds
+    n = 2 * (units + 37)
     seqs = [rng.integers(0, 20, 120, dtype=np.uint8) for _ in range(n)]
     with S.ScoreBank(alphabet=S.ALPHABET_PROTEIN, gap_model=S.GAP_GOTOH) as bank:
         bank.set_matrix(O.BLOSUM62, -11, -1)
