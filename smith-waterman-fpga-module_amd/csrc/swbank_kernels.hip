@@ -1383,6 +1383,9 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
 #ifndef SWK_UNIFORM_PTR
 #define SWK_UNIFORM_PTR 0  // target pointers in SGPRs
 #endif
+#ifndef SWK_HALF_AHEAD
+#define SWK_HALF_AHEAD 1  // two-pairs wave kernel: profile words one step ahead
+#endif
 #ifndef SWK_PROF_AHEAD
 // wave kernel, f16 profile (with SWK_RING_PF): a step's profile words are loaded during the
 // step before (the letters two steps ahead), so no step waits on its own LDS reads
@@ -2169,27 +2172,11 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   };
   ring_write(load_codes((uint32_t)hl));
   uint32_t ncode = load_codes(32u + hl);  // the next block's codes, one block ahead
-  uint32_t nra = ring_l[0], nrb = ring_l[64];
   const uint8_t* plds = prof + hl * 2 * K;
-  const auto step = [&](const int t, const bool even) __attribute__((always_inline)) {
-    if (!even && (t & 31) == 31) {  // the next 32 columns go in before step t + 1 reads them
-      ring_write(ncode);
-      // (t through an opaque copy: no per-step pointer increments for these loads)
-      uint32_t tt = (uint32_t)t;
-      asm volatile("" : "+s"(tt));
-      ncode = load_codes(tt + 33 + hl);
-    }
-    u16x2 upH = as_u16x2(dpp_shr1_zero(botH));
-    u16x2 upX = as_u16x2(GOTOH ? dpp_shr1_zero(botX) : dpp_shr1(as_u32(X0), botX));
-    upH = top ? H0 : upH;
-    upX = top ? X0 : upX;
-    const uint32_t rca = nra, rcb = nrb;
-    u16x2 diag = prevUpH;
-    prevUpH = upH;
-    __builtin_amdgcn_sched_barrier(0);
-    ProfLookupK16<K> lk;
-    const uint8_t* la = plds + rca;
-    const uint8_t* lb = plds + rcb;
+  const auto load_prof = [&](ProfLookupK16<K>& lk, uint32_t oa, uint32_t ob)
+      __attribute__((always_inline)) {
+    const uint8_t* la = plds + oa;
+    const uint8_t* lb = plds + ob;
 #pragma unroll
     for (int q = 0; q < K / 8; ++q) {
       const uint4 x = reinterpret_cast<const uint4*>(la)[q];
@@ -2197,9 +2184,52 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
       lk.lo[4 * q] = x.x; lk.lo[4 * q + 1] = x.y; lk.lo[4 * q + 2] = x.z; lk.lo[4 * q + 3] = x.w;
       lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z; lk.hi[4 * q + 3] = y.w;
     }
-    const uint32_t* np = ring_l + ((t + 1) & 31);  // the next step's profile offsets
-    nra = np[0];
-    nrb = np[64];
+  };
+  // AHEAD: a step's profile words are loaded during the step before (its ring entries two
+  // steps before), so no step waits on its own LDS reads: with 3-4 waves per SIMD the other
+  // waves hide less of that latency than the one-pair kernel's 6
+  constexpr bool AHEAD = SWK_HALF_AHEAD != 0;
+  ProfLookupK16<K> lkn;
+  uint32_t nra, nrb;
+  if constexpr (AHEAD) {
+    load_prof(lkn, ring_l[0], ring_l[64]);
+    nra = ring_l[1];
+    nrb = ring_l[65];
+  } else {
+    nra = ring_l[0];
+    nrb = ring_l[64];
+  }
+  const auto step = [&](const int t, const bool even) __attribute__((always_inline)) {
+    // the next 32 columns go in before they are read (AHEAD: two steps before)
+    if ((AHEAD ? even : !even) && (t & 31) == (AHEAD ? 30 : 31)) {
+      ring_write(ncode);
+      // (t through an opaque copy: no per-step pointer increments for these loads)
+      uint32_t tt = (uint32_t)t;
+      asm volatile("" : "+s"(tt));
+      ncode = load_codes(tt + (AHEAD ? 34u : 33u) + hl);
+    }
+    ProfLookupK16<K> lk;
+    if constexpr (AHEAD) {
+      lk = lkn;
+      load_prof(lkn, nra, nrb);
+      const uint32_t* np = ring_l + ((t + 2) & 31);
+      nra = np[0];
+      nrb = np[64];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    u16x2 upH = as_u16x2(dpp_shr1_zero(botH));
+    u16x2 upX = as_u16x2(GOTOH ? dpp_shr1_zero(botX) : dpp_shr1(as_u32(X0), botX));
+    upH = top ? H0 : upH;
+    upX = top ? X0 : upX;
+    u16x2 diag = prevUpH;
+    prevUpH = upH;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!AHEAD) {
+      load_prof(lk, nra, nrb);
+      const uint32_t* np = ring_l + ((t + 1) & 31);  // the next step's profile offsets
+      nra = np[0];
+      nrb = np[64];
+    }
     column_f16_lane_asm<K, GOTOH>(lk, diag, upX, Hl, Xl, best, noe, ne, no);
     asm volatile("" : "+v"(best));
     botH = as_u32(Hl[K - 1]);
