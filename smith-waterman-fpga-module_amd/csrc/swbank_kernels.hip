@@ -2172,15 +2172,17 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   };
   ring_write(load_codes((uint32_t)hl));
   uint32_t ncode = load_codes(32u + hl);  // the next block's codes, one block ahead
-  const uint8_t* plds = prof + hl * 2 * K;
+  // score_wave_half's LDS copy of the profile keeps each letter's rows 8-15 of every lane 512
+  // bytes after its rows 0-7: a ds_read_b128 of 16 lanes then covers all 64 banks
+  const uint8_t* plds = prof + hl * 16;
   const auto load_prof = [&](ProfLookupK16<K>& lk, uint32_t oa, uint32_t ob)
       __attribute__((always_inline)) {
     const uint8_t* la = plds + oa;
     const uint8_t* lb = plds + ob;
 #pragma unroll
     for (int q = 0; q < K / 8; ++q) {
-      const uint4 x = reinterpret_cast<const uint4*>(la)[q];
-      const uint4 y = reinterpret_cast<const uint4*>(lb)[q];
+      const uint4 x = *reinterpret_cast<const uint4*>(la + 512 * q);
+      const uint4 y = *reinterpret_cast<const uint4*>(lb + 512 * q);
       lk.lo[4 * q] = x.x; lk.lo[4 * q + 1] = x.y; lk.lo[4 * q + 2] = x.z; lk.lo[4 * q + 3] = x.w;
       lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z; lk.hi[4 * q + 3] = y.w;
     }
@@ -2263,11 +2265,12 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
     else wave_split_block<4, 2, false, true, GOTOH, true>(a, smem, lane);
     return;
   }
-  {
+  {  // the K = 8 profile (64 16-byte row groups per letter, PS = 1024) with group 2l + q at
+     // 32 q + l: lane l of a half reads its rows 16 l .. 16 l + 15 as 16 + 16 bytes, 512 apart
     const uint32_t words = (a.pad + 1) * a.PS / 16;
     const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
     for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
-      reinterpret_cast<uint4*>(prof)[i] = src[i];
+      reinterpret_cast<uint4*>(prof)[(i & ~63u) | (i & 1u) << 5 | (i & 63u) >> 1] = src[i];
     __syncthreads();
   }
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2567,7 +2570,7 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
   const uint32_t prof_bytes = (pad + 1) * PS;
   // two pairs per wave: f16 profile, K = 8 tables (a <= 512-row query), one segment
   if (half) {
-    if (K != 8 || col0 || !prof || !f16 || edge_in || edge_out || accum)
+    if (K != 8 || PS != 1024 || col0 || !prof || !f16 || edge_in || edge_out || accum)
       return hipErrorInvalidValue;
     return gotoh ? swk::launch_wave_half<true>(a, prof_bytes, st)
                  : swk::launch_wave_half<false>(a, prof_bytes, st);
