@@ -89,12 +89,15 @@ def merged_block(mode, zdown, last, nrows=8):
 
 
 def gotoh_block(mode, last, nrows=8):
+    """mode "L"/"P": perm lookups into S1; "pair": ready-made words p{i} (no lookup)."""
     out = []
     for i in range(nrows):
         dcur, dnext = ("%[Da]", "%[Db]") if i % 2 == 0 else ("%[Db]", "%[Da]")
         final = last and i == nrows - 1
         if final:
             out.append("s_nop 0")
+        elif mode == "pair":
+            out.append(f"v_pk_add_f16 {dnext}, %[h{i}], %[p{i}]")
         else:
             out.append(perm(mode, i))
             out.append(f"v_pk_add_f16 {dnext}, %[h{i}], %[S1]")
@@ -116,6 +119,15 @@ def pair_block(first, last, nrows=8):
     in and of the next block's first row out; the first block computes it from dg + pw."""
     out = ["v_pk_add_f16 %[Da], %[dg], %[pw] clamp"] if first else []
     return out + merged_block("pair", False, last, nrows)
+
+def pair_gotoh_block(first, last, nrows=8):
+    """Pair-profile block, Gotoh (DNA): as gotoh_block with the substitution words p{i} from
+    the letter-pair table, 7.5 VALU per 2 cells instead of 8.5.  F runs down the column in
+    %[F]; the first block computes row 0's D from dg + pw (the clamp is harmless: H is the max
+    of D and the floored E, F)."""
+    out = ["v_pk_add_f16 %[Da], %[dg], %[pw] clamp"] if first else []
+    return out + gotoh_block("pair", last, nrows)
+
 
 def fmt(lines):
     return "".join(f'  "{ln}\\n\\t" \\\n' for ln in lines) + '  ""\n'
@@ -145,6 +157,9 @@ def main():
     parts.append("#define SWK_F16PAIR_F \\\n" + fmt(pair_block(True, False)))
     parts.append("#define SWK_F16PAIR_M \\\n" + fmt(pair_block(False, False)))
     parts.append("#define SWK_F16PAIR_L \\\n" + fmt(pair_block(False, True)))
+    parts.append("#define SWK_F16PAIRG_F \\\n" + fmt(pair_gotoh_block(True, False)))
+    parts.append("#define SWK_F16PAIRG_M \\\n" + fmt(pair_gotoh_block(False, False)))
+    parts.append("#define SWK_F16PAIRG_L \\\n" + fmt(pair_gotoh_block(False, True)))
     # 4- and 2-row single blocks (the wave kernel's K = 4, and K = 2 of its split tail: a
     # whole column in one block)
     for nr in (4, 2):

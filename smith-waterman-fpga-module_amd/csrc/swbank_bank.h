@@ -116,6 +116,11 @@ inline void trace_mark(const char* what) {
   if (g_trace) g_trace->mark(what);
 }
 
+inline bool poison_buffers() {  // (read at every allocation: tests switch it per case)
+  const char* v = std::getenv("SWBANK_POISON");
+  return v && v[0] == '1';
+}
+
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
@@ -128,6 +133,13 @@ struct DevBuf {
     size_t want = std::max<size_t>(n, 64);
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), want * sizeof(T));
     if (e == hipSuccess) cap = want;
+    // (tests) SWBANK_POISON=1: new device buffers start as 0x3C bytes (f16 1.0 in every half)
+    // instead of whatever the allocator hands back, so a read of a word nobody wrote shows;
+    // complete before any bank stream uses the buffer
+    if (e == hipSuccess && poison_buffers()) {
+      e = hipMemset(p, 0x3C, want * sizeof(T));
+      if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    }
     return e;
   }
   void release() {
@@ -477,6 +489,7 @@ sw_status prepare(sw_bank* b);
 sw_status prepare_multi(sw_bank* b);
 sw_status prepare_i32(sw_bank* b);
 // ---- swbank_launch.hip
+void u16_gotoh_rows(const sw_bank* b, bool f16, int& R, int& W);
 sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                  const uint32_t* d_lens, size_t n, uint32_t max_len, int32_t* d_scores,
                  hipStream_t st, uint32_t packed = SWK_PACK_BYTES,

@@ -420,13 +420,15 @@ sw_status prepare(sw_bank* b) {
   const int qlen = (int)b->query.size();
   // the HDL column-0 rule differs from the plain recurrence only if a match pays for a gap
   const int col0 = (!gotoh && smax > o + e) ? 1 : 0;
-  // Rows per wave: 32 for the merged DNA LUT kernels; 16 for tiny queries and for the
-  // Gotoh / profile / column-0 variants, whose 32-row columns do not fit 128 VGPRs (the
-  // occupancy-4 budget) without spilling.  Queries longer than one workgroup (16 waves) run
+  // Rows per wave: 32 for the DNA LUT kernels (merged and Gotoh: the Gotoh f16 column with
+  // the letter-pair table runs 8.3-8.6 TCUPS at R = 32 against 7.8-8.2 at R = 16, and a
+  // 512-row query fits one workgroup); 16 for tiny queries and for the profile / column-0
+  // variants, whose 32-row columns do not fit 128 VGPRs (the occupancy-4 budget) without
+  // spilling.  Queries longer than one workgroup (16 waves) run
   // as segments of SWBANK_SEG rows (default: a full 16-wave workgroup, 16·R rows), each
   // segment's bottom row handed to the next through HBM.  SWBANK_R / SWBANK_RB / SWBANK_SEG
   // override (tuning only).
-  int R = (qlen <= 16 || gotoh || prof || col0) ? 16 : 32, RB = 4;
+  int R = (qlen <= 16 || prof || col0) ? 16 : 32, RB = 4;
   R = env_int("SWBANK_R", R);
   RB = env_int("SWBANK_RB", RB);
   const int max_rows = (R >= 64 ? 8 : 16) * R;
@@ -533,13 +535,20 @@ sw_status prepare(sw_bank* b) {
   // {s(q_{k+1}, a), s(q_{k+1}, b)} (f16 halves; rows past the query -2048) and the row-0 word
   // 4 bytes before it.  S2/16 = 1 and S1/16 = 4 (mod 16) put the 16 A/C/G/T slots on 16
   // different 4-bank LDS groups.
+  // DNA Gotoh (R = 16): one table per query segment, each of the tallest segment's rows (the
+  // Gotoh column is 7.5 VALU per 2 cells from the table against 8.5 with the row LUT).
   std::vector<uint32_t> tpair;
-  uint32_t pS1 = 0, pS2 = 0;
-  if (f16 && !prof && !gotoh && !col0 && R == 32 && segs.size() == 1 && segs[0].W <= 4 &&
-      A == SW_DNA_ALPHA) {
+  uint32_t pS1 = 0, pS2 = 0, pair_words = 0;
+  if (f16 && !prof && !col0 && A == SW_DNA_ALPHA &&
+      (gotoh ? R == 16 || R == 32 : R == 32 && segs.size() == 1 && segs[0].W <= 4)) {
     const uint32_t NR = (uint32_t)segs[0].W * R;
     pair_strides(NR, pS1, pS2);
-    tpair = pair_table(b->query.data(), qlen, 0, NR, m, A, pS1, pS2);
+    for (size_t sg = 0; sg < segs.size(); ++sg) {
+      const std::vector<uint32_t> t =
+          pair_table(b->query.data(), qlen, (int)sg * seg_rows, NR, m, A, pS1, pS2);
+      pair_words = (uint32_t)t.size();
+      tpair.insert(tpair.end(), t.begin(), t.end());
+    }
   }
   // wave-kernel layout of the same query: rows padded to 64K; queries past 1024 rows run as
   // 1024-row segments (K = 16), one table per segment, concatenated
@@ -647,7 +656,7 @@ sw_status prepare(sw_bank* b) {
   HIPOK(b, upload(b->qtab, tab));
   if (f16) HIPOK(b, upload(b->qtab16, tab16));
   if (!tpair.empty()) HIPOK(b, upload(b->qpair, tpair));
-  b->pair_bytes = (uint32_t)tpair.size() * 4;
+  b->pair_bytes = pair_words * 4;  // one segment's table
   b->pS1 = pS1;
   b->pS2 = pS2;
   HIPOK(b, hipEventRecord(b->ev_ready, b->stream));

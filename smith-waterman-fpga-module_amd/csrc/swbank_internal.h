@@ -41,7 +41,8 @@ typedef struct SwkWaveSplit {
 /* One chunk of a streamed host batch (uploaded before the launch): its first tile and the
  * offset of its codes in the device batch buffer.  Its code layout travels in a flag word per
  * chunk, 0 until the chunk's copy landed, then SWK_PACK_STREAM or SWK_PACK_NIBBLE;
- * SWK_STREAM_ABORT from a wave whose wait ran out (read as 2-bit codes; the host fails the
+ * SWK_STREAM_ABORT from a wave whose wait ran out, or from the host for a chunk it never sent
+ * (its targets read as empty, its region is never read; the host re-runs or fails the
  * call). */
 typedef struct SwkStreamChunk {
   unsigned tile0, res_off_lo, res_off_hi, pad;

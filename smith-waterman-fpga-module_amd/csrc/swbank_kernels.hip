@@ -734,8 +734,10 @@ template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR =
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
   static_assert(!MQ || !PROF, "several queries: row-LUT or pair-table variants");
   static_assert(!STREAM || (!MQ && !PROF), "streamed batches: single-query LUT / pair variants");
-  static_assert(C == 8 || (C == 4 && PAIR && MQ && !STREAM), "4-column chunks: MQ pair only");
-  static_assert(!PAIR || (R == 32 && F16 && !PROF && !GOTOH && !COL0), "PAIR: f16 merged R=32");
+  static_assert(C == 8 || (C == 4 && PAIR && !STREAM), "4-column chunks: pair tables only");
+  static_assert(!PAIR || ((R == 32 || (R == 16 && GOTOH)) && F16 && !PROF && !COL0 &&
+                          (!GOTOH || !MQ)),
+                "PAIR: f16, merged R = 32 or Gotoh R = 16 / 32 (one query)");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -780,6 +782,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int snc = (int)a.nsc;
   int scur = -1, st0 = 0;
   uint32_t scn = 0, sro_lo = 0, sro_hi = 0, smode = SWK_PACK_STREAM;
+  bool sabort = false;  // the current chunk was released as aborted
   // ragged streamed batches (ulen == 0): a chunk's region is offsets u64 | lengths u32 | visiting
   // order u32 (scn each) | codes at the next 16-byte boundary; the order of the chunk of the tile
   // this wave is scoring (wperm, its first tile wst0) maps score positions to targets
@@ -804,11 +807,18 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
                      (size_t)st0 * SWB_TILE));
       sro_lo = __builtin_amdgcn_readfirstlane(ssc[c].res_off_lo);
       sro_hi = __builtin_amdgcn_readfirstlane(ssc[c].res_off_hi);
-      smode = stream_mode(a.hflag, a.dflag, c, snc, lane) == SWK_PACK_NIBBLE
-                  ? SWK_PACK_NIBBLE
-                  : SWK_PACK_STREAM;
+      const uint32_t md = stream_mode(a.hflag, a.dflag, c, snc, lane);
+      sabort = md == SWK_STREAM_ABORT;
+      smode = md == SWK_PACK_NIBBLE ? SWK_PACK_NIBBLE : SWK_PACK_STREAM;
     }
     pk = smode;
+    if (sabort) {  // a chunk that never landed (the host re-runs the call): its region may
+      cperm = nullptr;  // hold anything, so its targets read as empty and scores go in order
+      Lane2 e;
+      e.llo = e.lhi = 0u;
+      e.plo = e.phi = a.res;
+      return e;
+    }
     const uint8_t* base = a.res + ((size_t)sro_hi << 32 | sro_lo);
     if (a.ulen == 0) {  // ragged: the chunk's own offsets, lengths and order
       const uint64_t* co = reinterpret_cast<const uint64_t*>(base);
@@ -1074,41 +1084,67 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           const uint32_t noe = as_u32(as_u16x2(NOE2)), ne = as_u32(as_u16x2(NE2)),
                  no = as_u32(as_u16x2(NO2));
           u16x2 bst = best;
-#define SWK_PAIR_OUT(B, DA)                                                                   \
+          u16x2 F = upX;  // Gotoh: F running down the column
+#define SWK_PAIR_HT(B)                                                                        \
   [h0] "+v"(Hl[B]), [h1] "+v"(Hl[B + 1]), [h2] "+v"(Hl[B + 2]), [h3] "+v"(Hl[B + 3]),          \
       [h4] "+v"(Hl[B + 4]), [h5] "+v"(Hl[B + 5]), [h6] "+v"(Hl[B + 6]), [h7] "+v"(Hl[B + 7]),  \
       [t0] "+v"(Xl[B]), [t1] "+v"(Xl[B + 1]), [t2] "+v"(Xl[B + 2]), [t3] "+v"(Xl[B + 3]),      \
       [t4] "+v"(Xl[B + 4]), [t5] "+v"(Xl[B + 5]), [t6] "+v"(Xl[B + 6]), [t7] "+v"(Xl[B + 7]),  \
-      [Da] DA(Da), [Db] "=&v"(Db), [X] "=&v"(X), [DN] "=&v"(DN), [IN] "=&v"(IN),              \
-      [best] "+v"(bst)
-#define SWK_PAIR_IN(P0, P1, UP)                                                               \
+      [Db] "=&v"(Db), [best] "+v"(bst)
+#define SWK_PAIR_OUT(B, DA) SWK_PAIR_HT(B), [Da] DA(Da), [X] "=&v"(X), [DN] "=&v"(DN), [IN] "=&v"(IN)
+#define SWK_PAIR_OUTG(B, DA)                                                                  \
+  SWK_PAIR_HT(B), [Da] DA(Da), [EN] "=&v"(X), [HN] "=&v"(DN), [FN] "=&v"(IN), [F] "+v"(F)
+#define SWK_PAIR_IN(P0, P1)                                                                   \
   [p0] "v"(P0.x), [p1] "v"(P0.y), [p2] "v"(P0.z), [p3] "v"(P0.w), [p4] "v"(P1.x),             \
-      [p5] "v"(P1.y), [p6] "v"(P1.z), [p7] "v"(P1.w), [up] "v"(UP), [noe] "s"(noe),           \
-      [ne] "s"(ne), [no] "s"(no)
+      [p5] "v"(P1.y), [p6] "v"(P1.z), [p7] "v"(P1.w), [noe] "s"(noe), [ne] "s"(ne), [no] "s"(no)
+// block B of the column: first (row-0 prologue), middle or last (no successor row)
+#define SWK_PAIR_BLOCK(KIND, B, P0, P1)                                                       \
+  if constexpr (GOTOH) {                                                                      \
+    if constexpr (KIND == 0)                                                                  \
+      asm volatile(SWK_F16PAIRG_F : SWK_PAIR_OUTG(B, "=&v")                                   \
+                   : SWK_PAIR_IN(P0, P1), [dg] "v"(diag), [pw] "v"(pw));                   \
+    else if constexpr (KIND == 1)                                                             \
+      asm volatile(SWK_F16PAIRG_M : SWK_PAIR_OUTG(B, "+v") : SWK_PAIR_IN(P0, P1));         \
+    else                                                                                      \
+      asm volatile(SWK_F16PAIRG_L : SWK_PAIR_OUTG(B, "+v") : SWK_PAIR_IN(P0, P1));         \
+  } else {                                                                                    \
+    if constexpr (KIND == 0)                                                                  \
+      asm volatile(SWK_F16PAIR_F : SWK_PAIR_OUT(B, "=&v")                                     \
+                   : SWK_PAIR_IN(P0, P1), [up] "v"(upX), [dg] "v"(diag), [pw] "v"(pw));                 \
+    else if constexpr (KIND == 1)                                                             \
+      asm volatile(SWK_F16PAIR_M : SWK_PAIR_OUT(B, "+v") : SWK_PAIR_IN(P0, P1), [up] "v"(Xl[B - 1]));   \
+    else                                                                                      \
+      asm volatile(SWK_F16PAIR_L : SWK_PAIR_OUT(B, "+v") : SWK_PAIR_IN(P0, P1), [up] "v"(Xl[B - 1]));   \
+  }
+          // each block's words are read one block ahead; the last block's wait for the next
+          // column's block 0 and row-0 word
           uint4 pB0 = ld4(acur + 48), pB1 = ld4(acur + 64);  // block 1
           __builtin_amdgcn_sched_barrier(0);
-          asm volatile(SWK_F16PAIR_F
-                       : SWK_PAIR_OUT(0, "=&v")
-                       : SWK_PAIR_IN(pA0, pA1, upX), [dg] "v"(diag), [pw] "v"(pw));
-          pA0 = ld4(acur + 80);  // block 2
-          pA1 = ld4(acur + 96);
-          __builtin_amdgcn_sched_barrier(0);
-          asm volatile(SWK_F16PAIR_M : SWK_PAIR_OUT(8, "+v") : SWK_PAIR_IN(pB0, pB1, Xl[7]));
-          pB0 = ld4(acur + 112);  // block 3
-          pB1 = ld4(acur + 128);
-          __builtin_amdgcn_sched_barrier(0);
-          asm volatile(SWK_F16PAIR_M : SWK_PAIR_OUT(16, "+v") : SWK_PAIR_IN(pA0, pA1, Xl[15]));
+          SWK_PAIR_BLOCK(0, 0, pA0, pA1)
+          if constexpr (R == 32) {
+            pA0 = ld4(acur + 80);  // block 2
+            pA1 = ld4(acur + 96);
+            __builtin_amdgcn_sched_barrier(0);
+            SWK_PAIR_BLOCK(1, 8, pB0, pB1)
+            pB0 = ld4(acur + 112);  // block 3
+            pB1 = ld4(acur + 128);
+            __builtin_amdgcn_sched_barrier(0);
+            SWK_PAIR_BLOCK(1, 16, pA0, pA1)
+          }
           acur = pair_addr(nwl, nwh, nsh);  // next column: block 0 and row-0 word
           pA0 = ld4(acur + 16);
           pA1 = ld4(acur + 32);
           pw = ld1(acur + 12);
           __builtin_amdgcn_sched_barrier(0);
-          asm volatile(SWK_F16PAIR_L : SWK_PAIR_OUT(24, "+v") : SWK_PAIR_IN(pB0, pB1, Xl[23]));
+          SWK_PAIR_BLOCK(2, R - 8, pB0, pB1)
+#undef SWK_PAIR_BLOCK
+#undef SWK_PAIR_HT
 #undef SWK_PAIR_OUT
+#undef SWK_PAIR_OUTG
 #undef SWK_PAIR_IN
           (void)Db; (void)X; (void)DN; (void)IN;
           best = bst;
-          upX = Xl[R - 1];
+          upX = GOTOH ? F : Xl[R - 1];
         } else if constexpr (F16) {
           // selector bytes {0x0C, code_lo, 0x0C, code_hi}: the LUT byte is the f16 high byte
           const uint32_t sel16 = 0x0Cu | ((uint32_t)(jj & 3) << 8) | (0x0Cu << 16) |
@@ -1382,6 +1418,9 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
 #endif
 #ifndef SWK_UNIFORM_PTR
 #define SWK_UNIFORM_PTR 0  // target pointers in SGPRs
+#endif
+#ifndef SWK_HALF_UNROLL
+#define SWK_HALF_UNROLL 4  // two-pairs wave kernel: steps per loop iteration (2 or 4)
 #endif
 #ifndef SWK_HALF_AHEAD
 #define SWK_HALF_AHEAD 1  // two-pairs wave kernel: profile words one step ahead
@@ -2201,6 +2240,10 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
     nra = ring_l[0];
     nrb = ring_l[64];
   }
+  // AHEAD: step t reads the ring entries of step t + 2 at rp = ring_l + ((t + 2) & 31); a pair
+  // of steps from an even t never wraps, so one address per pair and immediate offsets.
+  // SWK_HALF_UNROLL: steps per loop iteration (2 or 4)
+  const uint32_t* rp = ring_l;
   const auto step = [&](const int t, const bool even) __attribute__((always_inline)) {
     // the next 32 columns go in before they are read (AHEAD: two steps before)
     if ((AHEAD ? even : !even) && (t & 31) == (AHEAD ? 30 : 31)) {
@@ -2214,7 +2257,7 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
     if constexpr (AHEAD) {
       lk = lkn;
       load_prof(lkn, nra, nrb);
-      const uint32_t* np = ring_l + ((t + 2) & 31);
+      const uint32_t* np = rp + (t & 1);
       nra = np[0];
       nrb = np[64];
       __builtin_amdgcn_sched_barrier(0);
@@ -2238,9 +2281,13 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
     botX = as_u32(upX);
   };
   const int nsteps = Lmax + 31;
-  for (int t = 0; t < nsteps; t += 2) {
-    step(t, true);
-    step(t + 1, false);
+  for (int t = 0; t < nsteps; t += SWK_HALF_UNROLL) {
+#pragma unroll
+    for (int u = 0; u < SWK_HALF_UNROLL; u += 2) {
+      rp = ring_l + ((t + u + 2) & 31);
+      step(t + u, true);
+      step(t + u + 1, false);
+    }
   }
   uint32_t bx = (uint32_t)f16_unscore(best.x), by = (uint32_t)f16_unscore(best.y);
 #pragma unroll
@@ -2335,7 +2382,7 @@ static hipError_t launch_wave_half(const ScoreArgs& a, uint32_t prof_bytes, hipS
   X(16, 4, 0, 1, 1, 0) X(32, 4, 0, 1, 1, 0) X(64, 4, 0, 1, 1, 0)                              \
   X(16, 4, 0, 0, 0, 1) X(16, 4, 1, 0, 0, 1) X(32, 4, 0, 0, 0, 1) X(64, 4, 0, 0, 0, 1)         \
   X(16, 4, 0, 0, 1, 1)                                                                        \
-  X(16, 4, 0, 1, 0, 1) X(16, 4, 1, 1, 0, 1) X(16, 4, 0, 1, 1, 1)
+  X(16, 4, 0, 1, 0, 1) X(16, 4, 1, 1, 0, 1) X(16, 4, 0, 1, 1, 1) X(32, 4, 0, 0, 1, 1)
 
 extern "C" void swk_set_occ_cap(int per_cu) { swk::t_occ_cap = per_cu; }
 
@@ -2373,8 +2420,10 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
   a.sstride = sstride;
   const uint32_t prof_bytes = (pad + 1) * PS;
   if (nq > 1 && pair) {  // several queries, pair tables (PS = one table's bytes)
-    // more than 4 waves (a 512-row table): 4-column chunks, so the ring fits beside the table
-    if (R == 32 && f16 && !prof && !gotoh && !col0 && W > 4)
+    // more than 4 waves (a 512-row table): 4-column chunks, so the ring fits beside the table;
+    // every segment of a segmented set too (a short last segment reads exactly the edge
+    // chunks the one before it wrote)
+    if (R == 32 && f16 && !prof && !gotoh && !col0 && (W > 4 || a.edge_in || a.edge_out))
       return swk::launch_score<32, 4, false, false, false, true, true, true, false, 4>(a, W, 0, st);
     if (R == 32 && f16 && !prof && !gotoh && !col0)
       return swk::launch_score<32, 4, false, false, false, true, true, true>(a, W, 0, st);
@@ -2385,13 +2434,27 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
   if (R == RR && RB == 4 && !col0 && !prof && !pair && gotoh == GT && f16 == FH)                 \
     return swk::launch_score<RR, 4, false, false, (GT != 0), (FH != 0), false, true>(a, W, 0, st);
     SWK_MQ_CASE(32, 0, 1) SWK_MQ_CASE(32, 0, 0) SWK_MQ_CASE(16, 0, 1) SWK_MQ_CASE(16, 0, 0)
-    SWK_MQ_CASE(16, 1, 1) SWK_MQ_CASE(16, 1, 0) SWK_MQ_CASE(32, 1, 0)
+    SWK_MQ_CASE(16, 1, 1) SWK_MQ_CASE(16, 1, 0) SWK_MQ_CASE(32, 1, 1) SWK_MQ_CASE(32, 1, 0)
 #undef SWK_MQ_CASE
     return hipErrorInvalidValue;
   }
   if (pair) {  // PS = pair-table bytes
     if (R == 32 && f16 && !prof && !gotoh && !col0)
       return swk::launch_score<32, 4, false, false, false, true, true>(a, W, 0, st);
+    // DNA Gotoh: 8-column chunks while the hand-off ring fits beside the table, else 4 (a
+    // 512-row table beside 16 waves).  A segmented query runs every segment with 4: the edge
+    // rows one segment writes are exactly the chunks the next one reads
+#define SWK_GPAIR(RR)                                                                         \
+    if (R == RR && f16 && !prof && gotoh && !col0) {                                          \
+      const hipError_t e = a.edge_in || a.edge_out                                            \
+          ? hipErrorInvalidConfiguration                                                      \
+          : swk::launch_score<RR, 4, false, false, true, true, true>(a, W, 0, st);            \
+      if (e != hipErrorInvalidConfiguration) return e;                                        \
+      return swk::launch_score<RR, 4, false, false, true, true, true, false, false, 4>(a, W, 0, \
+                                                                                         st); \
+    }
+    SWK_GPAIR(32) SWK_GPAIR(16)
+#undef SWK_GPAIR
     return hipErrorInvalidValue;
   }
 #define SWK_CASE(RR, BB, C0, PF, GT, FH)                                                      \
@@ -2430,6 +2493,10 @@ extern "C" hipError_t swk_launch_stream(int R, int gotoh, int f16, int pair, con
   if (pair) {
     if (R == 32 && f16 && !gotoh)
       return swk::launch_score<32, 4, false, false, false, true, true, false, true>(a, W, 0, st);
+    if (R == 32 && f16 && gotoh)
+      return swk::launch_score<32, 4, false, false, true, true, true, false, true>(a, W, 0, st);
+    if (R == 16 && f16 && gotoh)
+      return swk::launch_score<16, 4, false, false, true, true, true, false, true>(a, W, 0, st);
     return hipErrorInvalidValue;
   }
 #define SWK_ST_CASE(RR, GT, FH)                                                                  \
@@ -2437,7 +2504,7 @@ extern "C" hipError_t swk_launch_stream(int R, int gotoh, int f16, int pair, con
     return swk::launch_score<RR, 4, false, false, (GT != 0), (FH != 0), false, false, true>(     \
         a, W, 0, st);
   SWK_ST_CASE(32, 0, 1) SWK_ST_CASE(32, 0, 0) SWK_ST_CASE(16, 0, 1) SWK_ST_CASE(16, 0, 0)
-  SWK_ST_CASE(16, 1, 1) SWK_ST_CASE(16, 1, 0)
+  SWK_ST_CASE(16, 1, 1) SWK_ST_CASE(16, 1, 0) SWK_ST_CASE(32, 1, 1) SWK_ST_CASE(32, 1, 0)
 #undef SWK_ST_CASE
   return hipErrorInvalidValue;
 }

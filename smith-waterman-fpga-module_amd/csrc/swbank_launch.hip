@@ -14,6 +14,16 @@ static bool one_len_bin(uint32_t min_len, uint32_t max_len) {
   return ((max_len - min_len) >> shift) == 0;
 }
 
+// The u16 Gotoh column at R = 32 does not fit 128 VGPRs (it spills); a one-segment query of
+// at most 256 rows runs it at R = 16 over the same row LUT (rows are laid out linearly, W x R
+// words padded past the query), in ceil(|q| / 16) waves.
+void u16_gotoh_rows(const sw_bank* b, bool f16, int& R, int& W) {
+  if (f16 || !b->gotoh() || b->prof || R != 32 || b->segs.size() != 1 || b->query.size() > 256)
+    return;
+  R = 16;
+  W = std::max(1, (int)((b->query.size() + 15) / 16));
+}
+
 // packed (SWK_PACK_*): RECORDS: d_res holds n 64-byte CAPI records (2-bit codes), d_offs and
 // d_lens are unused; STREAM: 2-bit codes, d_offs in bytes (the host feeder's DNA chunks).
 // perm/perm_n (optional, tile kernel): pass 0 visits the targets in the order perm[0..n)
@@ -76,14 +86,17 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   //    f = min(1, 0.45 + 0.15 w), x 0.85 when the query runs as several segments;
   //  wave kernel (queries <= 1024 rows): base rate x row fill (query / 64K lanes' rows) x
   //    column fill (L / (L + 63): the 63-step skew of the lane pipeline).
-  // Base GCUPS: tile f16 merged 9000 (profile 8000), f16 Gotoh 7500 (profile 7100), u16
+  // Base GCUPS: tile f16 merged 9000 (profile 8000), f16 Gotoh 8500 with the letter-pair
+  // table (7500 row LUT, profile 7100), u16
   // merged 7400 (profile 6500), u16 Gotoh 5800 (profile 5600); wave f16 merged 8600
   // (profile 7700), f16 Gotoh 7800 (profile 6800), u16 merged 7600 (profile 6600), u16 Gotoh
   // 6100 (profile 5200).  SWBANK_KERNEL=tile|wave forces one.
   const double tiles = (double)ntiles, W = b->segs[0].W;
   const double cu_frac = std::min(1.0, tiles / 256.0);
   const double wps = std::min(4.0, std::max(1.0, std::ceil(tiles / 256.0)) * W / 4.0);
-  const double tile_base = use_f16 ? (gotoh ? (b->prof ? 7100 : 7500) : (b->prof ? 8000 : 9000))
+  const bool pair_tab = use_f16 && b->pair_bytes != 0 && env_int("SWBANK_PAIR", 1) != 0;
+  const double tile_base = use_f16 ? (gotoh ? (b->prof ? 7100 : pair_tab ? 8500 : 7500)
+                                            : (b->prof ? 8000 : 9000))
                                    : (gotoh ? (b->prof ? 5600 : 5800) : (b->prof ? 6500 : 7400));
   const double tile_est = tile_base * cu_frac * std::min(1.0, 0.45 + 0.15 * wps) *
                           (nseg > 1 ? 0.85 : 1.0);
@@ -177,8 +190,10 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       }
     }
   } else {
+    int R0 = b->R, W0 = b->segs[0].W;  // (the first pass's rows per wave)
+    u16_gotoh_rows(b, use_f16, R0, W0);
     snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=%zu", arith,
-             b->prof ? "-profile" : use_pair ? " pair" : "", b->R, b->segs[0].W, nseg);
+             b->prof ? "-profile" : use_pair ? " pair" : "", R0, W0, nseg);
   }
   // A device batch (dsort) visits its targets longest first, sorted on the device, so every
   // tile holds similar lengths (a tile runs to its longest lane); SWBANK_DSORT=0 disables.
@@ -263,14 +278,16 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
         const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
         void* eout = s + 1 < nseg ? b->edge[s & 1].p : nullptr;
         const bool pair = f16 && use_pair;
-        HIPOK(b, swk_launch_score(b->R, b->RB, b->col0, b->prof, gotoh ? 1 : 0, f16 ? 1 : 0, res,
+        int R = b->R, Wl = b->segs[s].W;
+        u16_gotoh_rows(b, f16, R, Wl);
+        HIPOK(b, swk_launch_score(R, b->RB, b->col0, b->prof, gotoh ? 1 : 0, f16 ? 1 : 0, res,
                                   offs, lens, np,
-                                  pair ? b->qpair.p
+                                  pair ? b->qpair.p + s * (b->pair_bytes / 4)
                                   : f16 ? b->qtab16.p + b->segs[s].off16
                                         : b->qtab.p + b->segs[s].off,
                                   f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
                                   pair ? b->pair_bytes : f16 && b->prof ? b->PS16 : b->PS,
-                                  b->pad, b->segs[s].W, scores, ein, eout, ecols, s > 0 ? 1 : 0,
+                                  b->pad, Wl, scores, ein, eout, ecols, s > 0 ? 1 : 0,
                                   (int)packed, idx, nidx, (uint32_t)p0,
                                   pass == 0 ? ident : nullptr, pair ? 1 : 0, b->pS1, b->pS2,
                                   ulen, ustride, 1u, 0u, 0, st));
@@ -334,7 +351,7 @@ static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_
   const char* kforce = std::getenv("SWBANK_KERNEL");
   const bool mq = env_int("SWBANK_MQ", 1) != 0 && !b->prof && !b->col0 && exact &&
                   env_int("SWBANK_I32", 0) == 0 && (b->R == 16 || b->R == 32) && b->RB == 4 &&
-                  !(b->gotoh() && !use_f16 && b->R != 16) && n <= 0xFFFFFFFFull &&
+                  n <= 0xFFFFFFFFull &&
                   !(kforce && std::strcmp(kforce, "wave") == 0) && ntiles * nq <= 0x7FFFFFFFull;
   if (!mq) {  // one query at a time (each prepare()d in turn), then the set's layout again
     const std::vector<uint8_t> longest = b->query;

@@ -37,7 +37,9 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   const bool use_f16 = b->f16 && b->f16_neg >= -2048 && env_int("SWBANK_F16", 1) != 0 &&
                        std::min<uint64_t>(b->query.size(), L) * smax + smax <= 2048u;
   const bool pair = use_f16 && b->pair_bytes != 0 && env_int("SWBANK_PAIR", 1) != 0;
-  if (!(b->R == 16 || (b->R == 32 && !b->gotoh()))) return SW_OK;  // streamed variants
+  if (!(b->R == 16 || b->R == 32)) return SW_OK;  // streamed variants
+  int sR = b->R, sW = b->segs[0].W;
+  u16_gotoh_rows(b, use_f16, sR, sW);
 
   // chunks of whole tiles: 1/64 of the batch first, doubling up to 1/8
   std::vector<size_t> tile0;
@@ -125,13 +127,13 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       HIPOK(b, hipEventRecord(ev.a, ks));
       HIPOK(b, hipEventRecord(ev.b, ks));
     }
-    HIPOK(b, swk_launch_stream(b->R, b->gotoh() ? 1 : 0, use_f16 ? 1 : 0, pair ? 1 : 0, b->sbuf.p,
+    HIPOK(b, swk_launch_stream(sR, b->gotoh() ? 1 : 0, use_f16 ? 1 : 0, pair ? 1 : 0, b->sbuf.p,
                                n, rlens ? 0u : L, b->sdrec.p, hflag,
                                reinterpret_cast<uint32_t*>(b->sflag.p),
                                (uint32_t)nsc, b->sctr.p,
                                pair ? b->qpair.p : use_f16 ? b->qtab16.p : b->qtab.p,
                                use_f16 ? b->nv16 : b->nv, b->S, b->O, b->E,
-                               pair ? b->pair_bytes : 0, b->pad, b->segs[0].W,
+                               pair ? b->pair_bytes : 0, b->pad, sW,
                                reinterpret_cast<int32_t*>(b->shscores.p),
                                b->pS1, b->pS2, ks));
     HIPOK(b, hipEventRecord(b->ev_used, ks));
@@ -140,7 +142,7 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       b->events.push_back(ev);
     }
     snprintf(b->last_kernel, sizeof(b->last_kernel), "tile %s%s R=%d W=%d segs=1 streamed=%zu",
-             use_f16 ? "f16" : "u16", pair ? " pair" : "", b->R, b->segs[0].W, nsc);
+             use_f16 ? "f16" : "u16", pair ? " pair" : "", sR, sW, nsc);
     trace_mark("kernel");
     return SW_OK;
   };
@@ -397,7 +399,7 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     started = i == 0 || started;
   }
   // the issued chunks' words once their copies landed; on failure the chunks never sent are
-  // released to the kernel as aborted (it reads whatever their range holds) so it drains, and
+  // released to the kernel as aborted (their targets read as empty) so it drains, and
   // the call reports the error
   {
     std::lock_guard<std::mutex> lk(pm);

@@ -26,3 +26,11 @@ def oracle():
 def swbank():
     import swbank as S
     return S
+
+
+@pytest.fixture
+def poisoned_buffers(monkeypatch):
+    """SWBANK_POISON=1: every device buffer a bank allocates starts as 0x3C bytes (f16 1.0)
+    instead of whatever the allocator hands back (often zeros in a fresh process, stale data
+    late in a long session), so a kernel that reads a word nobody wrote fails every time."""
+    monkeypatch.setenv("SWBANK_POISON", "1")

@@ -533,6 +533,37 @@ def test_pair_table_path(bank, qlen, params, kernel_choice):
         assert kern.startswith("tile f16 R=") and "pair" not in kern, kern
 
 
+@pytest.mark.parametrize("qlen", [5, 17, 100, 128, 129, 255, 256, 257, 400, 512, 513, 1000])
+@pytest.mark.parametrize("params", [(5, -4, -10, -1), (2, -3, -5, -2), (4, 0, -8, -2)])
+def test_gotoh_pair_table_path(qlen, params, kernel_choice, poisoned_buffers):
+    """The letter-pair table in the Gotoh f16 tile column (R = 32; R = 16 for <= 16 rows):
+    one table per query segment (512 rows; 4-column chunks when the table and the segment
+    edges leave no room for 8), all 25 letter pairs incl. dense N, ragged lengths with empty
+    targets, homologs near the f16 bound; "tile" takes the pair table, "tile-lut" the
+    per-row LUT, "tile-u16" the u16 column (R = 16 up to 256 rows), all equal to the oracle."""
+    rng = np.random.default_rng(qlen * 13 + params[0])
+    q, seqs = _random_case(rng, qlen, 400, 300, p_n=0.25)
+    seqs += [rng.integers(0, 4, int(n), dtype=np.uint8) for n in rng.integers(0, 7, 200)]
+    for k in range(0, 400, 37):  # homologs: long gapped local alignments
+        m = q[rng.integers(0, max(1, qlen // 3)):][:300].copy()
+        m[::11] = rng.integers(0, 4, len(m[::11]))
+        seqs[k] = m
+    with S.ScoreBank(gap_model=S.GAP_GOTOH) as bank:
+        bank.set_penalties(*params)
+        bank.load_query(q)
+        got = bank.score_targets(seqs)
+        kern = bank.last_kernel()
+    res, offs, lens = O.pack_residues(seqs)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(params[0], params[1]), params[2],
+                         params[3], O.GAP_GOTOH)
+    assert (got == want).all(), (kern, [(i, int(lens[i]), int(got[i]), int(want[i]))
+                                        for i in np.nonzero(got != want)[0][:8]])
+    if kernel_choice == "tile":
+        assert kern.startswith("tile f16") and " pair R=" in kern, kern
+    elif kernel_choice == "tile-lut":
+        assert " pair" not in kern, kern
+
+
 @pytest.mark.parametrize("qlen", [32, 64, 128])
 @pytest.mark.parametrize("tail", [1, 10, 63, 64, 65, 121, 127])
 def test_partial_last_tile_full_chunks(bank, qlen, tail):

@@ -190,3 +190,25 @@ def test_query_set_pair_tables(monkeypatch, nq, rows):
     bad = np.argwhere(got != want)
     assert bad.size == 0, (kern, [(int(i), int(k), int(got[i, k]), int(want[i, k]))
                                   for i, k in bad[:6]])
+
+
+@pytest.mark.parametrize("qmax", [513, 520, 530, 1025])
+def test_query_set_pair_short_last_segment(monkeypatch, poisoned_buffers, qmax):
+    """A set whose longest query ends just past a 512-row segment: the last segment has 1-2
+    waves.  Every segment must run with the same column chunk (4), so the last one reads exactly
+    the edge columns the one before it wrote (with 8 it read up to 4 columns nobody wrote,
+    bytes from earlier allocations, and short tiles scored their padding columns)."""
+    monkeypatch.setenv("SWBANK_KERNEL", "tile")
+    rng = np.random.default_rng(qmax)
+    queries = [rng.integers(0, 4, L, dtype=np.uint8) for L in (qmax, 100, 300)]
+    seqs = _targets(rng, 700, 0, 21, 4, queries, p_n=0.01)  # many tiles of 1-6 chunks
+    with S.ScoreBank() as bank:
+        bank.set_penalties(5, -4, -12, -4)
+        bank.load_queries(queries)
+        got = _score_set(bank, queries, seqs)
+        kern = bank.last_kernel()
+    assert " pair " in kern, kern
+    want = _oracle_set(queries, seqs, O.dna_matrix(), -12, -4, O.GAP_MERGED)
+    bad = np.argwhere(got != want)
+    assert bad.size == 0, (kern, [(int(i), int(k), int(got[i, k]), int(want[i, k]))
+                                  for i, k in bad[:6]])

@@ -72,7 +72,7 @@ def test_stream_pair_f16(monkeypatch, L):
 
 
 @pytest.mark.parametrize("case", ["nibble-mid", "nibble-all", "u16", "gotoh-f16", "gotoh-u16",
-                                  "lut-f16"])
+                                  "lut-f16", "gotoh-lut", "gotoh-f16-256"])
 def test_stream_variants(monkeypatch, case):
     """4-bit chunks from the first chunk holding an N on; the row-LUT variants (u16, Gotoh
     R = 16, f16 without pair tables)."""
@@ -87,13 +87,14 @@ def test_stream_variants(monkeypatch, case):
         extra = list(range(24900, 25100))
     if case == "nibble-all":
         res[rng.random(res.size) < 0.02] = 4
-    if case == "lut-f16":
+    if case in ("lut-f16", "gotoh-lut"):
         monkeypatch.setenv("SWBANK_PAIR", "0")
     if case in ("u16", "gotoh-u16"):
         monkeypatch.setenv("SWBANK_F16", "0")
     gotoh = case.startswith("gotoh")
     params = (5, -4, -10, -1) if gotoh else REF
-    q = rng.integers(0, 4, 140, dtype=np.uint8)
+    # (256 rows: a 16-wave Gotoh workgroup, the largest pair table beside the ring)
+    q = rng.integers(0, 4, 256 if case.endswith("256") else 140, dtype=np.uint8)
     with S.ScoreBank(gap_model=S.GAP_GOTOH if gotoh else S.GAP_MERGED) as bank:
         bank.set_penalties(*params)
         bank.load_query(q)
@@ -105,8 +106,10 @@ def test_stream_variants(monkeypatch, case):
     assert "streamed=" in kern, kern
     if case in ("u16", "gotoh-u16"):
         assert kern.startswith("tile u16"), kern
-    if case == "lut-f16":
+    if case in ("lut-f16", "gotoh-lut"):
         assert kern.startswith("tile f16 R=") and " pair " not in kern, kern
+    if case.startswith("gotoh-f16"):
+        assert kern.startswith("tile f16 pair R=32"), kern
     assert np.array_equal(got, ref), kern
     sel = np.unique(np.concatenate([rng.choice(n, 500, replace=False), np.asarray(extra, int),
                                     np.arange(n - 128, n)]))
@@ -118,7 +121,7 @@ def test_stream_variants(monkeypatch, case):
 
 @pytest.mark.parametrize("where", ["first", "middle", "last"])
 @pytest.mark.parametrize("kind", ["code", "range"])
-def test_stream_errors(monkeypatch, where, kind):
+def test_stream_errors(monkeypatch, where, kind, poisoned_buffers):
     """A code outside the alphabet or a target past the residues, in the first, a middle or the
     last chunk: SW_ERR_ARG naming the target; the kernel drains (the chunks never sent are
     released as aborted) and the next call on the bank scores correctly."""
@@ -234,7 +237,7 @@ def test_stream_with_other_banks(monkeypatch):
             o.close()
 
 
-def test_stream_stalled_chunk_reruns(monkeypatch):
+def test_stream_stalled_chunk_reruns(monkeypatch, poisoned_buffers):
     """A chunk published past the kernel's wait bound (SWBANK_STREAM_HOLD_MS): the waiting waves
     mark it aborted, the kernel drains, and the call re-runs through the chunked feeder with
     exact scores; the bank stays usable for a streamed call afterwards."""
@@ -371,7 +374,7 @@ def test_stream_records(monkeypatch, L):
 
 
 @pytest.mark.parametrize("where", ["chunk0", "later", "too-long"])
-def test_stream_records_other_lengths(monkeypatch, where):
+def test_stream_records_other_lengths(monkeypatch, where, poisoned_buffers):
     """A record of another length ends streaming: in chunk 0 before the launch, later after
     the kernel drains; the chunked feeder then scores the call (exact), or reports a length
     past 232 (SW_ERR_ARG)."""
@@ -448,9 +451,12 @@ def test_stream_ragged(monkeypatch, case):
 
 
 @pytest.mark.parametrize("kind", ["code", "range"])
-def test_stream_ragged_errors(monkeypatch, kind):
+def test_stream_ragged_errors(monkeypatch, kind, poisoned_buffers):
     """A bad code or a target past the residues in a ragged streamed batch: SW_ERR_ARG naming
-    the target, and the bank scores the next call."""
+    the target, and the bank scores the next call.  The chunks never sent are released to the
+    running kernel as aborted; with poisoned buffers their regions hold 0x3C bytes, which the
+    kernel once read as offsets and visiting order (an illegal address): aborted targets now
+    read as empty."""
     monkeypatch.setenv("SWBANK_STREAM", "2")
     monkeypatch.setenv("SWBANK_STREAM_RAGGED", "1")  # opt-in
     rng = np.random.default_rng(71)
