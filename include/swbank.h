@@ -217,7 +217,8 @@ sw_status sw_bank_timing(sw_bank *bank, uint64_t *launches, double *pack_ms, dou
  * devices'), so silent slow paths show: host calls that ran as one streamed kernel, streamed
  * calls re-run through the chunked feeder because a chunk's wait ran out, streamed calls
  * declined for the memory cap (SWBANK_STREAM_MB) or a failed allocation, chunked host calls,
- * device-side length sorts, and multi-device gathers abandoned after their time limit. */
+ * device-side length sorts, multi-device gathers abandoned after their time limit, and chunks
+ * of chunked calls sent as mixed 2-bit / 4-bit codes (ragged DNA). */
 typedef struct sw_counters {
   uint64_t stream_calls;
   uint64_t stream_reruns;
@@ -225,6 +226,7 @@ typedef struct sw_counters {
   uint64_t chunked_calls;
   uint64_t device_sorts;
   uint64_t gather_timeouts;
+  uint64_t mixed_chunks;
 } sw_counters;
 sw_status sw_bank_counters(const sw_bank *bank, sw_counters *out);
 

@@ -344,6 +344,8 @@ struct sw_bank {
   hipStream_t copy_stream = nullptr;
   hipEvent_t h2d_done[NSLOT] = {}, kern_done[NSLOT] = {};
   PinBuf hslot[NSLOT], hscores;
+  std::vector<std::vector<uint32_t>> mlist;  // per pool part: a mixed chunk's 4-bit targets
+  std::vector<std::vector<uint8_t>> mstage;  // ... and their codes, packed while gathering
   std::vector<hipEvent_t> out_ev;  // per chunk: its scores are back in hscores
   hipStream_t out_stream = nullptr;  // scores back to the host, beside the next chunk's kernel
   hipStream_t stream2 = nullptr;     // odd chunks' kernels (scratch-free launches overlap)
@@ -490,6 +492,7 @@ sw_status prepare_multi(sw_bank* b);
 sw_status prepare_i32(sw_bank* b);
 // ---- swbank_launch.hip
 void u16_gotoh_rows(const sw_bank* b, bool f16, int& R, int& W);
+bool wave_preferred(const sw_bank* b, size_t n, uint32_t max_len, bool use_f16);
 sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                  const uint32_t* d_lens, size_t n, uint32_t max_len, int32_t* d_scores,
                  hipStream_t st, uint32_t packed = SWK_PACK_BYTES,

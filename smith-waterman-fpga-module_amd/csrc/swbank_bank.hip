@@ -243,6 +243,7 @@ extern "C" sw_status sw_bank_counters(const sw_bank* b, sw_counters* out) {
     out->chunked_calls += k->ctr.chunked_calls;
     out->device_sorts += k->ctr.device_sorts;
     out->gather_timeouts += k->ctr.gather_timeouts;
+    out->mixed_chunks += k->ctr.mixed_chunks;
   }
   return SW_OK;
 }

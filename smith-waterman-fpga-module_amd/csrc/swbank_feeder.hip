@@ -384,7 +384,17 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   const uint64_t smax0 = (uint64_t)std::max(0, b->smax);
   const bool uni_ok = env_int("SWBANK_UNIFORM", 1) != 0 && env_int("SWBANK_I32", 0) == 0 &&
                       std::min<uint64_t>(b->query.size(), max_len) * smax0 + smax0 <= 65535u;
-  std::vector<size_t> part(T + 1), part2(T + 1), part4(T + 1);
+  // Ragged DNA chunks cross as SWK_PACK_MIXED: every target in 2-bit codes from an even byte,
+  // or in 4-bit codes from an odd byte when it holds an N, with u32 offsets (8 header bytes per
+  // target instead of 16, and N costs 4 bits only in the targets that hold one); the tile
+  // kernel reads it (launches that would take the wave kernel or the int32 re-score, and host
+  // sorted chunks, keep the whole-chunk layouts).  SWBANK_MIXED=0 disables.
+  const bool mixed_ok = dna_pack && env_int("SWBANK_MIXED", 1) != 0 &&
+                        env_int("SWBANK_I32", 0) == 0 &&
+                        std::min<uint64_t>(b->query.size(), max_len) * smax0 + smax0 <= 65535u;
+  const bool f16_ok = b->f16 && b->f16_neg >= -2048 && env_int("SWBANK_F16", 1) != 0;
+  std::vector<size_t> mperm(chunks.size(), 0);  // a mixed chunk's sort order (device only)
+  std::vector<size_t> part(T + 1), part2(T + 1), part4(T + 1), psz(T + 1);
   std::vector<uint32_t> partmax(T), partmin(T);
   std::atomic<size_t> bad{SIZE_MAX}, oob{SIZE_MAX};
   std::atomic<uint32_t> wide{0};
@@ -401,15 +411,17 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     std::fill(part.begin(), part.end(), 0);
     std::fill(part2.begin(), part2.end(), 0);
     std::fill(part4.begin(), part4.end(), 0);
+    std::fill(psz.begin(), psz.end(), 0);
     oob = SIZE_MAX;
     pool.run([&](unsigned p) {
-      size_t acc = 0, acc2 = 0, acc4 = 0;
+      size_t acc = 0, acc2 = 0, acc4 = 0, acc2e = 0;
       uint32_t m = 0, mn = UINT32_MAX;
       bool out = false;
       for (size_t k = c.c0 + std::min(cnt, p * step); k < c.c0 + std::min(cnt, (p + 1) * step);
            ++k) {
         acc += lens[k];
         acc2 += (lens[k] + 3) / 4;
+        acc2e += ((lens[k] + 3) / 4 + 1) & ~(size_t)1;  // (mixed: 2-bit targets on even bytes)
         acc4 += (lens[k] + 1) / 2;
         m = std::max(m, lens[k]);
         mn = std::min(mn, lens[k]);
@@ -429,6 +441,7 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       part[p + 1] = acc;
       part2[p + 1] = acc2;
       part4[p + 1] = acc4;
+      psz[p + 1] = acc2e;
       partmax[p] = m;
       partmin[p] = mn;
     });
@@ -446,8 +459,86 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       part[p + 1] += part[p];
       part2[p + 1] += part2[p];
       part4[p + 1] += part4[p];
+      psz[p + 1] += psz[p];
     }
     uint32_t mode = SWK_PACK_BYTES;
+    const uint64_t ctop = std::min<uint64_t>(b->query.size(), chunk_max[gi]) * smax0 + smax0;
+    const bool cf16 = f16_ok && (ctop <= 2048u || env_int("SWBANK_F16_OPT", 1) != 0);
+    const size_t ca32 = align16(cnt * 8);
+    if (mixed_ok && !uni && (host_dsort || cnt <= SWB_TILE) &&
+        ca32 + align16(part2[T] + part4[T] + 3 * cnt + 32) + align16(cnt * 4 + 8) <= c.bytes &&
+        !wave_preferred(b, cnt, chunk_max[gi], cf16)) {
+      // pass 1: every target in 2-bit codes at its even 2-bit position (sizes known up front);
+      // a target with a code past 3 is packed again at once in 4-bit codes into the part's
+      // staging buffer (its residues still in cache: scattered re-reads later were latency
+      // bound).  Pass 2: each part's staged 4-bit targets land as one block at an odd position
+      // after the 2-bit region (their 2-bit bytes stay unused)
+      uint32_t* so32 = reinterpret_cast<uint32_t*>(slot);
+      uint32_t* sl32 = so32 + cnt;
+      uint8_t* mcodes = slot + ca32;
+      if (b->mlist.size() < T) b->mlist.resize(T);
+      if (b->mstage.size() < T) b->mstage.resize(T);
+      std::vector<size_t> r4(T + 1, 0);  // staged 4-bit bytes per part
+      wide = 0;
+      pool.run([&](unsigned p) {
+        const size_t lo = std::min(cnt, p * step), hi = std::min(cnt, (p + 1) * step);
+        // (list and stage live in this thread while they grow: the parts' vector headers
+        // share cache lines)
+        std::vector<uint32_t> nl;
+        std::vector<uint8_t> sg;
+        nl.swap(b->mlist[p]);
+        sg.swap(b->mstage[p]);
+        nl.clear();
+        const size_t scap = part4[p + 1] - part4[p] + 2 * (hi - lo) + 64;
+        if (sg.size() < scap) sg.resize(scap);
+        size_t at = psz[p], sat = 0;
+        uint32_t mx = 0;
+        for (size_t i = lo; i < hi; ++i) {
+          const size_t k = c.c0 + i;
+          const uint32_t l = lens[k];
+          if (pack2fn(residues + offsets[k], l, mcodes + at, wide_ok(k, l, at, 8, psz[p + 1])) >
+              3u) {
+            mx = std::max(mx, pack4fn(residues + offsets[k], l, sg.data() + sat,
+                                      wide_ok(k, l, sat, 16, scap)));
+            nl.push_back((uint32_t)i);
+            sat += ((l + 1) / 2 + 1) & ~(size_t)1;
+          }
+          so32[i] = (uint32_t)at;
+          sl32[i] = l;
+          at += ((l + 3) / 4 + 1) & ~(size_t)1;
+        }
+        b->mlist[p].swap(nl);
+        b->mstage[p].swap(sg);
+        r4[p + 1] = sat;
+        if (mx >= alpha) wide = 1;  // a code outside the alphabet: the byte path reports it
+      });
+      for (unsigned p = 0; p < T; ++p) r4[p + 1] += r4[p];
+      const size_t b4 = psz[T] + 1;  // odd: 4-bit targets start on odd bytes
+      trace_mark("g-mixed2");
+      if (r4[T] && wide.load() == 0) {
+        pool.run([&](unsigned p) {
+          const size_t base = b4 + r4[p];
+          std::memcpy(mcodes + base, b->mstage[p].data(), r4[p + 1] - r4[p]);
+          size_t sat = 0;
+          for (const uint32_t i : b->mlist[p]) {
+            so32[i] = (uint32_t)(base + sat);
+            sat += ((lens[c.c0 + i] + 1) / 2 + 1) & ~(size_t)1;
+          }
+        });
+      }
+      trace_mark("g-mixed4");
+      if (wide.load() == 0) {
+        const size_t end = b4 + r4[T];
+        std::memset(mcodes + end, 0, 16);  // a last chunk reads up to 3 bytes past
+        chunk_mode[gi] = SWK_PACK_MIXED;
+        ++b->ctr.mixed_chunks;
+        const bool uniform = chunk_min == chunk_max[gi];
+        dev_sort[gi] = !uniform && cnt > SWB_TILE;  // (one tile needs no order)
+        const size_t copied = ca32 + align16(end + 16);
+        mperm[gi++] = copied;  // the device sort's order (n + 2 words) goes after the codes
+        return copied;
+      }
+    }
     bool two = pack2;
     if (two) {  // optimistic: any code > 3 (N, or outside the alphabet) -> 4 bits or bytes
       wide = 0;
@@ -560,6 +651,7 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     const bool pm = has_perm[si], ds = dev_sort[si];
     const uint32_t mode = chunk_mode[si], ustride = chunk_stride[si];
     const int slot = (int)(si % sw_bank::NSLOT);
+    const size_t mp = mperm[si];
     const uint32_t ml = chunk_max[si++];
     uint32_t* scr = nullptr;
     if (ds) {  // the slot's own sort scratch, zeroed once (the sort kernels leave it zeroed)
@@ -577,6 +669,11 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     if (ustride)
       return launch(b, dslot + codes_at(cnt), nullptr, nullptr, cnt, ml, d_scores, ks, mode,
                     nullptr, nullptr, false, !overlap, nullptr, nullptr, ml, ustride);
+    if (mode == SWK_PACK_MIXED)  // u32 offsets | lengths | codes; the order after the codes
+      return launch(b, dslot + align16(cnt * 8), reinterpret_cast<const uint64_t*>(dslot),
+                    reinterpret_cast<const uint32_t*>(dslot + cnt * 4), cnt, ml, d_scores, ks,
+                    mode, nullptr, nullptr, ds, !overlap,
+                    ds ? reinterpret_cast<uint32_t*>(dslot + mp) : nullptr, scr);
     return launch(b, dslot + codes_at(cnt), reinterpret_cast<const uint64_t*>(dslot),
                   reinterpret_cast<const uint32_t*>(dslot + tl.lens_at), cnt, ml, d_scores,
                   ks, mode,

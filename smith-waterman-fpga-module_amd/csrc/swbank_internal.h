@@ -24,6 +24,10 @@
 #define SWK_PACK_STREAM 2u
 /* 4-bit stream: 2 codes per byte, low nibble first (DNA chunks that hold an N). */
 #define SWK_PACK_NIBBLE 3u
+/* Mixed stream (the host feeder's ragged DNA chunks, tile kernel only): each target in 2-bit
+ * codes from an even byte, or, when it holds an N, in 4-bit codes from an odd byte (the
+ * address parity is the format); offsets are u32 bytes from the codes' start. */
+#define SWK_PACK_MIXED 4u
 
 /* Wave kernel split tail (swk_launch_wave): the last `pairs` pairs run as P (2 or 4) row
  * segments of K/P rows per lane, one wave each, each segment's bottom row handed down through
@@ -42,10 +46,10 @@ typedef struct SwkWaveSplit {
  * offset of its codes in the device batch buffer.  Its code layout travels in a flag word per
  * chunk, 0 until the chunk's copy landed, then SWK_PACK_STREAM or SWK_PACK_NIBBLE;
  * SWK_STREAM_ABORT from a wave whose wait ran out, or from the host for a chunk it never sent
- * (its targets read as empty, its region is never read; the host re-runs or fails the
- * call). */
+ * (the host re-runs or fails the call; a ragged chunk is then read from the zeroed region at
+ * byte zero_off256 * 256 of the buffer: empty targets). */
 typedef struct SwkStreamChunk {
-  unsigned tile0, res_off_lo, res_off_hi, pad;
+  unsigned tile0, res_off_lo, res_off_hi, zero_off256;
 } SwkStreamChunk;
 #define SWK_STREAM_ABORT 0xFFFFFFFFu
 

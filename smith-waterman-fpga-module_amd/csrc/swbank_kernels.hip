@@ -398,6 +398,12 @@ __device__ __forceinline__ uint32_t record_len(const uint8_t* rec) {
   return min((uint32_t)load_u<uint16_t>(rec + 4), SWB_RECORD_MAX);
 }
 
+// SWK_PACK_MIXED: a target in 4-bit codes starts at an odd address, one in 2-bit codes at an
+// even one.
+__device__ __forceinline__ bool mixed_nibble(const uint8_t* p) {
+  return ((uint32_t)reinterpret_cast<uintptr_t>(p) & 1u) != 0;
+}
+
 // C = 4 (the 16-wave query-set kernel's 4-column chunks): codes [4c, 4c+4) in lo.x / hi.x.
 __device__ __forceinline__ uint32_t pad_tail4(uint32_t w, uint32_t j0, uint32_t len, uint32_t pad) {
   const uint32_t n = len > j0 ? min(len - j0, 4u) : 0u;
@@ -405,7 +411,8 @@ __device__ __forceinline__ uint32_t pad_tail4(uint32_t w, uint32_t j0, uint32_t 
   return (w & keep) | ((pad * 0x01010101u) & ~keep);
 }
 
-template <int C = 8>
+// MIX = false: the caller never passes SWK_PACK_MIXED (streamed and query-set variants)
+template <int C = 8, bool MIX = true>
 __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint32_t pad,
                                          uint32_t packed, uint2& lo, uint2& hi) {
   static_assert(C == 8 || C == 4, "chunks of 8 or 4 columns");
@@ -417,6 +424,14 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint3
       const uint32_t ch = min((uint32_t)c, max((t.lhi + 3) / 4, 1u) - 1);
       x = unpack8n(load_u<uint16_t>(t.plo + 2 * cl)).x;
       y = unpack8n(load_u<uint16_t>(t.phi + 2 * ch)).x;
+    } else if (MIX && packed == SWK_PACK_MIXED) {  // per target: 4-bit at an odd address
+      const uint32_t cl = min((uint32_t)c, max((t.llo + 3) / 4, 1u) - 1);
+      const uint32_t ch = min((uint32_t)c, max((t.lhi + 3) / 4, 1u) - 1);
+      const bool nl = mixed_nibble(t.plo), nh = mixed_nibble(t.phi);
+      const uint32_t wl = load_u<uint16_t>(t.plo + (nl ? 2 * cl : cl));
+      const uint32_t wh = load_u<uint16_t>(t.phi + (nh ? 2 * ch : ch));
+      x = nl ? unpack8n(wl).x : unpack8(wl).x;
+      y = nh ? unpack8n(wh).x : unpack8(wh).x;
     } else if (packed) {  // 1 byte per 4 codes (records: inside the data field)
       uint32_t cl = (uint32_t)c, ch = (uint32_t)c;
       if (packed == SWK_PACK_STREAM) {
@@ -450,7 +465,21 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint3
     return;
   }
   const uint32_t j0 = (uint32_t)c * 8;
-  if (packed == SWK_PACK_NIBBLE) {  // 4-bit stream, 4 bytes per 8 codes, clamped like below
+  if (MIX && packed == SWK_PACK_MIXED) {  // per target: 4-bit at an odd address, else 2-bit
+    // (a 2-bit chunk reads 4 bytes for its 2: the rest is the next target's or the 16 zero
+    // bytes the host writes after the last)
+    const uint32_t cl = min((uint32_t)c, max((t.llo + 7) / 8, 1u) - 1);
+    const uint32_t ch = min((uint32_t)c, max((t.lhi + 7) / 8, 1u) - 1);
+    const bool nl = mixed_nibble(t.plo), nh = mixed_nibble(t.phi);
+    const uint32_t wl = load_u<uint32_t>(t.plo + (nl ? 4 * cl : 2 * cl));
+    const uint32_t wh = load_u<uint32_t>(t.phi + (nh ? 4 * ch : 2 * ch));
+    lo = nl ? unpack8n(wl) : unpack8(wl);
+    hi = nh ? unpack8n(wh) : unpack8(wh);
+    if (!full) {
+      lo = pad_tail(lo, j0, t.llo, pad);
+      hi = pad_tail(hi, j0, t.lhi, pad);
+    }
+  } else if (packed == SWK_PACK_NIBBLE) {  // 4-bit stream, 4 bytes per 8 codes, clamped like below
     const uint32_t cl = min((uint32_t)c, max((t.llo + 7) / 8, 1u) - 1);
     const uint32_t ch = min((uint32_t)c, max((t.lhi + 7) / 8, 1u) - 1);
     lo = unpack8n(load_u<uint32_t>(t.plo + 4 * cl));
@@ -500,6 +529,7 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint3
 // records {u32 ID, u16 length, u8 data[58]} (aligner_Header.h:19-24).
 // idx (optional): position k of the batch is target idx[k] (the u16 re-score of the pairs an
 // optimistic f16 pass flagged).
+template <bool MIX = true>
 __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t* offs,
                                               const uint32_t* lens, size_t n, int tile, int lane,
                                               uint32_t packed, const uint32_t* idx,
@@ -543,8 +573,12 @@ __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t
   t.llo = va ? la : 0u;
   t.lhi = vb ? lb : 0u;
   // an empty target still needs a readable address for the branch-free slow path
-  t.plo = la ? res + offs[a] : reinterpret_cast<const uint8_t*>(lens);
-  t.phi = lb ? res + offs[b] : reinterpret_cast<const uint8_t*>(lens);
+  // (SWK_PACK_MIXED: u32 offsets; an empty target's even address reads as 2-bit)
+  const uint32_t* o32 = reinterpret_cast<const uint32_t*>(offs);
+  const uint64_t oa = MIX && packed == SWK_PACK_MIXED ? o32[a] : offs[a];
+  const uint64_t ob = MIX && packed == SWK_PACK_MIXED ? o32[b] : offs[b];
+  t.plo = la ? res + oa : reinterpret_cast<const uint8_t*>(lens);
+  t.phi = lb ? res + ob : reinterpret_cast<const uint8_t*>(lens);
   return t;
 }
 
@@ -782,7 +816,6 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int snc = (int)a.nsc;
   int scur = -1, st0 = 0;
   uint32_t scn = 0, sro_lo = 0, sro_hi = 0, smode = SWK_PACK_STREAM;
-  bool sabort = false;  // the current chunk was released as aborted
   // ragged streamed batches (ulen == 0): a chunk's region is offsets u64 | lengths u32 | visiting
   // order u32 (scn each) | codes at the next 16-byte boundary; the order of the chunk of the tile
   // this wave is scoring (wperm, its first tile wst0) maps score positions to targets
@@ -808,27 +841,27 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       sro_lo = __builtin_amdgcn_readfirstlane(ssc[c].res_off_lo);
       sro_hi = __builtin_amdgcn_readfirstlane(ssc[c].res_off_hi);
       const uint32_t md = stream_mode(a.hflag, a.dflag, c, snc, lane);
-      sabort = md == SWK_STREAM_ABORT;
       smode = md == SWK_PACK_NIBBLE ? SWK_PACK_NIBBLE : SWK_PACK_STREAM;
+      if (md == SWK_STREAM_ABORT && a.ulen == 0) {
+        // a ragged chunk that never landed (the host re-runs the call): its region may hold
+        // anything, so it is read from the zeroed region instead (empty targets, scores in
+        // order; uniform chunks read their own region as codes, always in bounds)
+        const uint64_t z = (uint64_t)__builtin_amdgcn_readfirstlane(ssc[c].zero_off256) * 256u;
+        sro_lo = (uint32_t)z;
+        sro_hi = (uint32_t)(z >> 32);
+      }
     }
     pk = smode;
-    if (sabort) {  // a chunk that never landed (the host re-runs the call): its region may
-      cperm = nullptr;  // hold anything, so its targets read as empty and scores go in order
-      Lane2 e;
-      e.llo = e.lhi = 0u;
-      e.plo = e.phi = a.res;
-      return e;
-    }
     const uint8_t* base = a.res + ((size_t)sro_hi << 32 | sro_lo);
     if (a.ulen == 0) {  // ragged: the chunk's own offsets, lengths and order
       const uint64_t* co = reinterpret_cast<const uint64_t*>(base);
       const uint32_t* cl = reinterpret_cast<const uint32_t*>(base + 8 * (size_t)scn);
       cperm = cl + scn;
-      return lane_targets(base + (((size_t)scn * 16 + 15) & ~(size_t)15), co, cl, scn, t - st0,
-                          lane, pk, cperm, 0u, 0u);
+      return lane_targets<false>(base + (((size_t)scn * 16 + 15) & ~(size_t)15), co, cl, scn,
+                                 t - st0, lane, pk, cperm, 0u, 0u);
     }
-    return lane_targets(base, nullptr, nullptr, scn, t - st0, lane, pk, nullptr, a.ulen,
-                        pk == SWK_PACK_NIBBLE ? (a.ulen + 1) / 2 : (a.ulen + 3) / 4);
+    return lane_targets<false>(base, nullptr, nullptr, scn, t - st0, lane, pk, nullptr, a.ulen,
+                               pk == SWK_PACK_NIBBLE ? (a.ulen + 1) / 2 : (a.ulen + 3) / 4);
   };
 
   // MQ order: row LUTs query-major (q = unit / ntiles; a wave reloads its LUT SGPRs when the
@@ -848,7 +881,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     wperm = cperm;
     wst0 = st0;
   } else {
-    cur = lane_targets(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen, a.ustride);
+    cur = lane_targets<!MQ>(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen,
+                            a.ustride);
   }
   int nch, nfull;
   tile_chunks<C>(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
@@ -904,7 +938,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   u16x2 best = {0, 0};
   u16x2 prevUpH = H0;  // H(row above, column -1)
   uint2 rlo, rhi;      // raw codes of the next chunk (prefetched one phase ahead)
-  load_raw<C>(cur, 0, nfull > 0, a.pad, packed, rlo, rhi);
+  load_raw<C, !STREAM && !MQ>(cur, 0, nfull > 0, a.pad, packed, rlo, rhi);
   if (STREAM && threadIdx.x == 0) sq[W] = total;
   __syncthreads();
 
@@ -994,15 +1028,15 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         }
       }
       if (!last) {
-        load_raw<C>(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
+        load_raw<C, !STREAM && !MQ>(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
       } else if (nunit < nunits) {  // first chunk of the next tile
         if constexpr (STREAM) cur = stream_tile(ntile, packed_n);
         else
-          cur = lane_targets(a.res, a.offs, a.lens, n, ntile, lane, packed, idx, a.ulen,
-                             a.ustride);
+          cur = lane_targets<!MQ>(a.res, a.offs, a.lens, n, ntile, lane, packed, idx, a.ulen,
+                                  a.ustride);
         tile_chunks<C>(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
                     n, nch_n, nfull_n);
-        load_raw<C>(cur, 0, nfull_n > 0, a.pad, STREAM ? packed_n : packed, rlo, rhi);
+        load_raw<C, !STREAM && !MQ>(cur, 0, nfull_n > 0, a.pad, STREAM ? packed_n : packed, rlo, rhi);
       }
       const int slot = g & 1;
       // next chunk's boundary row (never past the last unit's edge rows)

@@ -24,6 +24,47 @@ void u16_gotoh_rows(const sw_bank* b, bool f16, int& R, int& W) {
   W = std::max(1, (int)((b->query.size() + 15) / 16));
 }
 
+// The tile / wave choice for n targets of at most max_len codes in the given arithmetic
+// (before the layout constraints launch() adds).
+bool wave_preferred(const sw_bank* b, size_t n, uint32_t max_len, bool use_f16) {
+  const size_t nseg = b->segs.size();
+  const size_t ntiles = (n + SWB_TILE - 1) / SWB_TILE;
+  const bool gotoh = b->cfg.gap_model == SW_GAP_GOTOH;
+  // Kernel choice by a throughput model calibrated on MI355X (scripts/kernel_choice.py):
+  //  tile kernel: base rate x fraction of the 256 CUs holding a tile x f(waves per SIMD),
+  //    f = min(1, 0.45 + 0.15 w), x 0.85 when the query runs as several segments;
+  //  wave kernel (queries <= 1024 rows): base rate x row fill (query / 64K lanes' rows) x
+  //    column fill (L / (L + 63): the 63-step skew of the lane pipeline).
+  // Base GCUPS: tile f16 merged 9000 (profile 8000), f16 Gotoh 8500 with the letter-pair
+  // table (7500 row LUT, profile 7100), u16
+  // merged 7400 (profile 6500), u16 Gotoh 5800 (profile 5600); wave f16 merged 8600
+  // (profile 7700), f16 Gotoh 7800 (profile 6800), u16 merged 7600 (profile 6600), u16 Gotoh
+  // 6100 (profile 5200).  SWBANK_KERNEL=tile|wave forces one.
+  const double tiles = (double)ntiles, W = b->segs[0].W;
+  const double cu_frac = std::min(1.0, tiles / 256.0);
+  const double wps = std::min(4.0, std::max(1.0, std::ceil(tiles / 256.0)) * W / 4.0);
+  const bool pair_tab = use_f16 && b->pair_bytes != 0 && env_int("SWBANK_PAIR", 1) != 0;
+  const double tile_base = use_f16 ? (gotoh ? (b->prof ? 7100 : pair_tab ? 8500 : 7500)
+                                            : (b->prof ? 8000 : 9000))
+                                   : (gotoh ? (b->prof ? 5600 : 5800) : (b->prof ? 6500 : 7400));
+  const double tile_est = tile_base * cu_frac * std::min(1.0, 0.45 + 0.15 * wps) *
+                          (nseg > 1 ? 0.85 : 1.0);
+  double wave_est = 0;
+  if (b->wK > 0) {
+    const double rowfill = (double)b->query.size() / (64.0 * b->wK * b->wsegs);
+    const double colfill = max_len / (max_len + 63.0);
+    const double wave_base = use_f16 ? (gotoh ? (b->prof ? 6800 : 7800) : (b->prof ? 7700 : 8600))
+                                     : (gotoh ? (b->prof ? 5200 : 6100) : (b->prof ? 6600 : 7600));
+    wave_est = wave_base * rowfill * colfill *
+               (b->wsegs > 1 ? 0.9 : 1.0);
+  }
+  const char* kforce = std::getenv("SWBANK_KERNEL");
+  bool use_wave = b->wK > 0 && wave_est > tile_est;
+  if (kforce && std::strcmp(kforce, "tile") == 0) use_wave = false;
+  if (kforce && std::strcmp(kforce, "wave") == 0 && b->wK > 0) use_wave = true;
+  return use_wave;
+}
+
 // packed (SWK_PACK_*): RECORDS: d_res holds n 64-byte CAPI records (2-bit codes), d_offs and
 // d_lens are unused; STREAM: 2-bit codes, d_offs in bytes (the host feeder's DNA chunks).
 // perm/perm_n (optional, tile kernel): pass 0 visits the targets in the order perm[0..n)
@@ -81,38 +122,8 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   const bool opt16 = f16_ok && !exact16 && env_int("SWBANK_F16_OPT", 1) != 0 &&
                      n <= 0xFFFFFFFFull;  // the re-score list holds 32-bit target numbers
   const bool use_f16 = exact16 || opt16;
-  // Kernel choice by a throughput model calibrated on MI355X (scripts/kernel_choice.py):
-  //  tile kernel: base rate x fraction of the 256 CUs holding a tile x f(waves per SIMD),
-  //    f = min(1, 0.45 + 0.15 w), x 0.85 when the query runs as several segments;
-  //  wave kernel (queries <= 1024 rows): base rate x row fill (query / 64K lanes' rows) x
-  //    column fill (L / (L + 63): the 63-step skew of the lane pipeline).
-  // Base GCUPS: tile f16 merged 9000 (profile 8000), f16 Gotoh 8500 with the letter-pair
-  // table (7500 row LUT, profile 7100), u16
-  // merged 7400 (profile 6500), u16 Gotoh 5800 (profile 5600); wave f16 merged 8600
-  // (profile 7700), f16 Gotoh 7800 (profile 6800), u16 merged 7600 (profile 6600), u16 Gotoh
-  // 6100 (profile 5200).  SWBANK_KERNEL=tile|wave forces one.
-  const double tiles = (double)ntiles, W = b->segs[0].W;
-  const double cu_frac = std::min(1.0, tiles / 256.0);
-  const double wps = std::min(4.0, std::max(1.0, std::ceil(tiles / 256.0)) * W / 4.0);
-  const bool pair_tab = use_f16 && b->pair_bytes != 0 && env_int("SWBANK_PAIR", 1) != 0;
-  const double tile_base = use_f16 ? (gotoh ? (b->prof ? 7100 : pair_tab ? 8500 : 7500)
-                                            : (b->prof ? 8000 : 9000))
-                                   : (gotoh ? (b->prof ? 5600 : 5800) : (b->prof ? 6500 : 7400));
-  const double tile_est = tile_base * cu_frac * std::min(1.0, 0.45 + 0.15 * wps) *
-                          (nseg > 1 ? 0.85 : 1.0);
-  double wave_est = 0;
-  if (b->wK > 0) {
-    const double rowfill = (double)b->query.size() / (64.0 * b->wK * b->wsegs);
-    const double colfill = max_len / (max_len + 63.0);
-    const double wave_base = use_f16 ? (gotoh ? (b->prof ? 6800 : 7800) : (b->prof ? 7700 : 8600))
-                                     : (gotoh ? (b->prof ? 5200 : 6100) : (b->prof ? 6600 : 7600));
-    wave_est = wave_base * rowfill * colfill *
-               (b->wsegs > 1 ? 0.9 : 1.0);
-  }
-  const char* kforce = std::getenv("SWBANK_KERNEL");
-  bool use_wave = b->wK > 0 && wave_est > tile_est;
-  if (kforce && std::strcmp(kforce, "tile") == 0) use_wave = false;
-  if (kforce && std::strcmp(kforce, "wave") == 0 && b->wK > 0) use_wave = true;
+  bool use_wave = wave_preferred(b, n, max_len, use_f16);
+  if (packed == SWK_PACK_MIXED) use_wave = false;  // (the feeder's mixed chunks: tile kernel)
   // the f16 wave kernel carries profile offsets in 16-bit halves (24 letters + pad fit)
   if (use_f16 && b->prof && (size_t)(b->alpha + 1) * b->wPS16 > 65536) use_wave = false;
   const char* arith = opt16 ? "f16+u16-rescore" : use_f16 ? "f16" : "u16";

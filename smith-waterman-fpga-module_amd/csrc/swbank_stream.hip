@@ -50,20 +50,24 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   tile0.push_back(T);
   const size_t nib = (L + 1) / 2;  // 4-bit bytes per target (the 2-bit stream needs fewer)
   std::vector<size_t> roff(nsc + 1, 0);
-  size_t slot_bytes = 0;
+  size_t slot_bytes = 0, zbytes = 0;
   for (size_t i = 0; i < nsc; ++i) {
     const size_t cnt = std::min(n, tile0[i + 1] * SWB_TILE) - tile0[i] * SWB_TILE;
     const size_t head = rlens ? align16(cnt * 16) : 0;  // ragged: offsets | lengths | order
     roff[i + 1] = roff[i] + (head + cnt * nib + 64 + 255) / 256 * 256;
     slot_bytes = std::max(slot_bytes, roff[i + 1] - roff[i]);
+    zbytes = std::max(zbytes, head + 64);
   }
+  // ragged: a zeroed region after the chunks, which the kernel reads instead of a chunk the
+  // host never sent (released as aborted: its own region may hold anything)
+  if (!rlens) zbytes = 0;
   // Memory the streamed call keeps for the bank's lifetime: the batch's 4-bit codes on the
   // device (sbuf), NSLOT pinned host slots of the largest chunk (<= 1/8 of it each) and the
   // batch's scores in coherent host memory.  Past SWBANK_STREAM_MB (default 4096 MiB of device
   // codes + host scores), or when any of it cannot be allocated, the call runs through the
   // chunked feeder, whose slots are bounded by chunk_target() (counted: stream_declined).
   const size_t cap_bytes = (size_t)std::max(1, env_int("SWBANK_STREAM_MB", 4096)) << 20;
-  if (roff[nsc] + n * 4 > cap_bytes) {
+  if (roff[nsc] + zbytes + n * 4 > cap_bytes) {
     ++b->ctr.stream_declined;
     return SW_OK;
   }
@@ -80,7 +84,8 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   }
   hipStream_t ks = b->kstream;
   {
-    bool ok = b->sbuf.reserve(roff[nsc]) == hipSuccess && b->sflag.reserve(nsc * 4) == hipSuccess &&
+    bool ok = b->sbuf.reserve(roff[nsc] + zbytes) == hipSuccess &&
+              b->sflag.reserve(nsc * 4) == hipSuccess &&
               b->sdrec.reserve(nsc) == hipSuccess && b->sctr.reserve(1) == hipSuccess &&
               b->srec.reserve(nsc * sizeof(SwkStreamChunk)) == hipSuccess &&
               b->shflag.reserve(nsc * 8) == hipSuccess &&  // layout words | abort words
@@ -104,7 +109,8 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   SwkStreamChunk* rec = reinterpret_cast<SwkStreamChunk*>(b->srec.p);
   uint32_t* hflag = reinterpret_cast<uint32_t*>(b->shflag.p);
   for (size_t i = 0; i < nsc; ++i) {
-    rec[i] = SwkStreamChunk{(unsigned)tile0[i], (unsigned)roff[i], (unsigned)(roff[i] >> 32), 0u};
+    rec[i] = SwkStreamChunk{(unsigned)tile0[i], (unsigned)roff[i], (unsigned)(roff[i] >> 32),
+                            (unsigned)(roff[nsc] / 256)};
     __atomic_store_n(&hflag[i], 0u, __ATOMIC_RELAXED);
     __atomic_store_n(&hflag[nsc + i], 0u, __ATOMIC_RELAXED);
   }
@@ -120,6 +126,7 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                             ks));
     HIPOK(b, hipMemsetAsync(b->sflag.p, 0, nsc * 4, ks));
     HIPOK(b, hipMemsetAsync(b->sctr.p, 0, 4, ks));
+    if (zbytes) HIPOK(b, hipMemsetAsync(b->sbuf.p + roff[nsc], 0, zbytes, ks));
     if (b->timing) {
       HIPOK(b, hipEventCreate(&ev.a));
       HIPOK(b, hipEventCreate(&ev.b));

@@ -206,3 +206,60 @@ def test_feeder_uniform_chunks(monkeypatch, case):
     else:
         want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(*REF[:2]), *REF[2:])
     assert np.array_equal(got[sel], want), kern
+
+
+@pytest.mark.parametrize("case", ["sparse-n", "dense-n", "no-n", "tiny", "one-tile", "gotoh",
+                                  "long-query"])
+def test_feeder_mixed_chunks(monkeypatch, poisoned_buffers, case):
+    """Ragged DNA chunks as SWK_PACK_MIXED: each target in 2-bit codes from an even byte, or in
+    4-bit codes from an odd byte when it holds an N, u32 offsets, the longest-first order
+    sorted on the device after the codes.  Equal to the whole-chunk layouts (SWBANK_MIXED=0)
+    and to the oracle; the counter shows the chunks took the mixed layout."""
+    monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
+    monkeypatch.setenv("SWBANK_KERNEL", "tile")
+    rng = np.random.default_rng(len(case) * 13)
+    n, lo, hi = {"tiny": (20_000, 0, 9), "one-tile": (100, 0, 300)}.get(case, (30_000, 1, 250))
+    res, offs, lens = _ragged(rng, n, lo, hi)
+    p_n = {"sparse-n": 0.001, "dense-n": 0.05, "no-n": 0.0, "tiny": 0.02}.get(case, 0.003)
+    res[rng.random(res.size) < p_n] = 4
+    qlen = 700 if case == "long-query" else 100
+    q = rng.integers(0, 4, qlen, dtype=np.uint8)
+    for k in range(0, n, 97):  # homologs (high scores, long gapped alignments)
+        m = min(int(lens[k]), qlen)
+        res[int(offs[k]):int(offs[k]) + m] = q[:m]
+    gotoh = case == "gotoh"
+    params = (5, -4, -10, -1) if gotoh else REF
+    with S.ScoreBank(gap_model=S.GAP_GOTOH if gotoh else S.GAP_MERGED) as bank:
+        bank.set_penalties(*params)
+        bank.load_query(q)
+        got = bank.score_batch(res, offs, lens)
+        mixed = bank.counters()["mixed_chunks"]
+        monkeypatch.setenv("SWBANK_MIXED", "0")
+        ref = bank.score_batch(res, offs, lens)
+        assert bank.counters()["mixed_chunks"] == mixed
+    assert mixed >= 1, case
+    assert np.array_equal(got, ref), np.nonzero(got != ref)[0][:8]
+    sel = np.unique(np.concatenate([rng.choice(n, min(n, 700), replace=False),
+                                    np.arange(0, n, 97), np.arange(max(0, n - 130), n)]))
+    sub = [res[int(offs[k]):int(offs[k]) + int(lens[k])] for k in sel]
+    want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(*params[:2]), *params[2:],
+                         O.GAP_GOTOH if gotoh else O.GAP_MERGED)
+    assert np.array_equal(got[sel], want)
+
+
+def test_feeder_mixed_bad_code(monkeypatch):
+    """A code outside the alphabet in a mixed chunk: the byte path reports the target."""
+    monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
+    rng = np.random.default_rng(5)
+    res, offs, lens = _ragged(rng, 30_000, 5, 200)
+    res[rng.random(res.size) < 0.002] = 4
+    k = 20_000
+    bad = res.copy()
+    bad[int(offs[k]) + 1] = 9
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(rng.integers(0, 4, 100, dtype=np.uint8))
+        with pytest.raises(S.SwbankError) as ei:
+            bank.score_batch(bad, offs, lens)
+        assert ei.value.status == S.ERR_ARG and f"target {k}" in str(ei.value)
+        assert (bank.score_batch(res, offs, lens) >= 0).all()
