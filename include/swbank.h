@@ -217,8 +217,9 @@ sw_status sw_bank_timing(sw_bank *bank, uint64_t *launches, double *pack_ms, dou
  * devices'), so silent slow paths show: host calls that ran as one streamed kernel, streamed
  * calls re-run through the chunked feeder because a chunk's wait ran out, streamed calls
  * declined for the memory cap (SWBANK_STREAM_MB) or a failed allocation, chunked host calls,
- * device-side length sorts, multi-device gathers abandoned after their time limit, and chunks
- * of chunked calls sent as mixed 2-bit / 4-bit codes (ragged DNA). */
+ * device-side length sorts, multi-device gathers abandoned after their time limit, chunks
+ * of chunked calls sent as mixed 2-bit / 4-bit codes (ragged DNA), and the pool parts of those
+ * chunks packed as one run (targets back to back in the caller's residues). */
 typedef struct sw_counters {
   uint64_t stream_calls;
   uint64_t stream_reruns;
@@ -227,6 +228,7 @@ typedef struct sw_counters {
   uint64_t device_sorts;
   uint64_t gather_timeouts;
   uint64_t mixed_chunks;
+  uint64_t mixed_runs;
 } sw_counters;
 sw_status sw_bank_counters(const sw_bank *bank, sw_counters *out);
 

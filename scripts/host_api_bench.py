@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--no-records", action="store_true")
     ap.add_argument("--n-frac", type=float, default=0.0,
                     help="fraction of residues set to N (the feeder then sends 4-bit chunks)")
+    ap.add_argument("--bench-ragged", action="store_true",
+                    help="bench.py's ragged shape: lengths uniform in [64, 150], 0.1%% N")
     args = ap.parse_args()
     import swbank as S
     from oracle import oracle as O
@@ -38,6 +40,10 @@ def main():
     res = O.random_codes(2, int(lens.sum()), 4)
     if args.n_frac > 0:
         res[rng.random(res.size) < args.n_frac] = 4
+    if args.bench_ragged:
+        from bench import ragged_batch
+        res, offs, lens = ragged_batch(1000, n)
+        args.ragged = True
     cells = float(args.qlen) * float(lens.sum())
     out = {"n": n, "L": L, "qlen": args.qlen, "ragged": args.ragged, "n_frac": args.n_frac}
     with S.ScoreBank(device=0) as bank:

@@ -94,13 +94,12 @@ struct PhaseTrace {
   const char* path = std::getenv("SWBANK_TRACE_FILE");
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
   std::vector<std::pair<const char*, double>> marks;
-  void mark(const char* what) {
-    if (path)
-      marks.push_back({what, std::chrono::duration<double, std::micro>(
-                                 std::chrono::steady_clock::now() - t0).count()});
-  }
+  std::mutex mu;  // (the feeder's launch thread marks too)
+  void mark(const char* what) { mark_at(what, std::chrono::steady_clock::now()); }
   void mark_at(const char* what, std::chrono::steady_clock::time_point t) {
-    if (path) marks.push_back({what, std::chrono::duration<double, std::micro>(t - t0).count()});
+    if (!path) return;
+    std::lock_guard<std::mutex> g(mu);
+    marks.push_back({what, std::chrono::duration<double, std::micro>(t - t0).count()});
   }
   ~PhaseTrace() {
     if (!path || marks.empty()) return;
@@ -193,6 +192,11 @@ struct PinBuf {
   }
 };
 
+inline bool spin_yield() {
+  static const bool y = env_int("SWBANK_SPIN_YIELD", 0) != 0;
+  return y;
+}
+
 // Host worker threads for the host-buffer feeder (gather / scatter of a chunk): run(f) calls
 // f(part) for part = 0..size()-1, part 0 on the calling thread, and returns when all are done.
 // A host-API call runs several short jobs per chunk back to back, so idle workers spin on the
@@ -226,22 +230,26 @@ class HostPool {
     }
     cv_.notify_all();
     f(0);
-    while (pending_.load(std::memory_order_acquire) != 0) relax();
+    for (unsigned it = 1; pending_.load(std::memory_order_acquire) != 0; ++it) relax(it);
     job_ = nullptr;
   }
 
  private:
-  static void relax() {
+  // SWBANK_SPIN_YIELD=1: a spinning thread yields its core every 64 polls (meant for the
+  // occasional 8-10 ms calls, a preempted worker or launch thread being one suspect; A/B on the
+  // box did not remove them, so off by default)
+  static void relax(unsigned it) {
 #if defined(__SSE2__)
     _mm_pause();
 #endif
+    if ((it & 63) == 0 && spin_yield()) std::this_thread::yield();
   }
   void loop(unsigned i) {
     uint64_t seen = 0;
     for (;;) {
       const auto t0 = std::chrono::steady_clock::now();
       for (unsigned it = 1; gen_.load(std::memory_order_acquire) == seen; ++it) {
-        relax();
+        relax(it);
         if ((it & 255) == 0 &&
             std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
           std::unique_lock<std::mutex> l(m_);
@@ -262,6 +270,78 @@ class HostPool {
   std::atomic<unsigned> pending_{0};
   std::atomic<uint64_t> gen_{0};
   std::atomic<bool> stop_{false};
+};
+
+// The host feeder's launch thread: runs the HIP work of each chunk (its copy, the score
+// launches, the scores' return) in posting order while the caller's thread and the pool gather
+// the next chunk -- the chunk's ~11 HIP calls (30-60 us) were on the gather's critical path.
+// It sleeps on a condition variable between jobs (a spinning thread next to the pool's workers
+// would take a core from the gather); the caller spins in wait(k) for the first k jobs to be
+// done.  The first failing job's status sticks (later jobs are skipped) until reset().
+class Launcher {
+ public:
+  explicit Launcher(int device) : th_([this, device] { loop(device); }) {}
+  ~Launcher() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_one();
+    th_.join();
+  }
+  void post(std::function<sw_status()> f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(std::move(f));
+      ++posted_;
+    }
+    cv_.notify_one();
+  }
+  // spins until the first k posted jobs ran; their status
+  sw_status wait(size_t k) {
+    for (unsigned it = 1; done_.load(std::memory_order_acquire) < k; ++it) {
+#if defined(__SSE2__)
+      _mm_pause();
+#endif
+      if ((it & 63) == 0 && spin_yield()) std::this_thread::yield();
+    }
+    return st_.load(std::memory_order_acquire);
+  }
+  sw_status wait_all() { return wait(posted_); }  // (posted_ is the caller's own count)
+  void reset() {  // between calls, all jobs done
+    wait_all();
+    posted_ = 0;
+    done_.store(0);
+    st_.store(SW_OK);
+  }
+
+ private:
+  void loop(int device) {
+    (void)hipSetDevice(device);
+    for (;;) {
+      std::function<sw_status()> f;
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;  // stop_
+        f = std::move(q_.front());
+        q_.erase(q_.begin());
+      }
+      if (st_.load(std::memory_order_relaxed) == SW_OK) {
+        const sw_status s = f();
+        if (s != SW_OK) st_.store(s, std::memory_order_release);
+      }
+      done_.fetch_add(1, std::memory_order_acq_rel);
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::vector<std::function<sw_status()>> q_;
+  bool stop_ = false;
+  size_t posted_ = 0;  // (the posting thread's count)
+  std::atomic<size_t> done_{0};
+  std::atomic<sw_status> st_{SW_OK};
+  std::thread th_;  // last: started after the fields it reads
 };
 
 struct sw_bank {
@@ -337,22 +417,25 @@ struct sw_bank {
   DevBuf<uint32_t> stab[2], stab16[2];
   DevBuf<uint2> sring;
 
-  // host-buffer feeder (sw_score_batch / sw_score_records): NSLOT pinned staging slots and
-  // device slots, chunk i gathered on the host while chunk i-1 crosses PCIe on copy_stream
-  // and chunk i-2 is scored on `stream`
-  static constexpr int NSLOT = 3;
+  // host-buffer feeder (sw_score_batch / sw_score_records): NSLOT pinned staging slots, chunk
+  // i gathered on the host while chunk i-1 crosses PCIe on copy_stream and earlier chunks are
+  // scored on `stream` / stream2; NDSLOT device slots (chunk i's copy waits for the kernel of
+  // chunk i - NDSLOT only: with NSLOT device slots too, the copies trailed the kernels)
+  static constexpr int NSLOT = 3, NDSLOT = 6;
   hipStream_t copy_stream = nullptr;
-  hipEvent_t h2d_done[NSLOT] = {}, kern_done[NSLOT] = {};
+  hipEvent_t h2d_done[NSLOT] = {}, kern_done[NDSLOT] = {};
   PinBuf hslot[NSLOT], hscores;
   std::vector<std::vector<uint32_t>> mlist;  // per pool part: a mixed chunk's 4-bit targets
   std::vector<std::vector<uint8_t>> mstage;  // ... and their codes, packed while gathering
+  std::vector<std::vector<uint32_t>> mbad;   // ... a run block's positions of codes past 3
   std::vector<hipEvent_t> out_ev;  // per chunk: its scores are back in hscores
   hipStream_t out_stream = nullptr;  // scores back to the host, beside the next chunk's kernel
   hipStream_t stream2 = nullptr;     // odd chunks' kernels (scratch-free launches overlap)
   hipEvent_t ev_s2 = nullptr;
   double host_pack_ms = 0;         // feeder gather time of host calls (with timing on)
-  DevBuf<uint8_t> dslot[NSLOT];
-  DevBuf<uint32_t> sortscr[NSLOT];  // device sort scratch of each slot's chunk
+  int feed_dslots = NSLOT;         // device slots of the current feeder call
+  DevBuf<uint8_t> dslot[NDSLOT];
+  DevBuf<uint32_t> sortscr[NDSLOT];  // device sort scratch of each device slot's chunk
   // streamed host batches (one kernel for the whole call, equal-length DNA): the batch's codes
   // (chunks 256-byte aligned: no cache line holds two chunks, and nothing of a chunk is read
   // before its layout word is set, so no line is cached before its copy landed), the chunks'
@@ -370,6 +453,7 @@ struct sw_bank {
   PinBuf shscores{hipHostMallocCoherent};  // the streamed kernel writes the scores here
   std::vector<hipEvent_t> sev;
   std::unique_ptr<HostPool> pool;
+  std::unique_ptr<Launcher> launcher;  // the feeder's launch thread (SWBANK_LAUNCHER=0: none)
 
   // workspaces
   DevBuf<uint8_t> res;

@@ -189,8 +189,8 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   if (b->out_stream) (void)hipStreamSynchronize(b->out_stream);
   if (b->stream2) (void)hipStreamSynchronize(b->stream2);
   for (hipEvent_t e : b->out_ev) (void)hipEventDestroy(e);
-  for (int i = 0; i < sw_bank::NSLOT; ++i) {
-    b->hslot[i].release();
+  for (int i = 0; i < sw_bank::NSLOT; ++i) b->hslot[i].release();
+  for (int i = 0; i < sw_bank::NDSLOT; ++i) {
     b->dslot[i].release();
     b->sortscr[i].release();
   }
@@ -202,11 +202,12 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->shflag.release();
   b->shscores.release();
   for (hipEvent_t e : b->sev) (void)hipEventDestroy(e);
-  for (int i = 0; i < sw_bank::NSLOT; ++i) {
+  for (int i = 0; i < sw_bank::NSLOT; ++i)
     if (b->h2d_done[i]) (void)hipEventDestroy(b->h2d_done[i]);
+  for (int i = 0; i < sw_bank::NDSLOT; ++i)
     if (b->kern_done[i]) (void)hipEventDestroy(b->kern_done[i]);
-  }
   b->hscores.release();
+  b->launcher.reset();
   b->pool.reset();
   if (b->copy_stream) (void)hipStreamDestroy(b->copy_stream);
   if (b->out_stream) (void)hipStreamDestroy(b->out_stream);
@@ -244,6 +245,7 @@ extern "C" sw_status sw_bank_counters(const sw_bank* b, sw_counters* out) {
     out->device_sorts += k->ctr.device_sorts;
     out->gather_timeouts += k->ctr.gather_timeouts;
     out->mixed_chunks += k->ctr.mixed_chunks;
+    out->mixed_runs += k->ctr.mixed_runs;
   }
   return SW_OK;
 }

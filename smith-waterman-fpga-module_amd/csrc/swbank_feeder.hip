@@ -112,15 +112,17 @@ static sw_status feeder_init(sw_bank* b) {
   if (!b->pool) b->pool.reset(new (std::nothrow) HostPool(b->pool_threads ? b->pool_threads
                                                                           : host_threads()));
   if (!b->pool) return fail(b, SW_ERR_NOMEM, "host worker pool");
+  if (!b->launcher && env_int("SWBANK_LAUNCHER", 1) != 0)
+    b->launcher.reset(new (std::nothrow) Launcher(b->device));
   if (b->copy_stream) return SW_OK;
   HIPOK(b, hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
   HIPOK(b, hipStreamCreateWithFlags(&b->out_stream, hipStreamNonBlocking));
   HIPOK(b, hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
   HIPOK(b, hipEventCreateWithFlags(&b->ev_s2, hipEventDisableTiming));
-  for (int i = 0; i < sw_bank::NSLOT; ++i) {
+  for (int i = 0; i < sw_bank::NSLOT; ++i)
     HIPOK(b, hipEventCreateWithFlags(&b->h2d_done[i], hipEventDisableTiming));
+  for (int i = 0; i < sw_bank::NDSLOT; ++i)
     HIPOK(b, hipEventCreateWithFlags(&b->kern_done[i], hipEventDisableTiming));
-  }
   return SW_OK;
 }
 
@@ -147,10 +149,15 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   ++b->ctr.chunked_calls;
   size_t slot_bytes = 0;
   for (const Chunk& c : chunks) slot_bytes = std::max(slot_bytes, c.bytes);
-  for (int i = 0; i < std::min<int>(sw_bank::NSLOT, (int)chunks.size()); ++i) {
+  // device slots: NDSLOT while they take at most 1 GiB (SWBANK_DSLOTS overrides), else NSLOT
+  const int nds = std::max(1, std::min(sw_bank::NDSLOT,
+      env_int("SWBANK_DSLOTS", slot_bytes * sw_bank::NDSLOT <= ((size_t)1 << 30)
+                                   ? sw_bank::NDSLOT : sw_bank::NSLOT)));
+  b->feed_dslots = nds;
+  for (int i = 0; i < std::min<int>(sw_bank::NSLOT, (int)chunks.size()); ++i)
     HIPOK(b, b->hslot[i].reserve(slot_bytes));
+  for (int i = 0; i < std::min<int>(nds, (int)chunks.size()); ++i)
     HIPOK(b, b->dslot[i].reserve(slot_bytes));
-  }
   HIPOK(b, b->scores.reserve(n));
   if (out) {
     HIPOK(b, b->hscores.reserve(n * 4));
@@ -162,22 +169,53 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   }
   // overlapped chunk launches run two at a time: each takes at most SWBANK_CHUNK_OCC (2)
   // workgroups per CU, so a chunk's tiles are several per workgroup (less pipeline fill and
-  // drain per tile) and the two streams share the chip
-  struct OccCap {
-    explicit OccCap(int c) { swk_set_occ_cap(c); }
-    ~OccCap() { swk_set_occ_cap(0); }
-  } occ_cap(overlap ? std::max(0, env_int("SWBANK_CHUNK_OCC", 2)) : 0);
+  // drain per tile) and the two streams share the chip (a per-thread setting: set by the
+  // thread that launches)
+  const int occ = overlap ? std::max(0, env_int("SWBANK_CHUNK_OCC", 2)) : 0;
+  Launcher* lz = b->launcher.get();
+  if (lz) lz->reset();
   const auto fail_sync = [&](sw_status s) {
+    if (lz) lz->wait_all();
     (void)hipStreamSynchronize(b->stream);
     (void)hipStreamSynchronize(b->stream2);
     (void)hipStreamSynchronize(b->copy_stream);
     (void)hipStreamSynchronize(b->out_stream);
     return s;
   };
+  PhaseTrace* tr = g_trace;
+  // chunk i's HIP work: its copy once slot s is free, the score launches, the scores' return
+  const auto launch_chunk = [&, tr](size_t i, size_t from, size_t bytes) -> sw_status {
+    const int s = (int)(i % sw_bank::NSLOT), d = (int)(i % nds);
+    const Chunk& c = chunks[i];
+    if (i >= (size_t)nds) HIPOK(b, hipStreamWaitEvent(b->copy_stream, b->kern_done[d], 0));
+    HIPOK(b, hipMemcpyAsync(b->dslot[d].p + from, b->hslot[s].p + from, bytes - from,
+                            hipMemcpyHostToDevice, b->copy_stream));
+    HIPOK(b, hipEventRecord(b->h2d_done[s], b->copy_stream));
+    hipStream_t ks = overlap && (i & 1) ? b->stream2 : b->stream;
+    HIPOK(b, hipStreamWaitEvent(ks, b->h2d_done[s], 0));
+    // the last chunk has no later launch to share the chip with: the whole GPU
+    swk_set_occ_cap(i + 1 == chunks.size() ? 0 : occ);
+    const sw_status sst = score(b->dslot[d].p, c, b->scores.p + c.c0, ks);
+    swk_set_occ_cap(0);
+    if (sst != SW_OK) return sst;
+    if (tr) tr->mark("launched");
+    HIPOK(b, hipEventRecord(b->kern_done[d], ks));
+    if (out) {
+      HIPOK(b, hipStreamWaitEvent(b->out_stream, b->kern_done[d], 0));
+      HIPOK(b, hipMemcpyAsync(b->hscores.p + c.c0 * 4, b->scores.p + c.c0, (c.c1 - c.c0) * 4,
+                              hipMemcpyDeviceToHost, b->out_stream));
+      HIPOK(b, hipEventRecord(b->out_ev[i], b->out_stream));
+    }
+    return SW_OK;
+  };
   for (size_t i = 0; i < chunks.size(); ++i) {
     const int s = (int)(i % sw_bank::NSLOT);
     const Chunk& c = chunks[i];
-    if (i >= (size_t)sw_bank::NSLOT) HIPOK(b, hipEventSynchronize(b->h2d_done[s]));
+    if (i >= (size_t)sw_bank::NSLOT) {
+      // slot s is free once chunk i - NSLOT's copy (enqueued by the launch thread) landed
+      if (lz && (st = lz->wait(i - sw_bank::NSLOT + 1)) != SW_OK) return fail_sync(st);
+      HIPOK(b, hipEventSynchronize(b->h2d_done[s]));
+    }
     trace_mark("gather<");
     const auto t0 = std::chrono::steady_clock::now();
     size_t from = 0;  // leading slot bytes the device does not need (a uniform chunk's headers)
@@ -187,25 +225,12 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
       b->host_pack_ms +=
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (bytes == 0) return fail_sync(SW_ERR_ARG);
-    if (i >= (size_t)sw_bank::NSLOT)
-      HIPOK(b, hipStreamWaitEvent(b->copy_stream, b->kern_done[s], 0));
-    HIPOK(b, hipMemcpyAsync(b->dslot[s].p + from, b->hslot[s].p + from, bytes - from,
-                            hipMemcpyHostToDevice, b->copy_stream));
-    HIPOK(b, hipEventRecord(b->h2d_done[s], b->copy_stream));
-    hipStream_t ks = overlap && (i & 1) ? b->stream2 : b->stream;
-    HIPOK(b, hipStreamWaitEvent(ks, b->h2d_done[s], 0));
-    // the last chunk has no later launch to share the chip with: the whole GPU
-    if (overlap && i + 1 == chunks.size()) swk_set_occ_cap(0);
-    if ((st = score(b->dslot[s].p, c, b->scores.p + c.c0, ks)) != SW_OK) return fail_sync(st);
-    trace_mark("launched");
-    HIPOK(b, hipEventRecord(b->kern_done[s], ks));
-    if (out) {
-      HIPOK(b, hipStreamWaitEvent(b->out_stream, b->kern_done[s], 0));
-      HIPOK(b, hipMemcpyAsync(b->hscores.p + c.c0 * 4, b->scores.p + c.c0, (c.c1 - c.c0) * 4,
-                              hipMemcpyDeviceToHost, b->out_stream));
-      HIPOK(b, hipEventRecord(b->out_ev[i], b->out_stream));
-    }
+    if (lz)
+      lz->post([&launch_chunk, i, from, bytes] { return launch_chunk(i, from, bytes); });
+    else if ((st = launch_chunk(i, from, bytes)) != SW_OK)
+      return fail_sync(st);
   }
+  if (lz && (st = lz->wait_all()) != SW_OK) return fail_sync(st);
   if (overlap) {  // the bank stream (the multi-device gather, the next call) after stream2
     HIPOK(b, hipEventRecord(b->ev_s2, b->stream2));
     HIPOK(b, hipStreamWaitEvent(b->stream, b->ev_s2, 0));
@@ -396,6 +421,12 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   std::vector<size_t> mperm(chunks.size(), 0);  // a mixed chunk's sort order (device only)
   std::vector<size_t> part(T + 1), part2(T + 1), part4(T + 1), psz(T + 1);
   std::vector<uint32_t> partmax(T), partmin(T);
+  // mixed chunks: a part whose non-empty targets lie in ascending, non-overlapping order in the
+  // residues with gaps of at most 1/8 of its codes packs as ONE run from rbase[p] (rspan codes,
+  // gaps included); UINT64_MAX: one packer call per target.  SWBANK_MIXED_RUNS=0 disables.
+  std::vector<uint64_t> rbase(T), rspan(T);
+  const bool runs_ok = env_int("SWBANK_MIXED_RUNS", 1) != 0;
+  const swpack::PackRunFn runfn = swpack::run_packer(avx2);
   std::atomic<size_t> bad{SIZE_MAX}, oob{SIZE_MAX};
   std::atomic<uint32_t> wide{0};
   size_t gi = 0, si = 0;
@@ -414,21 +445,33 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     std::fill(psz.begin(), psz.end(), 0);
     oob = SIZE_MAX;
     pool.run([&](unsigned p) {
-      size_t acc = 0, acc2 = 0, acc4 = 0, acc2e = 0;
+      size_t acc = 0, acc2 = 0, acc4 = 0;
       uint32_t m = 0, mn = UINT32_MAX;
-      bool out = false;
+      bool out = false, mono = runs_ok;
+      uint64_t first = UINT64_MAX, end = 0;  // the run: first start, last end
       for (size_t k = c.c0 + std::min(cnt, p * step); k < c.c0 + std::min(cnt, (p + 1) * step);
            ++k) {
-        acc += lens[k];
-        acc2 += (lens[k] + 3) / 4;
-        acc2e += ((lens[k] + 3) / 4 + 1) & ~(size_t)1;  // (mixed: 2-bit targets on even bytes)
-        acc4 += (lens[k] + 1) / 2;
-        m = std::max(m, lens[k]);
-        mn = std::min(mn, lens[k]);
+        const uint32_t l = lens[k];
+        acc += l;
+        acc2 += (l + 3) / 4;
+        acc4 += (l + 1) / 2;
+        m = std::max(m, l);
+        mn = std::min(mn, l);
         // the target must lie inside the caller's residues (checked before any byte is read;
         // the pack passes below re-read this part's offsets from cache)
-        out |= offsets[k] > nres || lens[k] > nres - offsets[k];
+        out |= offsets[k] > nres || l > nres - offsets[k];
+        if (l) {
+          mono &= first == UINT64_MAX || offsets[k] >= end;
+          if (first == UINT64_MAX) first = offsets[k];
+          end = offsets[k] + l;
+        }
       }
+      const uint64_t span = first == UINT64_MAX ? 0 : end - first;
+      const bool run = mono && first != UINT64_MAX && !out && span <= acc + acc / 8 + 64 &&
+                       span < (1ull << 30);
+      rbase[p] = run ? first : UINT64_MAX;
+      rspan[p] = run ? span : 0;
+      const size_t acc2e = run ? (span + 3) / 4 : acc2;  // (mixed: this part's 2-bit bytes)
       if (out)
         for (size_t k = c.c0 + std::min(cnt, p * step); k < c.c0 + std::min(cnt, (p + 1) * step);
              ++k)
@@ -466,54 +509,95 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     const bool cf16 = f16_ok && (ctop <= 2048u || env_int("SWBANK_F16_OPT", 1) != 0);
     const size_t ca32 = align16(cnt * 8);
     if (mixed_ok && !uni && (host_dsort || cnt <= SWB_TILE) &&
-        ca32 + align16(part2[T] + part4[T] + 3 * cnt + 32) + align16(cnt * 4 + 8) <= c.bytes &&
-        !wave_preferred(b, cnt, chunk_max[gi], cf16)) {
-      // pass 1: every target in 2-bit codes at its even 2-bit position (sizes known up front);
-      // a target with a code past 3 is packed again at once in 4-bit codes into the part's
-      // staging buffer (its residues still in cache: scattered re-reads later were latency
-      // bound).  Pass 2: each part's staged 4-bit targets land as one block at an odd position
-      // after the 2-bit region (their 2-bit bytes stay unused)
+        ca32 + align16(psz[T] + part4[T] + 3 * cnt + 32) + align16(cnt * 4 + 8) <= c.bytes &&
+        psz[T] + part4[T] + 16 < (1ull << 29) && !wave_preferred(b, cnt, chunk_max[gi], cf16)) {
+      // pass 1: every target in 2-bit codes (offset word: its 2-bit position << 1, see
+      // SWK_PACK_MIXED) -- a part whose targets lie back to back in the residues as ONE run (one
+      // packer call per 16 Ki codes, the positions of codes past 3 reported), else one call per
+      // target.  A target with a code past 3 is packed again at once in 4-bit codes into the
+      // part's staging buffer (its residues still in cache: scattered re-reads later were
+      // latency bound).  Pass 2: each part's staged 4-bit targets land as one block after the
+      // 2-bit region (their 2-bit bytes stay unused), offset words (byte << 1) | 1
       uint32_t* so32 = reinterpret_cast<uint32_t*>(slot);
       uint32_t* sl32 = so32 + cnt;
       uint8_t* mcodes = slot + ca32;
       if (b->mlist.size() < T) b->mlist.resize(T);
       if (b->mstage.size() < T) b->mstage.resize(T);
+      if (b->mbad.size() < T) b->mbad.resize(T);
       std::vector<size_t> r4(T + 1, 0);  // staged 4-bit bytes per part
+      std::atomic<uint32_t> nruns{0};
       wide = 0;
       pool.run([&](unsigned p) {
         const size_t lo = std::min(cnt, p * step), hi = std::min(cnt, (p + 1) * step);
         // (list and stage live in this thread while they grow: the parts' vector headers
         // share cache lines)
-        std::vector<uint32_t> nl;
+        std::vector<uint32_t> nl, bad;
         std::vector<uint8_t> sg;
         nl.swap(b->mlist[p]);
         sg.swap(b->mstage[p]);
+        bad.swap(b->mbad[p]);
         nl.clear();
-        const size_t scap = part4[p + 1] - part4[p] + 2 * (hi - lo) + 64;
+        const size_t scap = part4[p + 1] - part4[p] + 64;
         if (sg.size() < scap) sg.resize(scap);
-        size_t at = psz[p], sat = 0;
+        size_t sat = 0;
         uint32_t mx = 0;
-        for (size_t i = lo; i < hi; ++i) {
+        const auto stage4 = [&](size_t i) {
           const size_t k = c.c0 + i;
           const uint32_t l = lens[k];
-          if (pack2fn(residues + offsets[k], l, mcodes + at, wide_ok(k, l, at, 8, psz[p + 1])) >
-              3u) {
-            mx = std::max(mx, pack4fn(residues + offsets[k], l, sg.data() + sat,
-                                      wide_ok(k, l, sat, 16, scap)));
-            nl.push_back((uint32_t)i);
-            sat += ((l + 1) / 2 + 1) & ~(size_t)1;
+          mx = std::max(mx, pack4fn(residues + offsets[k], l, sg.data() + sat,
+                                    wide_ok(k, l, sat, 16, scap)));
+          nl.push_back((uint32_t)i);
+          sat += (l + 1) / 2;
+        };
+        if (rbase[p] != UINT64_MAX) {
+          const uint64_t o0 = rbase[p], span = rspan[p];
+          const uint64_t pos0 = 4 * (uint64_t)psz[p];  // the run's first 2-bit position
+          for (size_t i = lo; i < hi; ++i) {
+            const size_t k = c.c0 + i;
+            so32[i] = lens[k] ? (uint32_t)((pos0 + offsets[k] - o0) << 1) : 0u;
+            sl32[i] = lens[k];
           }
-          so32[i] = (uint32_t)at;
-          sl32[i] = l;
-          at += ((l + 3) / 4 + 1) & ~(size_t)1;
+          // 16 Ki codes per packer call: the N targets of a block are re-packed while its
+          // residues are in cache; `cur` walks the targets (ascending, non-overlapping)
+          size_t cur = lo, marked = SIZE_MAX;
+          for (uint64_t x0 = 0; x0 < span; x0 += 16384) {
+            const uint64_t x1 = std::min<uint64_t>(span, x0 + 16384);
+            bad.clear();
+            runfn(residues + o0 + x0, (size_t)(x1 - x0), mcodes + psz[p] + x0 / 4, (uint32_t)x0,
+                  bad);
+            for (const uint32_t x : bad) {
+              const uint64_t r = o0 + x;
+              while (cur < hi && (lens[c.c0 + cur] == 0 ||
+                                  offsets[c.c0 + cur] + lens[c.c0 + cur] <= r))
+                ++cur;
+              if (cur >= hi) break;
+              if (offsets[c.c0 + cur] > r || cur == marked) continue;  // a gap; done already
+              stage4(cur);
+              marked = cur;
+            }
+          }
+          ++nruns;
+        } else {
+          size_t at = psz[p];
+          for (size_t i = lo; i < hi; ++i) {
+            const size_t k = c.c0 + i;
+            const uint32_t l = lens[k];
+            if (pack2fn(residues + offsets[k], l, mcodes + at, wide_ok(k, l, at, 8, psz[p + 1])) >
+                3u)
+              stage4(i);
+            so32[i] = (uint32_t)(at << 3);
+            sl32[i] = l;
+            at += (l + 3) / 4;
+          }
         }
         b->mlist[p].swap(nl);
         b->mstage[p].swap(sg);
+        b->mbad[p].swap(bad);
         r4[p + 1] = sat;
         if (mx >= alpha) wide = 1;  // a code outside the alphabet: the byte path reports it
       });
       for (unsigned p = 0; p < T; ++p) r4[p + 1] += r4[p];
-      const size_t b4 = psz[T] + 1;  // odd: 4-bit targets start on odd bytes
+      const size_t b4 = psz[T];  // the 4-bit region, right after the 2-bit one
       trace_mark("g-mixed2");
       if (r4[T] && wide.load() == 0) {
         pool.run([&](unsigned p) {
@@ -521,13 +605,14 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
           std::memcpy(mcodes + base, b->mstage[p].data(), r4[p + 1] - r4[p]);
           size_t sat = 0;
           for (const uint32_t i : b->mlist[p]) {
-            so32[i] = (uint32_t)(base + sat);
-            sat += ((lens[c.c0 + i] + 1) / 2 + 1) & ~(size_t)1;
+            so32[i] = (uint32_t)((base + sat) << 1) | 1u;
+            sat += (lens[c.c0 + i] + 1) / 2;
           }
         });
       }
       trace_mark("g-mixed4");
       if (wide.load() == 0) {
+        b->ctr.mixed_runs += nruns.load();
         const size_t end = b4 + r4[T];
         std::memset(mcodes + end, 0, 16);  // a last chunk reads up to 3 bytes past
         chunk_mode[gi] = SWK_PACK_MIXED;
@@ -650,7 +735,7 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     const SlotTail tl = slot_tail(cnt * 8, cnt);
     const bool pm = has_perm[si], ds = dev_sort[si];
     const uint32_t mode = chunk_mode[si], ustride = chunk_stride[si];
-    const int slot = (int)(si % sw_bank::NSLOT);
+    const int slot = (int)(si % b->feed_dslots);  // (the chunk's device slot)
     const size_t mp = mperm[si];
     const uint32_t ml = chunk_max[si++];
     uint32_t* scr = nullptr;

@@ -25,8 +25,9 @@
 /* 4-bit stream: 2 codes per byte, low nibble first (DNA chunks that hold an N). */
 #define SWK_PACK_NIBBLE 3u
 /* Mixed stream (the host feeder's ragged DNA chunks, tile kernel only): each target in 2-bit
- * codes from an even byte, or, when it holds an N, in 4-bit codes from an odd byte (the
- * address parity is the format); offsets are u32 bytes from the codes' start. */
+ * codes, or, when it holds an N, in 4-bit codes; u32 offset words from the codes' start:
+ * (byte << 1) | 1 for a 4-bit target, position << 1 for a 2-bit one, the position counting
+ * 2-bit codes (a target of a run packed back to back starts inside a byte). */
 #define SWK_PACK_MIXED 4u
 
 /* Wave kernel split tail (swk_launch_wave): the last `pairs` pairs run as P (2 or 4) row

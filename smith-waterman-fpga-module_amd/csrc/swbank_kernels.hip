@@ -398,10 +398,27 @@ __device__ __forceinline__ uint32_t record_len(const uint8_t* rec) {
   return min((uint32_t)load_u<uint16_t>(rec + 4), SWB_RECORD_MAX);
 }
 
-// SWK_PACK_MIXED: a target in 4-bit codes starts at an odd address, one in 2-bit codes at an
-// even one.
-__device__ __forceinline__ bool mixed_nibble(const uint8_t* p) {
-  return ((uint32_t)reinterpret_cast<uintptr_t>(p) & 1u) != 0;
+// SWK_PACK_MIXED: the target's u32 offset word o is (byte << 1) | 1 for 4-bit codes and
+// position << 1 for 2-bit codes, `position` counting 2-bit codes from res (targets packed back
+// to back as one run start inside a byte).  Lane2 keeps the format in the pointer's top bits:
+// bit 63 = 4-bit, bits 61-62 = the 2-bit start inside its byte (device addresses are < 2^57).
+constexpr uint64_t SWK_MIX_NIB = 1ull << 63;
+constexpr uint64_t SWK_MIX_ADDR = (1ull << 61) - 1;
+__device__ __forceinline__ const uint8_t* mixed_ptr(const uint8_t* res, uint32_t o) {
+  const uint64_t p = reinterpret_cast<uint64_t>(res);
+  return reinterpret_cast<const uint8_t*>(
+      (o & 1u) ? (p + (o >> 1)) | SWK_MIX_NIB : (p + (o >> 3)) | (uint64_t)((o >> 1) & 3u) << 61);
+}
+// Codes of C-column chunk cl of a mixed target (C = 8: a 32-bit load, C = 4: 16 bits), 2-bit
+// codes shifted down to the chunk's first; nib: the target is in 4-bit codes
+template <int C>
+__device__ __forceinline__ uint32_t mixed_word(const uint8_t* tp, uint32_t cl, bool& nib) {
+  const uint64_t v = reinterpret_cast<uint64_t>(tp);
+  nib = (v & SWK_MIX_NIB) != 0;
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(v & SWK_MIX_ADDR);
+  if (nib) return C == 4 ? (uint32_t)load_u<uint16_t>(p + 2 * cl) : load_u<uint32_t>(p + 4 * cl);
+  const uint32_t w = C == 4 ? (uint32_t)load_u<uint16_t>(p + cl) : load_u<uint32_t>(p + 2 * cl);
+  return w >> (2u * (uint32_t)(v >> 61 & 3u));
 }
 
 // C = 4 (the 16-wave query-set kernel's 4-column chunks): codes [4c, 4c+4) in lo.x / hi.x.
@@ -427,9 +444,9 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint3
     } else if (MIX && packed == SWK_PACK_MIXED) {  // per target: 4-bit at an odd address
       const uint32_t cl = min((uint32_t)c, max((t.llo + 3) / 4, 1u) - 1);
       const uint32_t ch = min((uint32_t)c, max((t.lhi + 3) / 4, 1u) - 1);
-      const bool nl = mixed_nibble(t.plo), nh = mixed_nibble(t.phi);
-      const uint32_t wl = load_u<uint16_t>(t.plo + (nl ? 2 * cl : cl));
-      const uint32_t wh = load_u<uint16_t>(t.phi + (nh ? 2 * ch : ch));
+      bool nl, nh;  // (2-bit: 4 codes from bit 0-6 of a 16-bit load)
+      const uint32_t wl = mixed_word<4>(t.plo, cl, nl);
+      const uint32_t wh = mixed_word<4>(t.phi, ch, nh);
       x = nl ? unpack8n(wl).x : unpack8(wl).x;
       y = nh ? unpack8n(wh).x : unpack8(wh).x;
     } else if (packed) {  // 1 byte per 4 codes (records: inside the data field)
@@ -466,13 +483,13 @@ __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint3
   }
   const uint32_t j0 = (uint32_t)c * 8;
   if (MIX && packed == SWK_PACK_MIXED) {  // per target: 4-bit at an odd address, else 2-bit
-    // (a 2-bit chunk reads 4 bytes for its 2: the rest is the next target's or the 16 zero
+    // (a 2-bit chunk reads 4 bytes for its 2-3: the rest is the next target's or the 16 zero
     // bytes the host writes after the last)
     const uint32_t cl = min((uint32_t)c, max((t.llo + 7) / 8, 1u) - 1);
     const uint32_t ch = min((uint32_t)c, max((t.lhi + 7) / 8, 1u) - 1);
-    const bool nl = mixed_nibble(t.plo), nh = mixed_nibble(t.phi);
-    const uint32_t wl = load_u<uint32_t>(t.plo + (nl ? 4 * cl : 2 * cl));
-    const uint32_t wh = load_u<uint32_t>(t.phi + (nh ? 4 * ch : 2 * ch));
+    bool nl, nh;
+    const uint32_t wl = mixed_word<8>(t.plo, cl, nl);
+    const uint32_t wh = mixed_word<8>(t.phi, ch, nh);
     lo = nl ? unpack8n(wl) : unpack8(wl);
     hi = nh ? unpack8n(wh) : unpack8(wh);
     if (!full) {
@@ -573,12 +590,18 @@ __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t
   t.llo = va ? la : 0u;
   t.lhi = vb ? lb : 0u;
   // an empty target still needs a readable address for the branch-free slow path
-  // (SWK_PACK_MIXED: u32 offsets; an empty target's even address reads as 2-bit)
-  const uint32_t* o32 = reinterpret_cast<const uint32_t*>(offs);
-  const uint64_t oa = MIX && packed == SWK_PACK_MIXED ? o32[a] : offs[a];
-  const uint64_t ob = MIX && packed == SWK_PACK_MIXED ? o32[b] : offs[b];
-  t.plo = la ? res + oa : reinterpret_cast<const uint8_t*>(lens);
-  t.phi = lb ? res + ob : reinterpret_cast<const uint8_t*>(lens);
+  // (SWK_PACK_MIXED: u32 offset words, see mixed_ptr; an empty target's untagged address
+  // reads as 2-bit)
+  if constexpr (MIX) {
+    if (packed == SWK_PACK_MIXED) {
+      const uint32_t* o32 = reinterpret_cast<const uint32_t*>(offs);
+      t.plo = la ? mixed_ptr(res, o32[a]) : reinterpret_cast<const uint8_t*>(lens);
+      t.phi = lb ? mixed_ptr(res, o32[b]) : reinterpret_cast<const uint8_t*>(lens);
+      return t;
+    }
+  }
+  t.plo = la ? res + offs[a] : reinterpret_cast<const uint8_t*>(lens);
+  t.phi = lb ? res + offs[b] : reinterpret_cast<const uint8_t*>(lens);
   return t;
 }
 

@@ -24,6 +24,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <vector>
 #if defined(__SSE2__)
 #include <emmintrin.h>
 #endif
@@ -147,6 +148,67 @@ __attribute__((target("avx2"))) inline uint32_t pack_4bit_avx2(const uint8_t* sr
   return j >= l ? mx : std::max(mx, pack_4bit(src + j, l - j, dst + j / 2));
 }
 #endif
+
+// pack_2bit_flag: a RUN of l codes (several targets back to back in the caller's residues) ->
+// ceil(l/4) bytes of 2-bit codes, as pack_2bit, and the position (+ base) of every code past 3
+// appended to `bad` in ascending order: the caller finds the targets that hold an N from them
+// and packs those again in 4-bit codes.  One call per run instead of one per target (the call
+// overhead was most of a ragged gather).  No `wide` form: only the run's last < 32 codes take
+// the short loop.
+inline void pack_2bit_flag(const uint8_t* src, size_t l, uint8_t* dst, uint32_t base,
+                           std::vector<uint32_t>& bad) {
+  for (size_t j = 0; j < l; j += 32) {
+    const uint32_t m = (uint32_t)std::min<size_t>(32, l - j);
+    if (pack_2bit(src + j, m, dst + j / 4) > 3u) {
+      // a code past 3 spills into its byte's other codes (the packers assume codes <= 3), and
+      // in a run those may belong to the neighbouring target: the step again from codes & 3
+      uint8_t tmp[32];
+      for (uint32_t t = 0; t < m; ++t) {
+        if (src[j + t] > 3u) bad.push_back(base + (uint32_t)(j + t));
+        tmp[t] = src[j + t] & 3u;
+      }
+      pack_2bit(tmp, m, dst + j / 4);
+    }
+  }
+}
+
+#if defined(__x86_64__)
+__attribute__((target("avx2"))) inline void pack_2bit_flag_avx2(const uint8_t* src, size_t l,
+                                                                uint8_t* dst, uint32_t base,
+                                                                std::vector<uint32_t>& bad) {
+  size_t j = 0;
+  const __m256i w1 = _mm256_set1_epi16(0x0401), w2 = _mm256_set1_epi32(0x00100001);
+  const __m256i sh = _mm256_setr_epi8(0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                                      0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
+  const __m256i pd = _mm256_setr_epi32(0, 4, 1, 1, 1, 1, 1, 1);
+  const __m256i three = _mm256_set1_epi8(3);
+  for (; j + 32 <= l; j += 32) {
+    const __m256i r = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + j));
+    // bit t set: code t <= 3 (unsigned: min(r, 3) == r)
+    const uint32_t ok =
+        (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(_mm256_min_epu8(r, three), r));
+    if (__builtin_expect(ok != 0xFFFFFFFFu, 0))
+      for (uint32_t m = ~ok; m; m &= m - 1) bad.push_back(base + (uint32_t)j + __builtin_ctz(m));
+    // codes & 3: a code past 3 would spill into its byte's other codes, which in a run may be
+    // the neighbouring target's
+    const __m256i v = _mm256_and_si256(r, three);
+    const __m256i u = _mm256_madd_epi16(_mm256_maddubs_epi16(v, w1), w2);
+    const __m256i x = _mm256_permutevar8x32_epi32(_mm256_shuffle_epi8(u, sh), pd);
+    _mm_storel_epi64(reinterpret_cast<__m128i*>(dst + j / 4), _mm256_castsi256_si128(x));
+  }
+  if (j < l) pack_2bit_flag(src + j, l - j, dst + j / 4, base + (uint32_t)j, bad);
+}
+#endif
+
+typedef void (*PackRunFn)(const uint8_t*, size_t, uint8_t*, uint32_t, std::vector<uint32_t>&);
+inline PackRunFn run_packer(bool avx2) {
+#if defined(__x86_64__)
+  if (avx2 && __builtin_cpu_supports("avx2")) return pack_2bit_flag_avx2;
+#else
+  (void)avx2;
+#endif
+  return pack_2bit_flag;
+}
 
 // The packers for this host: AVX2 forms when the CPU has AVX2 and `avx2` is allowed, else the
 // SSE2 ones (which ignore `wide`).

@@ -45,7 +45,7 @@ EXPORTS = (
 )
 ABI_VERSION = 3
 COUNTERS = ("stream_calls", "stream_reruns", "stream_declined", "chunked_calls", "device_sorts",
-            "gather_timeouts", "mixed_chunks")
+            "gather_timeouts", "mixed_chunks", "mixed_runs")
 MAX_DEVICES = 16
 RECORD_BYTES, RECORD_MAX_BASES = 64, 232
 

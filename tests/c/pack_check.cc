@@ -83,9 +83,39 @@ static int check(bool avx2, int bits, bool with_n, unsigned seed) {
   return 0;
 }
 
+// The run packer (one call per run of back-to-back targets): 2-bit bytes of every code (& 3)
+// and the ascending positions (+ base) of the codes past 3, including codes >= 128 (an
+// unsigned compare), runs of every length 0..700 (the short tail) with and without N.
+static int check_run(bool avx2, unsigned seed) {
+  std::mt19937 rng(seed);
+  const swpack::PackRunFn fn = swpack::run_packer(avx2);
+  for (int rep = 0; rep < 40; ++rep) {
+    const size_t l = rng() % 701;
+    std::vector<uint8_t> src(l + 32);
+    std::vector<uint32_t> want_bad, got_bad{7u};  // (appended to, not cleared)
+    const unsigned dens = 1 + rng() % 60;
+    for (size_t i = 0; i < l; ++i) {
+      src[i] = rng() & 3;
+      if (rng() % dens == 0) src[i] = (uint8_t)(rng() % 3 == 0 ? 4 + rng() % 252 : 4);
+      if (src[i] > 3) want_bad.push_back(1000u + (uint32_t)i);
+    }
+    std::vector<uint8_t> out((l + 3) / 4 + 16, 0xEE), want((l + 3) / 4, 0);
+    for (size_t i = 0; i < l; ++i) want[i / 4] |= (uint8_t)((src[i] & 3u) << (2 * (i % 4)));
+    fn(src.data(), l, out.data(), 1000u, got_bad);
+    if (memcmp(out.data(), want.data(), want.size()) != 0 || got_bad.size() != want_bad.size() + 1 ||
+        !std::equal(want_bad.begin(), want_bad.end(), got_bad.begin() + 1)) {
+      fprintf(stderr, "run packer avx2 %d seed %u len %zu: bytes or N positions differ\n",
+              (int)avx2, seed, l);
+      return 1;
+    }
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const bool avx2 = argc > 1 && strcmp(argv[1], "avx2") == 0;
   int bad = 0;
+  for (unsigned seed = 1; seed <= 20; ++seed) bad |= check_run(avx2, seed);
   for (int bits : {2, 4})
     for (int nn = 0; nn < 2; ++nn)
       for (unsigned seed = 1; seed <= 20; ++seed) bad |= check(avx2, bits, nn != 0, seed);

@@ -247,6 +247,59 @@ def test_feeder_mixed_chunks(monkeypatch, poisoned_buffers, case):
     assert np.array_equal(got[sel], want)
 
 
+@pytest.mark.parametrize("layout", ["runs", "gaps", "empties", "shuffled", "runs-off"])
+def test_feeder_mixed_runs(monkeypatch, poisoned_buffers, layout):
+    """Mixed chunks whose pool parts hold targets back to back in the residues pack each part
+    as ONE run (targets start inside a byte, offset word = 2-bit position << 1; the N targets
+    found from the run packer's positions and re-packed in 4-bit codes): "runs" back to back,
+    "gaps" small gaps between targets (packed with the run), "empties" zero-length targets at
+    offset 0 in between, "shuffled" offsets out of order (one packer call per target), and
+    "runs-off" (SWBANK_MIXED_RUNS=0).  Scores equal the whole-chunk layouts and the oracle; the
+    counter shows which form ran."""
+    monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
+    monkeypatch.setenv("SWBANK_KERNEL", "tile")
+    if layout == "runs-off":
+        monkeypatch.setenv("SWBANK_MIXED_RUNS", "0")
+    rng = np.random.default_rng(17 + len(layout))
+    n = 40_000
+    lens = rng.integers(1, 180, n).astype(np.uint32)
+    gap = rng.integers(0, 4, n) if layout == "gaps" else np.zeros(n, np.int64)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gap[:-1].astype(np.uint64))
+    total = int(offs[-1] + lens[-1])
+    res = rng.integers(0, 4, total + 8, dtype=np.uint8)
+    res[rng.random(res.size) < 0.002] = 4  # N, also in the gaps (must not mark a neighbour)
+    if layout == "empties":
+        e = rng.random(n) < 0.05
+        lens[e] = 0
+        offs[e] = 0
+    if layout == "shuffled":
+        p = rng.permutation(n)
+        offs, lens = offs[p].copy(), lens[p].copy()
+    q = rng.integers(0, 4, 120, dtype=np.uint8)
+    for k in range(0, n, 89):  # homologs: high scores that a wrong code would change
+        m = min(int(lens[k]), 120)
+        res[int(offs[k]):int(offs[k]) + m] = q[:m]
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        got = bank.score_batch(res, offs, lens)
+        c = bank.counters()
+        monkeypatch.setenv("SWBANK_MIXED", "0")
+        ref = bank.score_batch(res, offs, lens)
+    assert c["mixed_chunks"] >= 1
+    if layout in ("runs", "gaps", "empties"):
+        assert c["mixed_runs"] >= c["mixed_chunks"], c
+    else:
+        assert c["mixed_runs"] == 0, c
+    assert np.array_equal(got, ref), np.nonzero(got != ref)[0][:8]
+    sel = np.unique(np.concatenate([rng.choice(n, 800, replace=False), np.arange(0, n, 89),
+                                    np.arange(n - 130, n)]))
+    sub = [res[int(offs[k]):int(offs[k]) + int(lens[k])] for k in sel]
+    want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(*REF[:2]), *REF[2:])
+    assert np.array_equal(got[sel], want)
+
+
 def test_feeder_mixed_bad_code(monkeypatch):
     """A code outside the alphabet in a mixed chunk: the byte path reports the target."""
     monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
