@@ -587,6 +587,23 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
 // ---- swbank_feeder.hip
 bool chunk_perm(HostPool& pool, const uint32_t* len, size_t n, uint32_t* perm);
 bool scratch_free(const sw_bank* b, uint32_t max_len);
+// A ragged DNA chunk [c0, c0 + cnt) in the mixed layout (SWK_PACK_MIXED), the pool's parts of
+// `step` targets each, planned by the caller's lengths pass: part p packs as one run from
+// residue rbase[p] (rspan[p] codes, gaps included) or, rbase[p] == UINT64_MAX, per target; its
+// 2-bit bytes start at psz[p] of mcodes, psz[T] and part4[T] bound the 2-bit and 4-bit regions.
+// Writes the offset words so32[], lengths sl32[] and the codes; `end` = the codes' end (16 zero
+// bytes follow).  order != nullptr: the chunk's longest-first visiting order (a stable counting
+// sort) is written to order[] in the same pass, part p's next position in bin (hi - len) >> shift
+// at order_pos[p * nbin + bin].  False when a code is outside the alphabet (nothing usable).
+struct MixedOrder {
+  std::vector<uint32_t> pos;
+  uint32_t hi = 0, shift = 0, nbin = 0;
+};
+bool mixed_pack(sw_bank* b, const uint8_t* residues, size_t nres, const uint64_t* offsets,
+                const uint32_t* lens, size_t c0, size_t cnt, size_t step,
+                const std::vector<uint64_t>& rbase, const std::vector<uint64_t>& rspan,
+                const std::vector<size_t>& psz, const std::vector<size_t>& part4, uint32_t* so32,
+                uint32_t* sl32, uint8_t* mcodes, uint32_t* order, MixedOrder* mo, size_t& end);
 sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres, const uint64_t* offsets,
                      const uint32_t* lens, size_t n, int32_t* out);
 sw_status records_feed(sw_bank* b, const uint8_t* recs, size_t n, int32_t* out);

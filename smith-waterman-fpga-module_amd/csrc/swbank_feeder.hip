@@ -296,6 +296,131 @@ bool scratch_free(const sw_bank* b, uint32_t max_len) {
   return b->segs.size() == 1 && b->wsegs == 1 && !need32 && !opt16;
 }
 
+// Pass 1: every target in 2-bit codes (offset word: its 2-bit position << 1, see
+// SWK_PACK_MIXED) -- a part whose targets lie back to back in the residues as ONE run (one
+// packer call per 16 Ki codes, the positions of codes past 3 reported), else one call per
+// target.  A target with a code past 3 is packed again at once in 4-bit codes into the part's
+// staging buffer (its residues still in cache: scattered re-reads later were latency bound).
+// Pass 2: each part's staged 4-bit targets land as one block after the 2-bit region (their
+// 2-bit bytes stay unused), offset words (byte << 1) | 1.  (Declared in swbank_bank.h.)
+bool mixed_pack(sw_bank* b, const uint8_t* residues, size_t nres, const uint64_t* offsets,
+                const uint32_t* lens, size_t c0, size_t cnt, size_t step,
+                const std::vector<uint64_t>& rbase, const std::vector<uint64_t>& rspan,
+                const std::vector<size_t>& psz, const std::vector<size_t>& part4, uint32_t* so32,
+                uint32_t* sl32, uint8_t* mcodes, uint32_t* order, MixedOrder* mo, size_t& end) {
+  HostPool& pool = *b->pool;
+  const unsigned T = pool.size();
+  const bool avx2 = env_int("SWBANK_AVX2", 1) != 0;
+  const swpack::PackFn pack2fn = swpack::packer(2, avx2), pack4fn = swpack::packer(4, avx2);
+  const swpack::PackRunFn runfn = swpack::run_packer(avx2);
+  const uint32_t alpha = (uint32_t)b->alpha;
+  // a target's last 32-code step may store past its end while it stays inside the part's output
+  // (later targets of the part rewrite those bytes) and reads inside the residues
+  const auto wide_ok = [&](size_t k, uint32_t l, size_t at, size_t step_bytes, size_t part_end) {
+    const size_t steps = (l + 31u) / 32u;
+    return offsets[k] + steps * 32 <= nres && at + steps * step_bytes <= part_end;
+  };
+  if (b->mlist.size() < T) b->mlist.resize(T);
+  if (b->mstage.size() < T) b->mstage.resize(T);
+  if (b->mbad.size() < T) b->mbad.resize(T);
+  std::vector<size_t> r4(T + 1, 0);  // staged 4-bit bytes per part
+  std::atomic<uint32_t> nruns{0}, wide{0};
+  pool.run([&](unsigned p) {
+    const size_t lo = std::min(cnt, p * step), hi = std::min(cnt, (p + 1) * step);
+    // (list and stage live in this thread while they grow: the parts' vector headers share
+    // cache lines)
+    std::vector<uint32_t> nl, bad;
+    std::vector<uint8_t> sg;
+    nl.swap(b->mlist[p]);
+    sg.swap(b->mstage[p]);
+    bad.swap(b->mbad[p]);
+    nl.clear();
+    const size_t scap = part4[p + 1] - part4[p] + 64;
+    if (sg.size() < scap) sg.resize(scap);
+    size_t sat = 0;
+    uint32_t mx = 0;
+    uint32_t* opos = mo ? mo->pos.data() + (size_t)p * mo->nbin : nullptr;
+    const auto place = [&](size_t i, uint32_t l) {  // (the fused counting sort's scatter)
+      if (opos) order[opos[(mo->hi - std::min(l, mo->hi)) >> mo->shift]++] = (uint32_t)i;
+    };
+    const auto stage4 = [&](size_t i) {
+      const size_t k = c0 + i;
+      const uint32_t l = lens[k];
+      mx = std::max(mx, pack4fn(residues + offsets[k], l, sg.data() + sat,
+                                wide_ok(k, l, sat, 16, scap)));
+      nl.push_back((uint32_t)i);
+      sat += (l + 1) / 2;
+    };
+    if (rbase[p] != UINT64_MAX) {
+      const uint64_t o0 = rbase[p], span = rspan[p];
+      const uint64_t pos0 = 4 * (uint64_t)psz[p];  // the run's first 2-bit position
+      for (size_t i = lo; i < hi; ++i) {
+        const size_t k = c0 + i;
+        const uint32_t l = lens[k];
+        so32[i] = l ? (uint32_t)((pos0 + offsets[k] - o0) << 1) : 0u;
+        sl32[i] = l;
+        place(i, l);
+      }
+      // 16 Ki codes per packer call: the N targets of a block are re-packed while its
+      // residues are in cache; `cur` walks the targets (ascending, non-overlapping)
+      size_t cur = lo, marked = SIZE_MAX;
+      for (uint64_t x0 = 0; x0 < span; x0 += 16384) {
+        const uint64_t x1 = std::min<uint64_t>(span, x0 + 16384);
+        bad.clear();
+        runfn(residues + o0 + x0, (size_t)(x1 - x0), mcodes + psz[p] + x0 / 4, (uint32_t)x0, bad);
+        for (const uint32_t x : bad) {
+          const uint64_t r = o0 + x;
+          while (cur < hi &&
+                 (lens[c0 + cur] == 0 || offsets[c0 + cur] + lens[c0 + cur] <= r))
+            ++cur;
+          if (cur >= hi) break;
+          if (offsets[c0 + cur] > r || cur == marked) continue;  // a gap; done already
+          stage4(cur);
+          marked = cur;
+        }
+      }
+      ++nruns;
+    } else {
+      size_t at = psz[p];
+      for (size_t i = lo; i < hi; ++i) {
+        const size_t k = c0 + i;
+        const uint32_t l = lens[k];
+        if (pack2fn(residues + offsets[k], l, mcodes + at, wide_ok(k, l, at, 8, psz[p + 1])) > 3u)
+          stage4(i);
+        so32[i] = (uint32_t)(at << 3);
+        sl32[i] = l;
+        place(i, l);
+        at += (l + 3) / 4;
+      }
+    }
+    b->mlist[p].swap(nl);
+    b->mstage[p].swap(sg);
+    b->mbad[p].swap(bad);
+    r4[p + 1] = sat;
+    if (mx >= alpha) wide = 1;  // a code outside the alphabet
+  });
+  if (wide.load() != 0) return false;
+  for (unsigned p = 0; p < T; ++p) r4[p + 1] += r4[p];
+  const size_t b4 = psz[T];  // the 4-bit region, right after the 2-bit one
+  trace_mark("g-mixed2");
+  if (r4[T]) {
+    pool.run([&](unsigned p) {
+      const size_t base = b4 + r4[p];
+      std::memcpy(mcodes + base, b->mstage[p].data(), r4[p + 1] - r4[p]);
+      size_t sat = 0;
+      for (const uint32_t i : b->mlist[p]) {
+        so32[i] = (uint32_t)((base + sat) << 1) | 1u;
+        sat += (lens[c0 + i] + 1) / 2;
+      }
+    });
+  }
+  trace_mark("g-mixed4");
+  b->ctr.mixed_runs += nruns.load();
+  end = b4 + r4[T];
+  std::memset(mcodes + end, 0, 16);  // a last target's chunk reads up to 3 bytes past
+  return true;
+}
+
 // The host-buffer batch through the feeder (n >= 1, buffers checked by the caller).
 sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
                             const uint64_t* offsets, const uint32_t* lens, size_t n,
@@ -426,7 +551,6 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   // gaps included); UINT64_MAX: one packer call per target.  SWBANK_MIXED_RUNS=0 disables.
   std::vector<uint64_t> rbase(T), rspan(T);
   const bool runs_ok = env_int("SWBANK_MIXED_RUNS", 1) != 0;
-  const swpack::PackRunFn runfn = swpack::run_packer(avx2);
   std::atomic<size_t> bad{SIZE_MAX}, oob{SIZE_MAX};
   std::atomic<uint32_t> wide{0};
   size_t gi = 0, si = 0;
@@ -511,110 +635,12 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     if (mixed_ok && !uni && (host_dsort || cnt <= SWB_TILE) &&
         ca32 + align16(psz[T] + part4[T] + 3 * cnt + 32) + align16(cnt * 4 + 8) <= c.bytes &&
         psz[T] + part4[T] + 16 < (1ull << 29) && !wave_preferred(b, cnt, chunk_max[gi], cf16)) {
-      // pass 1: every target in 2-bit codes (offset word: its 2-bit position << 1, see
-      // SWK_PACK_MIXED) -- a part whose targets lie back to back in the residues as ONE run (one
-      // packer call per 16 Ki codes, the positions of codes past 3 reported), else one call per
-      // target.  A target with a code past 3 is packed again at once in 4-bit codes into the
-      // part's staging buffer (its residues still in cache: scattered re-reads later were
-      // latency bound).  Pass 2: each part's staged 4-bit targets land as one block after the
-      // 2-bit region (their 2-bit bytes stay unused), offset words (byte << 1) | 1
+      // the mixed layout (mixed_pack): u32 offset words | lengths | codes; a code outside the
+      // alphabet sends the chunk on to the whole-chunk layouts, where the byte path reports it
       uint32_t* so32 = reinterpret_cast<uint32_t*>(slot);
-      uint32_t* sl32 = so32 + cnt;
-      uint8_t* mcodes = slot + ca32;
-      if (b->mlist.size() < T) b->mlist.resize(T);
-      if (b->mstage.size() < T) b->mstage.resize(T);
-      if (b->mbad.size() < T) b->mbad.resize(T);
-      std::vector<size_t> r4(T + 1, 0);  // staged 4-bit bytes per part
-      std::atomic<uint32_t> nruns{0};
-      wide = 0;
-      pool.run([&](unsigned p) {
-        const size_t lo = std::min(cnt, p * step), hi = std::min(cnt, (p + 1) * step);
-        // (list and stage live in this thread while they grow: the parts' vector headers
-        // share cache lines)
-        std::vector<uint32_t> nl, bad;
-        std::vector<uint8_t> sg;
-        nl.swap(b->mlist[p]);
-        sg.swap(b->mstage[p]);
-        bad.swap(b->mbad[p]);
-        nl.clear();
-        const size_t scap = part4[p + 1] - part4[p] + 64;
-        if (sg.size() < scap) sg.resize(scap);
-        size_t sat = 0;
-        uint32_t mx = 0;
-        const auto stage4 = [&](size_t i) {
-          const size_t k = c.c0 + i;
-          const uint32_t l = lens[k];
-          mx = std::max(mx, pack4fn(residues + offsets[k], l, sg.data() + sat,
-                                    wide_ok(k, l, sat, 16, scap)));
-          nl.push_back((uint32_t)i);
-          sat += (l + 1) / 2;
-        };
-        if (rbase[p] != UINT64_MAX) {
-          const uint64_t o0 = rbase[p], span = rspan[p];
-          const uint64_t pos0 = 4 * (uint64_t)psz[p];  // the run's first 2-bit position
-          for (size_t i = lo; i < hi; ++i) {
-            const size_t k = c.c0 + i;
-            so32[i] = lens[k] ? (uint32_t)((pos0 + offsets[k] - o0) << 1) : 0u;
-            sl32[i] = lens[k];
-          }
-          // 16 Ki codes per packer call: the N targets of a block are re-packed while its
-          // residues are in cache; `cur` walks the targets (ascending, non-overlapping)
-          size_t cur = lo, marked = SIZE_MAX;
-          for (uint64_t x0 = 0; x0 < span; x0 += 16384) {
-            const uint64_t x1 = std::min<uint64_t>(span, x0 + 16384);
-            bad.clear();
-            runfn(residues + o0 + x0, (size_t)(x1 - x0), mcodes + psz[p] + x0 / 4, (uint32_t)x0,
-                  bad);
-            for (const uint32_t x : bad) {
-              const uint64_t r = o0 + x;
-              while (cur < hi && (lens[c.c0 + cur] == 0 ||
-                                  offsets[c.c0 + cur] + lens[c.c0 + cur] <= r))
-                ++cur;
-              if (cur >= hi) break;
-              if (offsets[c.c0 + cur] > r || cur == marked) continue;  // a gap; done already
-              stage4(cur);
-              marked = cur;
-            }
-          }
-          ++nruns;
-        } else {
-          size_t at = psz[p];
-          for (size_t i = lo; i < hi; ++i) {
-            const size_t k = c.c0 + i;
-            const uint32_t l = lens[k];
-            if (pack2fn(residues + offsets[k], l, mcodes + at, wide_ok(k, l, at, 8, psz[p + 1])) >
-                3u)
-              stage4(i);
-            so32[i] = (uint32_t)(at << 3);
-            sl32[i] = l;
-            at += (l + 3) / 4;
-          }
-        }
-        b->mlist[p].swap(nl);
-        b->mstage[p].swap(sg);
-        b->mbad[p].swap(bad);
-        r4[p + 1] = sat;
-        if (mx >= alpha) wide = 1;  // a code outside the alphabet: the byte path reports it
-      });
-      for (unsigned p = 0; p < T; ++p) r4[p + 1] += r4[p];
-      const size_t b4 = psz[T];  // the 4-bit region, right after the 2-bit one
-      trace_mark("g-mixed2");
-      if (r4[T] && wide.load() == 0) {
-        pool.run([&](unsigned p) {
-          const size_t base = b4 + r4[p];
-          std::memcpy(mcodes + base, b->mstage[p].data(), r4[p + 1] - r4[p]);
-          size_t sat = 0;
-          for (const uint32_t i : b->mlist[p]) {
-            so32[i] = (uint32_t)((base + sat) << 1) | 1u;
-            sat += (lens[c.c0 + i] + 1) / 2;
-          }
-        });
-      }
-      trace_mark("g-mixed4");
-      if (wide.load() == 0) {
-        b->ctr.mixed_runs += nruns.load();
-        const size_t end = b4 + r4[T];
-        std::memset(mcodes + end, 0, 16);  // a last chunk reads up to 3 bytes past
+      size_t end = 0;
+      if (mixed_pack(b, residues, nres, offsets, lens, c.c0, cnt, step, rbase, rspan, psz, part4,
+                     so32, so32 + cnt, slot + ca32, nullptr, nullptr, end)) {
         chunk_mode[gi] = SWK_PACK_MIXED;
         ++b->ctr.mixed_chunks;
         const bool uniform = chunk_min == chunk_max[gi];

@@ -428,7 +428,7 @@ __device__ __forceinline__ uint32_t pad_tail4(uint32_t w, uint32_t j0, uint32_t 
   return (w & keep) | ((pad * 0x01010101u) & ~keep);
 }
 
-// MIX = false: the caller never passes SWK_PACK_MIXED (streamed and query-set variants)
+// MIX = false: the caller never passes SWK_PACK_MIXED (the query-set variants)
 template <int C = 8, bool MIX = true>
 __device__ __forceinline__ void load_raw(const Lane2& t, int c, bool full, uint32_t pad,
                                          uint32_t packed, uint2& lo, uint2& hi) {
@@ -839,8 +839,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int snc = (int)a.nsc;
   int scur = -1, st0 = 0;
   uint32_t scn = 0, sro_lo = 0, sro_hi = 0, smode = SWK_PACK_STREAM;
-  // ragged streamed batches (ulen == 0): a chunk's region is offsets u64 | lengths u32 | visiting
-  // order u32 (scn each) | codes at the next 16-byte boundary; the order of the chunk of the tile
+  // ragged streamed batches (ulen == 0): a chunk's region is mixed offset words u32 (see
+  // mixed_ptr) | lengths u32 | visiting order u32 (scn each) | codes (SWK_PACK_MIXED: the 2-bit
+  // region, then the 4-bit one) at the next 16-byte boundary; the order of the chunk of the tile
   // this wave is scoring (wperm, its first tile wst0) maps score positions to targets
   const uint32_t* cperm = nullptr;
   const uint32_t* wperm = nullptr;
@@ -864,7 +865,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       sro_lo = __builtin_amdgcn_readfirstlane(ssc[c].res_off_lo);
       sro_hi = __builtin_amdgcn_readfirstlane(ssc[c].res_off_hi);
       const uint32_t md = stream_mode(a.hflag, a.dflag, c, snc, lane);
-      smode = md == SWK_PACK_NIBBLE ? SWK_PACK_NIBBLE : SWK_PACK_STREAM;
+      // (ragged chunks cross in the mixed layout; an aborted one reads as empty mixed targets)
+      smode = a.ulen == 0 ? SWK_PACK_MIXED
+                          : md == SWK_PACK_NIBBLE ? SWK_PACK_NIBBLE : SWK_PACK_STREAM;
       if (md == SWK_STREAM_ABORT && a.ulen == 0) {
         // a ragged chunk that never landed (the host re-runs the call): its region may hold
         // anything, so it is read from the zeroed region instead (empty targets, scores in
@@ -876,14 +879,15 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     }
     pk = smode;
     const uint8_t* base = a.res + ((size_t)sro_hi << 32 | sro_lo);
-    if (a.ulen == 0) {  // ragged: the chunk's own offsets, lengths and order
-      const uint64_t* co = reinterpret_cast<const uint64_t*>(base);
-      const uint32_t* cl = reinterpret_cast<const uint32_t*>(base + 8 * (size_t)scn);
+    if (a.ulen == 0) {  // ragged: the chunk's own mixed offset words, lengths and order
+      const uint32_t* co = reinterpret_cast<const uint32_t*>(base);
+      const uint32_t* cl = co + scn;
       cperm = cl + scn;
-      return lane_targets<false>(base + (((size_t)scn * 16 + 15) & ~(size_t)15), co, cl, scn,
-                                 t - st0, lane, pk, cperm, 0u, 0u);
+      return lane_targets<true>(base + (((size_t)scn * 12 + 15) & ~(size_t)15),
+                                reinterpret_cast<const uint64_t*>(co), cl, scn, t - st0, lane, pk,
+                                cperm, 0u, 0u);
     }
-    return lane_targets<false>(base, nullptr, nullptr, scn, t - st0, lane, pk, nullptr, a.ulen,
+    return lane_targets<true>(base, nullptr, nullptr, scn, t - st0, lane, pk, nullptr, a.ulen,
                                pk == SWK_PACK_NIBBLE ? (a.ulen + 1) / 2 : (a.ulen + 3) / 4);
   };
 
@@ -961,7 +965,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   u16x2 best = {0, 0};
   u16x2 prevUpH = H0;  // H(row above, column -1)
   uint2 rlo, rhi;      // raw codes of the next chunk (prefetched one phase ahead)
-  load_raw<C, !STREAM && !MQ>(cur, 0, nfull > 0, a.pad, packed, rlo, rhi);
+  load_raw<C, !MQ>(cur, 0, nfull > 0, a.pad, packed, rlo, rhi);
   if (STREAM && threadIdx.x == 0) sq[W] = total;
   __syncthreads();
 
@@ -1051,7 +1055,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         }
       }
       if (!last) {
-        load_raw<C, !STREAM && !MQ>(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
+        load_raw<C, !MQ>(cur, c + 1, c + 1 < nfull, a.pad, packed, rlo, rhi);
       } else if (nunit < nunits) {  // first chunk of the next tile
         if constexpr (STREAM) cur = stream_tile(ntile, packed_n);
         else
@@ -1059,7 +1063,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
                                   a.ustride);
         tile_chunks<C>(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
                     n, nch_n, nfull_n);
-        load_raw<C, !STREAM && !MQ>(cur, 0, nfull_n > 0, a.pad, STREAM ? packed_n : packed, rlo, rhi);
+        load_raw<C, !MQ>(cur, 0, nfull_n > 0, a.pad, STREAM ? packed_n : packed, rlo, rhi);
       }
       const int slot = g & 1;
       // next chunk's boundary row (never past the last unit's edge rows)

@@ -28,6 +28,7 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
       env_int("SWBANK_PACK2", 1) == 0 || env_int("SWBANK_UNIFORM", 1) == 0 ||
       !scratch_free(b, L) || n > 0x7FFFFFFFull)
     return SW_OK;
+  if (rlens && env_int("SWBANK_MIXED", 1) == 0) return SW_OK;  // (ragged: the mixed layout)
   const char* kforce = std::getenv("SWBANK_KERNEL");
   if (kforce && std::strcmp(kforce, "wave") == 0) return SW_OK;
   const size_t T = (n + SWB_TILE - 1) / SWB_TILE;
@@ -46,15 +47,36 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   const size_t cap = std::max<size_t>(1, T / 8);
   for (size_t t = 0, sz = std::max<size_t>(1, T / 64); t < T; t += sz, sz = std::min(cap, 2 * sz))
     tile0.push_back(t);
+  // SWBANK_STREAM_TAPER=k: the last chunk cut into halves k times (1/2, 1/4, .., the rest), so
+  // the kernel's work after the last copy landed is a small chunk
+  const int taper = env_int("SWBANK_STREAM_TAPER", 0);
+  if (taper > 0 && tile0.size() > 1) {
+    const size_t last = tile0.back();
+    size_t rem = T - last, at = last;
+    tile0.pop_back();
+    tile0.push_back(at);
+    for (int k = 0; k < taper && rem / 2 >= 8; ++k) {
+      at += rem / 2;
+      rem -= rem / 2;
+      tile0.push_back(at);
+    }
+  }
   const size_t nsc = tile0.size();
   tile0.push_back(T);
   const size_t nib = (L + 1) / 2;  // 4-bit bytes per target (the 2-bit stream needs fewer)
+  const size_t PT0 = b->pool ? b->pool->size() : 1;
   std::vector<size_t> roff(nsc + 1, 0);
   size_t slot_bytes = 0, zbytes = 0;
   for (size_t i = 0; i < nsc; ++i) {
     const size_t cnt = std::min(n, tile0[i + 1] * SWB_TILE) - tile0[i] * SWB_TILE;
-    const size_t head = rlens ? align16(cnt * 16) : 0;  // ragged: offsets | lengths | order
-    roff[i + 1] = roff[i] + (head + cnt * nib + 64 + 255) / 256 * 256;
+    // ragged: offset words | lengths | order, then the mixed codes: the 2-bit region (a run's
+    // gaps included: at most 1/8 more codes, + a byte per part) and the 4-bit one (bounded by
+    // every target in 4-bit codes)
+    const size_t head = rlens ? align16(cnt * 12) : 0;
+    const size_t body = rlens ? cnt * ((L + 3) / 4) + cnt * (size_t)L / 32 + cnt * nib + 32 * PT0
+                              : cnt * nib;
+    if (rlens && head + body + 64 >= ((size_t)1 << 29)) return SW_OK;  // (u32 offset words)
+    roff[i + 1] = roff[i] + (head + body + 64 + 255) / 256 * 256;
     slot_bytes = std::max(slot_bytes, roff[i + 1] - roff[i]);
     zbytes = std::max(zbytes, head + 64);
   }
@@ -198,6 +220,18 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   const size_t steps32 = (L + 31u) / 32u;
   bool nib_mode = false;  // from the first chunk holding an N on: 4-bit chunks
   std::atomic<size_t> oob{SIZE_MAX};
+  // ragged: per part its run, 2-bit and 4-bit byte prefixes; the order's length bins (batch
+  // longest first, at most 1024 bins of 2^shift lengths) and each part's next slot per bin
+  std::vector<uint64_t> rbase(PT), rspan(PT);
+  std::vector<size_t> psz(PT + 1, 0), p4(PT + 1, 0);
+  const bool runs_ok = env_int("SWBANK_MIXED_RUNS", 1) != 0;
+  MixedOrder mo;
+  if (rlens) {
+    mo.hi = L;
+    while ((L >> mo.shift) >= 1024u) ++mo.shift;
+    mo.nbin = (L >> mo.shift) + 1;
+    mo.pos.assign((size_t)PT * mo.nbin, 0u);
+  }
   std::atomic<uint32_t> wide{0};
   sw_status err = SW_OK;
   bool started = false;     // the kernel is enqueued
@@ -219,16 +253,21 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t md = 0;
     size_t sb = 0, bytes = 0;
-    if (rlens) {  // ragged: offsets | lengths | order, then the codes at the next 16 bytes
-      const size_t ca = align16(cnt * 16), step = (cnt + PT - 1) / PT;
-      uint64_t* so = reinterpret_cast<uint64_t*>(codes);
-      uint32_t* sl = reinterpret_cast<uint32_t*>(codes + cnt * 8);
-      uint32_t* sp = sl + cnt;
-      uint8_t* cb = codes + ca;
-      std::vector<size_t> p2(PT + 1, 0), p4(PT + 1, 0);
-      pool.run([&](unsigned p) {  // lengths, bounds, packed bytes per part
+    if (rlens) {  // ragged: mixed offset words | lengths | order, then the codes (mixed layout)
+      const size_t ca = align16(cnt * 12);
+      uint32_t* so32 = reinterpret_cast<uint32_t*>(codes);
+      uint32_t* sl32 = so32 + cnt;
+      uint32_t* sp = sl32 + cnt;
+      // lengths pass: bounds, each part's run (targets back to back in the residues, as the
+      // chunked feeder's mixed chunks), its 2-bit and 4-bit bytes, and its histogram over the
+      // order's length bins (the longest-first order is then placed while packing: no sort pass)
+      std::fill(mo.pos.begin(), mo.pos.end(), 0u);
+      pool.run([&](unsigned p) {
         const size_t lo = std::min(cnt, p * step), hi = std::min(cnt, (p + 1) * step);
-        size_t a2 = 0, a4 = 0;
+        size_t a1 = 0, a2 = 0, a4 = 0;
+        bool mono = runs_ok;
+        uint64_t first = UINT64_MAX, last = 0;
+        uint32_t* h = mo.pos.data() + (size_t)p * mo.nbin;
         for (size_t j = lo; j < hi; ++j) {
           const size_t k = c0 + j;
           const uint32_t l = rlens[k];
@@ -238,43 +277,44 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
             }
             return;
           }
-          sl[j] = l;
+          a1 += l;
           a2 += (l + 3) / 4;
           a4 += (l + 1) / 2;
+          ++h[(mo.hi - std::min(l, mo.hi)) >> mo.shift];
+          if (l) {
+            mono &= first == UINT64_MAX || offsets[k] >= last;
+            if (first == UINT64_MAX) first = offsets[k];
+            last = offsets[k] + l;
+          }
         }
-        p2[p + 1] = a2;
+        const uint64_t span = first == UINT64_MAX ? 0 : last - first;
+        const bool run = mono && first != UINT64_MAX && span <= a1 + a1 / 8 + 64 &&
+                         span < (1ull << 30);
+        rbase[p] = run ? first : UINT64_MAX;
+        rspan[p] = run ? span : 0;
+        psz[p + 1] = run ? (span + 3) / 4 : a2;
         p4[p + 1] = a4;
       });
-      for (unsigned p = 0; p < PT; ++p) {
-        p2[p + 1] += p2[p];
-        p4[p + 1] += p4[p];
-      }
-      for (int pass = nib_mode ? 1 : 0; oob.load() == SIZE_MAX && pass < 2 && md == 0; ++pass) {
-        const bool two = pass == 0;
-        const std::vector<size_t>& pre = two ? p2 : p4;
-        const size_t stepb = two ? 8 : 16;
-        const swpack::PackFn fn = two ? pack2fn : pack4fn;
-        wide = 0;
-        pool.run([&](unsigned p) {
-          const size_t lo = std::min(cnt, p * step), hi = std::min(cnt, (p + 1) * step);
-          size_t at = pre[p];
-          uint32_t acc = 0;
-          for (size_t j = lo; j < hi; ++j) {
-            const size_t k = c0 + j;
-            const uint32_t l = sl[j];
-            const size_t st = (l + 31u) / 32u;
-            // full vector steps past the target's end stay inside this part's output and read
-            // inside the residues (later targets of the part rewrite those bytes)
-            const bool w = offsets[k] + st * 32 <= nres && at + st * stepb <= pre[p + 1];
-            const uint32_t v = fn(residues + offsets[k], l, cb + at, w);
-            acc = two ? (acc | v) : std::max(acc, v);
-            so[j] = at;
-            at += two ? (l + 3) / 4 : (l + 1) / 2;
+      if (oob.load() == SIZE_MAX) {
+        for (unsigned p = 0; p < PT; ++p) {
+          psz[p + 1] += psz[p];
+          p4[p + 1] += p4[p];
+        }
+        uint32_t at = 0;  // bins longest first, parts in input order: a stable order
+        for (uint32_t bin = 0; bin < mo.nbin; ++bin)
+          for (unsigned p = 0; p < PT; ++p) {
+            uint32_t& x = mo.pos[(size_t)p * mo.nbin + bin];
+            const uint32_t c = x;
+            x = at;
+            at += c;
           }
-          if (two ? acc > 3u : acc >= (uint32_t)SW_DNA_ALPHA) wide = 1;
-        });
-        if (wide.load() == 0) md = two ? SWK_PACK_STREAM : SWK_PACK_NIBBLE;
-        else if (two) nib_mode = true;
+        size_t end = 0;
+        if (mixed_pack(b, residues, nres, offsets, rlens, c0, cnt, step, rbase, rspan, psz, p4,
+                       so32, sl32, codes + ca, sp, &mo, end)) {
+          md = SWK_PACK_MIXED;
+          bytes = ca + end;
+          ++b->ctr.mixed_chunks;
+        }
       }
       if (oob.load() == SIZE_MAX && md == 0) {  // a code outside the alphabet
         for (size_t j = 0; j < cnt && err == SW_OK; ++j)
@@ -287,11 +327,6 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
             }
         if (err == SW_OK) err = fail(b, SW_ERR_ARG, "code outside alphabet");
         break;
-      }
-      if (md != 0) {
-        if (!chunk_perm(pool, sl, cnt, sp))  // already longest first: the identity
-          for (size_t j = 0; j < cnt; ++j) sp[j] = (uint32_t)j;
-        bytes = ca + (md == SWK_PACK_STREAM ? p2[PT] : p4[PT]);
       }
     } else if (recs) {  // 2-bit data bytes of every record; lengths must all be L
       sb = (L + 3) / 4;

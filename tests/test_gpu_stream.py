@@ -413,19 +413,27 @@ def _ragged(rng, n, lo, hi, p_n=0.0, gap=0):
     return res, offs, lens
 
 
-@pytest.mark.parametrize("case", ["2bit", "nibble", "empty", "gaps", "big", "u16", "gotoh"])
-def test_stream_ragged(monkeypatch, case):
-    """Ragged batches stream too when asked (SWBANK_STREAM_RAGGED=1): each chunk carries its
-    offsets, lengths and longest-first order ahead of its codes; scores equal the chunked
-    feeder's (SWBANK_STREAM_RAGGED=0) and the oracle's on a sample."""
+@pytest.mark.parametrize("case", ["2bit", "nibble", "empty", "gaps", "big", "u16", "gotoh",
+                                  "shuffled", "noruns", "long"])
+def test_stream_ragged(monkeypatch, poisoned_buffers, case):
+    """Ragged batches stream (SWBANK_STREAM_RAGGED): each chunk carries its mixed offset words,
+    lengths and longest-first order (placed while packing) ahead of its codes, the targets in
+    2-bit codes or, when they hold an N, 4-bit codes; parts whose targets lie back to back pack
+    as runs.  Scores equal the chunked feeder's (SWBANK_STREAM_RAGGED=0) and the oracle's on a
+    sample."""
     if case != "big":
         monkeypatch.setenv("SWBANK_STREAM", "2")
-    monkeypatch.setenv("SWBANK_STREAM_RAGGED", "1")  # opt-in
+    monkeypatch.setenv("SWBANK_STREAM_RAGGED", "1")
+    if case == "noruns":
+        monkeypatch.setenv("SWBANK_MIXED_RUNS", "0")
     rng = np.random.default_rng(len(case) * 13)
-    n = 300_000 if case == "big" else 30_000
-    lo, hi = {"empty": (0, 40), "big": (64, 150)}.get(case, (20, 200))
-    res, offs, lens = _ragged(rng, n, lo, hi, p_n=0.002 if case in ("nibble", "big") else 0.0,
-                              gap=3 if case == "gaps" else 0)
+    n = 300_000 if case == "big" else 6_000 if case == "long" else 30_000
+    lo, hi = {"empty": (0, 40), "big": (64, 150), "long": (300, 1500)}.get(case, (20, 200))
+    p_n = 0.002 if case in ("nibble", "big", "shuffled", "noruns", "long") else 0.0
+    res, offs, lens = _ragged(rng, n, lo, hi, p_n=p_n, gap=3 if case == "gaps" else 0)
+    if case == "shuffled":  # offsets out of order: no part is a run
+        perm = rng.permutation(n)
+        offs, lens = offs[perm].copy(), lens[perm].copy()
     gotoh = case == "gotoh"
     params = (5, -4, -10, -1) if gotoh else REF
     if case == "u16":
@@ -437,9 +445,15 @@ def test_stream_ragged(monkeypatch, case):
         got = bank.score_batch(res, offs, lens)
         kern = bank.last_kernel()
         best = bank.best()
+        c = bank.counters()
         monkeypatch.setenv("SWBANK_STREAM_RAGGED", "0")
         ref = bank.score_batch(res, offs, lens)
     assert "streamed=" in kern, kern
+    assert c["stream_calls"] == 1 and c["mixed_chunks"] >= 1, c
+    if case in ("shuffled", "noruns"):
+        assert c["mixed_runs"] == 0, c
+    elif case != "empty":
+        assert c["mixed_runs"] >= 1, c
     assert np.array_equal(got, ref), kern
     top = int(np.argmax(got))
     assert best[1:] == (int(got[top]), top)
@@ -448,6 +462,27 @@ def test_stream_ragged(monkeypatch, case):
     want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(*params[:2]), *params[2:],
                          O.GAP_GOTOH if gotoh else O.GAP_MERGED)
     assert np.array_equal(got[sel], want), kern
+
+
+def test_stream_ragged_back_to_back(monkeypatch, poisoned_buffers):
+    """Three ragged streamed calls on one bank with other data and lengths each time: every
+    call's scores are exact (no stale chunk codes, orders or offset words)."""
+    monkeypatch.setenv("SWBANK_STREAM", "2")
+    monkeypatch.setenv("SWBANK_STREAM_RAGGED", "1")
+    rng = np.random.default_rng(5)
+    q = rng.integers(0, 4, 96, dtype=np.uint8)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        for seed in range(3):
+            res, offs, lens = _ragged(np.random.default_rng(100 + seed), 20_000, 30, 160,
+                                      p_n=0.003)
+            got = bank.score_batch(res, offs, lens)
+            assert "streamed=" in bank.last_kernel()
+            sel = rng.choice(len(lens), 300, replace=False)
+            sub = [res[int(offs[j]):int(offs[j]) + int(lens[j])] for j in sel]
+            want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(), -12, -4)
+            assert np.array_equal(got[sel], want), seed
 
 
 @pytest.mark.parametrize("kind", ["code", "range"])
