@@ -97,12 +97,15 @@ static std::vector<size_t> chunk_bounds(size_t total) {
   size_t sz = first_kb > 0 ? (size_t)first_kb << 10
               : env_int("SWBANK_CHUNK_MB", 0) > 0 ? cap : std::max<size_t>(1 << 20, cap / 4);
   for (size_t at = sz; at < total; at += sz, sz = std::min(cap, sz * 2)) bounds.push_back(at);
-  // SWBANK_CHUNK_TAIL=1: the last chunk as a half and two quarters, so the call's final
-  // launches (which nothing overlaps) are short
-  const size_t last = bounds.empty() ? 0 : bounds.back(), rem = total - last;
-  if (env_int("SWBANK_CHUNK_TAIL", 0) != 0 && rem >= ((size_t)4 << 20)) {
-    bounds.push_back(last + rem / 2);
-    bounds.push_back(last + rem / 2 + rem / 4);
+  // SWBANK_CHUNK_TAIL=k: the last chunk cut in halves k + 1 times (k = 1: a half and two
+  // quarters), so the call's final copy, sort and launch (which nothing overlaps) are short
+  const size_t last = bounds.empty() ? 0 : bounds.back();
+  const int tail = env_int("SWBANK_CHUNK_TAIL", 0);
+  for (size_t at = last, rem = total - last, i = 0;
+       tail > 0 && i < (size_t)tail + 1 && rem >= ((size_t)2 << 20); ++i) {
+    at += rem / 2;
+    rem -= rem / 2;
+    bounds.push_back(at);
   }
   return bounds;
 }
