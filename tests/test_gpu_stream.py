@@ -516,3 +516,42 @@ def test_stream_ragged_errors(monkeypatch, kind, poisoned_buffers):
     sel = rng.choice(len(lens), 300, replace=False)
     sub = [res[int(offs[j]):int(offs[j]) + int(lens[j])] for j in sel]
     assert np.array_equal(got[sel], O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(), -12, -4))
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_stream_ragged_fuzz(monkeypatch, seed):
+    """Seeded ragged streamed batches: random lengths (incl. empty), N rates, gaps between and
+    shuffles of the targets in the residues, match/mismatch/gap penalties, both gap models and
+    f16/u16 -- every call equal to the chunked feeder's scores and to the oracle on a sample."""
+    rng = np.random.default_rng(9000 + seed)
+    monkeypatch.setenv("SWBANK_STREAM", "2")
+    monkeypatch.setenv("SWBANK_STREAM_RAGGED", "1")
+    if rng.random() < 0.3:
+        monkeypatch.setenv("SWBANK_F16", "0")
+    if rng.random() < 0.2:
+        monkeypatch.setenv("SWBANK_MIXED_RUNS", "0")
+    n = int(rng.integers(300, 20_000))
+    lo = int(rng.integers(0, 60))
+    hi = lo + int(rng.integers(1, 400))
+    res, offs, lens = _ragged(rng, n, lo, hi, p_n=float(rng.choice([0.0, 0.0005, 0.01, 0.2])),
+                              gap=int(rng.choice([0, 0, 1, 5])))
+    if rng.random() < 0.25:
+        perm = rng.permutation(n)
+        offs, lens = offs[perm].copy(), lens[perm].copy()
+    ma, mm = int(rng.integers(1, 8)), -int(rng.integers(1, 8))
+    go, ge = -int(rng.integers(1, 16)), -int(rng.integers(1, 5))
+    gotoh = rng.random() < 0.4
+    q = rng.integers(0, 4, int(rng.integers(1, 200)), dtype=np.uint8)
+    with S.ScoreBank(gap_model=S.GAP_GOTOH if gotoh else S.GAP_MERGED) as bank:
+        bank.set_penalties(ma, mm, go, ge)
+        bank.load_query(q)
+        got = bank.score_batch(res, offs, lens)
+        kern = bank.last_kernel()
+        monkeypatch.setenv("SWBANK_STREAM_RAGGED", "0")
+        ref = bank.score_batch(res, offs, lens)
+    assert np.array_equal(got, ref), kern
+    sel = np.unique(np.concatenate([rng.choice(n, min(n, 200), replace=False), [n - 1]]))
+    sub = [res[int(offs[k]):int(offs[k]) + int(lens[k])] for k in sel]
+    want = O.score_batch(q, *S.pack_targets(sub), O.dna_matrix(ma, mm), go, ge,
+                         O.GAP_GOTOH if gotoh else O.GAP_MERGED)
+    assert np.array_equal(got[sel], want), kern
