@@ -1483,6 +1483,12 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
 #ifndef SWK_HALF_UNROLL
 #define SWK_HALF_UNROLL 4  // two-pairs wave kernel: steps per loop iteration (2 or 4)
 #endif
+#ifndef SWK_HALF_PRIO
+#define SWK_HALF_PRIO 0  // two-pairs wave kernel: issue priority of the main waves (split tail: 0)
+#endif
+#ifndef SWK_TAIL_PRIO
+#define SWK_TAIL_PRIO 0  // ... and of the split tail's segment waves (A/B)
+#endif
 #ifndef SWK_HALF_AHEAD
 #define SWK_HALF_AHEAD 1  // two-pairs wave kernel: profile words one step ahead
 #endif
@@ -2369,6 +2375,7 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
   uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
   const int lane = threadIdx.x & 63;
   if (blockIdx.x < a.split_blocks) {  // block-uniform
+    if (SWK_TAIL_PRIO > 0) __builtin_amdgcn_s_setprio(SWK_TAIL_PRIO);
     if (a.split_P == 4) wave_split_block<2, 4, false, true, GOTOH, true>(a, smem, lane);
     else wave_split_block<4, 2, false, true, GOTOH, true>(a, smem, lane);
     return;
@@ -2381,6 +2388,9 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
       reinterpret_cast<uint4*>(prof)[(i & ~63u) | (i & 1u) << 5 | (i & 63u) >> 1] = src[i];
     __syncthreads();
   }
+  // SWK_HALF_PRIO > 0: the main waves issue ahead of the split tail's segment waves, which then
+  // fill the issue slots the main waves leave idle instead of stretching their SIMDs
+  if (SWK_HALF_PRIO > 0) __builtin_amdgcn_s_setprio(SWK_HALF_PRIO);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const size_t p0 = 2 * ((size_t)(blockIdx.x - a.split_blocks) * (blockDim.x >> 6) + wave);
   const size_t n = a.n;
