@@ -438,7 +438,12 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   HostPool& pool = *b->pool;
   const unsigned T = pool.size();
   const unsigned P = n >= 65536 ? T : 1;
-  const size_t pstep = (n + P - 1) / P;
+  // parts of whole 1024-target blocks: the pass also keeps each block's code count, from which
+  // the chunk cuts below are found without a second pass over the lengths
+  constexpr size_t CB = 1024;
+  const size_t pstep = ((n + P - 1) / P + CB - 1) / CB * CB;
+  const size_t nblk = (n + CB - 1) / CB;
+  std::vector<size_t> cpre(nblk + 1, 0);  // block code counts, then their exclusive prefix
   const auto run_parts = [&](const std::function<void(unsigned)>& f) {
     if (P > 1) pool.run(f);
     else f(0u);
@@ -448,10 +453,16 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   run_parts([&](unsigned p) {
     size_t acc = 0;
     uint32_t m = 0, mn = UINT32_MAX;
-    for (size_t k = std::min(n, p * pstep); k < std::min(n, (p + 1) * pstep); ++k) {
-      acc += lens[k];
-      m = std::max(m, lens[k]);
-      mn = std::min(mn, lens[k]);
+    const size_t e = std::min(n, (p + 1) * pstep);
+    for (size_t b0 = std::min(n, p * pstep); b0 < e; b0 += CB) {
+      size_t bs = 0;
+      for (size_t k = b0; k < std::min(e, b0 + CB); ++k) {
+        bs += lens[k];
+        m = std::max(m, lens[k]);
+        mn = std::min(mn, lens[k]);
+      }
+      cpre[b0 / CB + 1] = bs;
+      acc += bs;
     }
     psum[p + 1] = acc;
     pmax[p] = m;
@@ -480,20 +491,7 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   const auto codes_at = [](size_t cnt) { return align16(cnt * 16 + 8); };
   std::vector<size_t> bounds = chunk_bounds(total);
   bounds.push_back(SIZE_MAX);  // sentinel
-  std::vector<std::vector<std::pair<size_t, size_t>>> pcut(P);  // (end position, code prefix)
-  run_parts([&](unsigned p) {
-    size_t acc = psum[p];
-    // the next boundary above this part's start; a cut after target k when the running code
-    // count reaches it (several boundaries inside one target make one cut)
-    size_t j = std::upper_bound(bounds.begin(), bounds.end(), acc) - bounds.begin();
-    for (size_t k = std::min(n, p * pstep); k < std::min(n, (p + 1) * pstep); ++k) {
-      acc += lens[k];
-      if (acc >= bounds[j]) {
-        while (acc >= bounds[j]) ++j;
-        if (k + 1 < n) pcut[p].push_back({k + 1, acc});
-      }
-    }
-  });
+  for (size_t i = 0; i < nblk; ++i) cpre[i + 1] += cpre[i];
   std::vector<Chunk> chunks;
   size_t c0 = 0, a0 = 0;
   const auto add_chunk = [&](size_t c1, size_t a1) {
@@ -501,8 +499,19 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     c0 = c1;
     a0 = a1;
   };
-  for (const auto& cuts : pcut)
-    for (const auto& ca : cuts) add_chunk(ca.first, ca.second);
+  // a cut after target k when the running code count reaches the next boundary (several
+  // boundaries inside one target make one cut): the block where the count crosses it (the block
+  // prefix), then a scan of that block only
+  for (size_t j = 0, blk = 0; bounds[j] <= total;) {
+    const size_t B = bounds[j];
+    while (blk + 1 < nblk && cpre[blk + 1] < B) ++blk;
+    size_t acc = cpre[blk], k = blk * CB;
+    for (; k < n; ++k)
+      if ((acc += lens[k]) >= B) break;
+    if (k >= n) break;  // (not reached: B <= total)
+    while (bounds[j] <= acc) ++j;
+    if (k + 1 < n) add_chunk(k + 1, acc);
+  }
   trace_mark("cuts");
   add_chunk(n, total);
   std::vector<uint32_t> chunk_max(chunks.size(), 0);  // set by the chunk's gather
