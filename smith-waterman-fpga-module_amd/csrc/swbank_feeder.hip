@@ -170,11 +170,14 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
       b->out_ev.push_back(e);
     }
   }
-  // overlapped chunk launches run two at a time: each takes at most SWBANK_CHUNK_OCC (2)
-  // workgroups per CU, so a chunk's tiles are several per workgroup (less pipeline fill and
-  // drain per tile) and the two streams share the chip (a per-thread setting: set by the
+  // overlapped chunk launches may run two at a time; SWBANK_CHUNK_OCC=m caps each at m
+  // workgroups per CU so the two streams share the chip (a per-thread setting: set by the
   // thread that launches)
-  const int occ = overlap ? std::max(0, env_int("SWBANK_CHUNK_OCC", 2)) : 0;
+  // (round 3: no cap by default.  With the launch thread and 6 device slots the chunk kernels
+  // are paced by the gather and mostly run one at a time, and a half-chip kernel running alone
+  // took ~220 us per 1/8 chunk against ~175 at full occupancy; SWBANK_CHUNK_OCC=2 restores the
+  // cap)
+  const int occ = overlap ? std::max(0, env_int("SWBANK_CHUNK_OCC", 0)) : 0;
   Launcher* lz = b->launcher.get();
   if (lz) lz->reset();
   const auto fail_sync = [&](sw_status s) {
