@@ -90,6 +90,8 @@ def parse():
                     help="q100xdata500 / data500 / ragged: copies of the 499-target data500 "
                          "batch per GPU")
     ap.add_argument("--target-len", type=int, default=128)
+    ap.add_argument("--targets", type=int, default=0,
+                    help="q100xdata500: targets per GPU (default --reps x 499)")
     ap.add_argument("--reads", type=int, default=131072, help="reads150x1k: reads per GPU")
     ap.add_argument("--slice", type=int, default=16, help="reads150x1k: 1-kbp targets")
     ap.add_argument("--ptargets", type=int, default=12500, help="protein512x1k: per GPU")
@@ -159,12 +161,12 @@ class Workload:
             self.bank = S.ScoreBank(device=dev.index)
             self.bank.set_penalties(*PEN)
         if w == "q100xdata500":
-            n, L = 499 * args.reps, args.target_len
+            n, L = args.targets or 499 * args.reps, args.target_len
             self.set_uniform(make_codes(1000 + rank, n, L))
             self.name = f"query100x{n}x{L}"
-            self.desc = (f"query100.fa (128 bp) x synthetic data500-shaped batch: {args.reps} x "
-                         f"499 seeded uniform-ACGT {L}-bp targets per GPU (the shape of "
-                         f"data/data500.fa; BASELINE configs[2])")
+            self.desc = (f"query100.fa (128 bp) x synthetic data500-shaped batch: {n} "
+                         f"(= {n / 499:g} x 499) seeded uniform-ACGT {L}-bp targets per GPU (the "
+                         f"shape of data/data500.fa; BASELINE configs[2])")
         elif w == "data500":
             from oracle.oracle import encode_dna, golden_fasta, read_fasta
             lib = [encode_dna(sq) for _, sq in read_fasta(golden_fasta("data500.fa"))]

@@ -52,8 +52,10 @@ extern "C" {
 
 /* ABI 2: ids on the batch calls and the batch best hit (ScoreBank_v2.v:39-43), multi-device
  * banks (sw_config.n_devices / devices[]), scores past the 16-bit lanes (int32 re-score).
- * ABI 3: sw_score_batch_device_range (caller length range) and sw_bank_counters. */
-#define SWBANK_ABI_VERSION 3
+ * ABI 3: sw_score_batch_device_range (caller length range) and sw_bank_counters.
+ * ABI 4: sw_bank_counters takes the caller's struct size; multi-device banks take device
+ *        batches and query sets. */
+#define SWBANK_ABI_VERSION 4
 
 typedef int32_t sw_status;
 enum {
@@ -125,7 +127,8 @@ sw_status sw_load_query(sw_bank *bank, uint64_t id, const uint8_t *codes, uint32
  * of the set into d_scores[i * n + k] (query-major), in one launch per query segment (the
  * tile kernel streams (query, tile) units, so a workgroup scores many tiles per launch); the
  * other scoring calls return SW_ERR_STATE while a set of more than one query is loaded.
- * nq == 1 is sw_load_query.  Single-device banks. */
+ * nq == 1 is sw_load_query.  A multi-device bank loads the set on every device (the
+ * reference broadcasts its query to every module, ScoreBank_v2.v:101-102). */
 sw_status sw_load_queries(sw_bank *bank, size_t nq, const uint64_t *ids, const uint8_t *codes,
                           const uint64_t *offsets, const uint32_t *lens);
 
@@ -150,7 +153,11 @@ sw_status sw_score_batch(sw_bank *bank, const uint8_t *residues, size_t residues
  * lengths differ, then longest first (an on-device length sort).  d_scores receives int32
  * scores in input order.  With d_ids (device, may be NULL) the call also records the batch's
  * best hit on the device (sw_batch_best); without, it records nothing.  Nothing is copied to
- * or from the host.  Single-device banks only (SW_ERR_UNSUPPORTED on a multi-device bank).
+ * or from the host.  On a multi-device bank (ABI 4) the buffers and the stream belong to the
+ * root device (devices[0]): device d scores the contiguous range [n*d/D, n*(d+1)/D) reading the
+ * root's buffers through peer access and writes its scores into d_scores, its work ordered
+ * after the caller's stream and the caller's stream after it (SW_ERR_UNSUPPORTED when a device
+ * cannot access the root's memory).
  * Device memory is not validated: the caller keeps every target inside d_residues
  * (d_offsets[k] + d_lens[k] <= its size) and every d_lens[k] <= max_len. */
 sw_status sw_score_batch_device(sw_bank *bank, const uint8_t *d_residues,
@@ -191,7 +198,8 @@ sw_status sw_load_query_record(sw_bank *bank, const void *record);
 /* Host records in, unbiased scores out in input order (the kernel reads the 2-bit codes); the
  * best hit (sw_batch_best) carries the record's ID.  Multi-device banks deal the records. */
 sw_status sw_score_records(sw_bank *bank, const void *records, size_t n, int32_t *scores_out);
-/* Device-resident records (n x 64 B) -> device scores, asynchronous on `stream`. */
+/* Device-resident records (n x 64 B) -> device scores, asynchronous on `stream` (a
+ * multi-device bank: contiguous ranges per device, as sw_score_batch_device). */
 sw_status sw_score_records_device(sw_bank *bank, const void *d_records, size_t n,
                                   int32_t *d_scores, void *stream);
 
@@ -220,6 +228,9 @@ sw_status sw_bank_timing(sw_bank *bank, uint64_t *launches, double *pack_ms, dou
  * device-side length sorts, multi-device gathers abandoned after their time limit, chunks
  * of chunked calls sent as mixed 2-bit / 4-bit codes (ragged DNA), and the pool parts of those
  * chunks packed as one run (targets back to back in the caller's residues). */
+/* out_size = sizeof(sw_counters) as the caller compiled it: the library writes that many bytes
+ * (its counters first, zeros past them), so a struct that grows in a later ABI never overflows
+ * an older caller's buffer. */
 typedef struct sw_counters {
   uint64_t stream_calls;
   uint64_t stream_reruns;
@@ -230,7 +241,7 @@ typedef struct sw_counters {
   uint64_t mixed_chunks;
   uint64_t mixed_runs;
 } sw_counters;
-sw_status sw_bank_counters(const sw_bank *bank, sw_counters *out);
+sw_status sw_bank_counters(const sw_bank *bank, sw_counters *out, size_t out_size);
 
 /* Which kernel the last score call ran, e.g. "tile f16 R=32 W=4 segs=1 grid=998" or
  * "wave u16 K=4" (empty before the first call).  No reference counterpart: the RTL has one

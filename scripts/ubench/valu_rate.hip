@@ -9,16 +9,18 @@
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 #define ITERS 4096
 
-template <int KIND>
+// NC: independent chains per thread (8: issue rate; 1-4: how much a wave's own dependency
+// chains limit it at few waves per SIMD)
+template <int KIND, int NC = 8>
 __global__ void __launch_bounds__(256) k(uint32_t* out, uint32_t seed, unsigned long long* ticks) {
   uint32_t a[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) a[i] = seed * (threadIdx.x + 1) + i * 77;
   const uint32_t b = seed ^ 0x00050005u;
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
-  for (int it = 0; it < ITERS; ++it) {
+  for (int it = 0; it < ITERS * 8 / NC; ++it) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NC; ++i) {
       if (KIND == 0) {  // v_pk_max_u16
         u16x2 x = __builtin_bit_cast(u16x2, a[i]), y = __builtin_bit_cast(u16x2, b);
         a[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y) + (u16x2){1, 1});
@@ -84,7 +86,7 @@ __global__ void __launch_bounds__(256) k(uint32_t* out, uint32_t seed, unsigned 
   if (threadIdx.x == 0) atomicAdd(ticks, t1 - t0);
 }
 
-template <int KIND>
+template <int KIND, int NC = 8>
 void run(const char* name, int blocks) {
   uint32_t* out;
   unsigned long long* ticks;
@@ -93,10 +95,10 @@ void run(const char* name, int blocks) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(256), 0, 0, out, 3u, ticks);
+  hipLaunchKernelGGL((k<KIND, NC>), dim3(blocks), dim3(256), 0, 0, out, 3u, ticks);
   hipMemset(ticks, 0, 8);
   hipEventRecord(e0);
-  hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(256), 0, 0, out, 3u, ticks);
+  hipLaunchKernelGGL((k<KIND, NC>), dim3(blocks), dim3(256), 0, 0, out, 3u, ticks);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms;
@@ -106,15 +108,17 @@ void run(const char* name, int blocks) {
   const double waves = blocks * 4.0;
   const double instr = waves * ITERS * 8 * 2;  // 2 VALU per chain step
   const double simd_cycles = 1024.0 * ms * 1e-3 * 2.4e9;
-  printf("{\"kind\": \"%s\", \"blocks\": %d, \"ms\": %.3f, \"wave_instr_per_simd_cycle_at_2.4GHz\": %.3f, "
-         "\"avg_wave_ticks\": %.0f}\n",
-         name, blocks, ms, instr / simd_cycles, (double)t / blocks);
+  printf("{\"kind\": \"%s\", \"chains\": %d, \"blocks\": %d, \"waves_per_simd\": %.2f, "
+         "\"ms\": %.3f, \"wave_instr_per_simd_cycle_at_2.4GHz\": %.3f, \"avg_wave_ticks\": %.0f}\n",
+         name, NC, blocks, waves / 1024.0, ms, instr / simd_cycles, (double)t / blocks);
   hipFree(out);
   hipFree(ticks);
 }
 
 int main() {
-  for (int blocks : {2048, 8192}) {
+  // issue rates at 4 and 8 resident waves per SIMD (1,024 / 2,048 blocks of 4 waves), and a
+  // longer run (8,192 blocks: 32 waves per SIMD over time)
+  for (int blocks : {1024, 2048, 8192}) {
     run<0>("v_pk_max_u16+v_pk_add_u16", blocks);
     run<1>("v_max_u32+v_add_u32", blocks);
     run<2>("v_perm_b32+v_add_u32", blocks);
@@ -126,6 +130,14 @@ int main() {
     run<8>("mix: pk_f16 add+max3 (4 chains) | f32 add+max (4 chains)", blocks);
     run<9>("v_add_f32_e64 clamp+v_max3_f32", blocks);
     run<10>("mix: u32 max+add (4 chains) | f32 add+max (4 chains)", blocks);
+  }
+  // dependency-limited issue: the packed f16 pair with 1, 2 or 4 chains per wave at 1-4 waves
+  // per SIMD (the wave kernel runs 3 waves per SIMD on configs[4])
+  for (int blocks : {256, 512, 768, 1024}) {
+    run<6, 1>("v_pk_add_f16+v_pk_maximum3_f16", blocks);
+    run<6, 2>("v_pk_add_f16+v_pk_maximum3_f16", blocks);
+    run<6, 4>("v_pk_add_f16+v_pk_maximum3_f16", blocks);
+    run<6, 8>("v_pk_add_f16+v_pk_maximum3_f16", blocks);
   }
   return 0;
 }

@@ -480,6 +480,13 @@ struct sw_bank {
   unsigned pool_threads = 0; // feeder threads (0: host_threads(); children share the host)
   DevBuf<int32_t> grecv;
   PinBuf hrecv;
+  // device batches on a multi-device bank (multi_device): every child's kernels read the
+  // caller's buffers on the root device through peer access, enabled once (peer_ready);
+  // ev_join: a child's work on its stream is done (the caller's stream waits on it);
+  // best_root: the last device call's best hit is tracked by kids[0]
+  bool peer_ready = false;
+  hipEvent_t ev_join = nullptr;
+  bool best_root = false;
   // on-device longest-first order of a ragged device batch (sw_score_batch_device):
   // dperm = visiting order + count, dsort = histogram / scan scratch
   DevBuf<uint32_t> dperm, dsort;
@@ -615,5 +622,17 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres, const ui
 sw_status multi_batch(sw_bank* b, const uint8_t* residues, size_t nres, const uint64_t* offsets,
                       const uint32_t* lens, size_t n, int32_t* scores_out);
 sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_t* scores_out);
+// Device buffers (on the root device, devices[0]) over a multi-device bank: contiguous ranges
+// of the batch, one per device, asynchronous on the caller's stream (records: n x 64-B
+// records at d_res, d_offs / d_lens unused).
+sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
+                       const uint32_t* d_lens, const uint64_t* d_ids, size_t n, uint32_t min_len,
+                       uint32_t max_len, int32_t* d_scores, hipStream_t hs, bool records);
+// ---- swbank_launch.hip (device batches against a query set; sstride: between query rows)
+sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
+                     const uint32_t* d_lens, size_t n, uint32_t min_len, uint32_t max_len,
+                     int32_t* d_scores, hipStream_t st, size_t sstride);
+sw_status track_best_device(sw_bank* b, const int32_t* d_scores, const uint64_t* d_ids, size_t n,
+                            hipStream_t st);
 
 #endif  // SWBANK_BANK_H

@@ -144,6 +144,8 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   if (b->is_multi() || !b->comms.empty()) {
     const Rccl& r = rccl();
     for (void* c : b->comms) (void)r.commDestroy(static_cast<ncclComm_t>(c));
+    (void)hipSetDevice(b->device);
+    if (b->ev_join) (void)hipEventDestroy(b->ev_join);
     for (sw_bank* k : b->kids) sw_bank_destroy(k);
     b->dpool.reset();
     b->pool.reset();
@@ -168,6 +170,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   if (b->ev_ready) (void)hipEventDestroy(b->ev_ready);
   if (b->ev_used) (void)hipEventDestroy(b->ev_used);
   if (b->best_ev) (void)hipEventDestroy(b->best_ev);
+  if (b->ev_join) (void)hipEventDestroy(b->ev_join);
   b->fb_idx.release();
   b->fb_cnt.release();
   b->best_key.release();
@@ -234,19 +237,22 @@ extern "C" const char* sw_last_error(const sw_bank* b) { return b ? b->err : "nu
 
 extern "C" const char* sw_last_kernel(const sw_bank* b) { return b ? b->last_kernel : ""; }
 
-extern "C" sw_status sw_bank_counters(const sw_bank* b, sw_counters* out) {
+extern "C" sw_status sw_bank_counters(const sw_bank* b, sw_counters* out, size_t out_size) {
   if (!b || !out) return SW_ERR_ARG;
-  *out = b->ctr;
+  sw_counters c = b->ctr;
   for (const sw_bank* k : b->kids) {
-    out->stream_calls += k->ctr.stream_calls;
-    out->stream_reruns += k->ctr.stream_reruns;
-    out->stream_declined += k->ctr.stream_declined;
-    out->chunked_calls += k->ctr.chunked_calls;
-    out->device_sorts += k->ctr.device_sorts;
-    out->gather_timeouts += k->ctr.gather_timeouts;
-    out->mixed_chunks += k->ctr.mixed_chunks;
-    out->mixed_runs += k->ctr.mixed_runs;
+    c.stream_calls += k->ctr.stream_calls;
+    c.stream_reruns += k->ctr.stream_reruns;
+    c.stream_declined += k->ctr.stream_declined;
+    c.chunked_calls += k->ctr.chunked_calls;
+    c.device_sorts += k->ctr.device_sorts;
+    c.gather_timeouts += k->ctr.gather_timeouts;
+    c.mixed_chunks += k->ctr.mixed_chunks;
+    c.mixed_runs += k->ctr.mixed_runs;
   }
+  // a caller built against an older (shorter) struct gets its prefix, a newer one zeroes past ours
+  std::memset(out, 0, out_size);
+  std::memcpy(out, &c, std::min(out_size, sizeof(c)));
   return SW_OK;
 }
 
@@ -296,8 +302,12 @@ extern "C" sw_status sw_set_matrix(sw_bank* b, const int8_t* m, int32_t alpha, i
 
 extern "C" sw_status sw_load_query(sw_bank* b, uint64_t id, const uint8_t* codes, uint32_t len) {
   if (!b || (!codes && len)) return SW_ERR_ARG;
-  if (b->is_multi())
-    return each_kid(b, [&](sw_bank* k) { return sw_load_query(k, id, codes, len); });
+  if (b->is_multi()) {  // the query goes to every device (ScoreBank_v2.v:101-102)
+    const sw_status st = each_kid(b, [&](sw_bank* k) { return sw_load_query(k, id, codes, len); });
+    b->qset.clear();
+    b->have_query = st == SW_OK;
+    return st;
+  }
   const uint32_t cap = b->cfg.max_query_len ? b->cfg.max_query_len : SWB_MAX_QUERY;
   if (len > cap)
     return fail(b, SW_ERR_UNSUPPORTED, "query length %u exceeds the bank maximum %u", len, cap);
@@ -318,8 +328,13 @@ extern "C" sw_status sw_load_queries(sw_bank* b, size_t nq, const uint64_t* ids,
                                      const uint8_t* codes, const uint64_t* offsets,
                                      const uint32_t* lens) {
   if (!b || nq == 0 || !offsets || !lens) return SW_ERR_ARG;
-  if (b->is_multi())
-    return fail(b, SW_ERR_UNSUPPORTED, "query sets need a single-device bank");
+  if (b->is_multi()) {  // the set goes to every device (ScoreBank_v2.v:101-102)
+    const sw_status st = each_kid(
+        b, [&](sw_bank* k) { return sw_load_queries(k, nq, ids, codes, offsets, lens); });
+    b->qset = b->kids[0]->qset;  // (sizes only: the guards and sw_query_count read it)
+    b->have_query = st == SW_OK;
+    return st;
+  }
   if (nq > 65536) return fail(b, SW_ERR_UNSUPPORTED, "more than 65536 queries in one set");
   if (nq == 1) return sw_load_query(b, ids ? ids[0] : 0, codes + offsets[0], lens[0]);
   const uint32_t cap = b->cfg.max_query_len ? b->cfg.max_query_len : SWB_MAX_QUERY;
@@ -431,7 +446,10 @@ sw_status prepare(sw_bank* b) {
   // as segments of SWBANK_SEG rows (default: a full 16-wave workgroup, 16·R rows), each
   // segment's bottom row handed to the next through HBM.  SWBANK_R / SWBANK_RB / SWBANK_SEG
   // override (tuning only).
-  int R = (qlen <= 16 || prof || col0) ? 16 : 32, RB = 4;
+  // u16 Gotoh keeps R = 16 when no f16 pass can run (its 32-row column spills past 128 VGPRs);
+  // u16 passes that follow an f16 pass (optimistic re-scores) are rare and use the f16 layout
+  const bool u16_only = gotoh && (!f16_range || env_int("SWBANK_F16", 1) == 0);
+  int R = (qlen <= 16 || prof || col0 || u16_only) ? 16 : 32, RB = 4;
   R = env_int("SWBANK_R", R);
   RB = env_int("SWBANK_RB", RB);
   const int max_rows = (R >= 64 ? 8 : 16) * R;
@@ -854,8 +872,9 @@ extern "C" sw_status sw_bank_timing(sw_bank* b, uint64_t* launches, double* pack
 extern "C" sw_status sw_best_hit_device(sw_bank* b, const int32_t* d_scores, const uint64_t* d_ids,
                                         size_t n, uint64_t* d_out, void* stream) {
   if (!b) return SW_ERR_ARG;
-  if (b->is_multi())
-    return fail(b, SW_ERR_UNSUPPORTED, "device buffers need a single-device bank");
+  if (b->is_multi())  // on the root device, where the multi-device calls leave the scores
+    return sw_best_hit_device(b->kids[0], d_scores, d_ids, n, d_out,
+                              stream ? stream : b->kids[0]->stream);
   if (!d_scores || !d_out || n == 0 || n > 0xFFFFFFFFull)
     return fail(b, SW_ERR_ARG, "sw_best_hit_device: empty, null or > 2^32 scores");
   HIPOK(b, hipSetDevice(b->device));

@@ -188,6 +188,17 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     (void)hipStreamSynchronize(b->out_stream);
     return s;
   };
+  // a HIP failure once jobs are posted: the launch thread may still hold jobs that reference
+  // this frame (launch_chunk, chunks, the caller's gather state), so drain it before returning.
+  // SWBANK_FEED_FAULT=k (a test hook) reports a failure at sync point k: chunk k's slot wait
+  // (NSLOT <= k < chunks, jobs in flight), then the stream join, each chunk's result wait and
+  // the final sync
+  const int fault_at = env_int("SWBANK_FEED_FAULT", -1);
+  const auto hip_sync = [&](hipError_t e, size_t i, const char* what) -> sw_status {
+    if (e == hipSuccess && fault_at >= 0 && (size_t)fault_at == i) e = hipErrorLaunchFailure;
+    if (e == hipSuccess) return SW_OK;
+    return fail_sync(fail(b, SW_ERR_HIP, "%s (chunk %zu): %s", what, i, hipGetErrorString(e)));
+  };
   PhaseTrace* tr = g_trace;
   // chunk i's HIP work: its copy once slot s is free, the score launches, the scores' return
   const auto launch_chunk = [&, tr](size_t i, size_t from, size_t bytes) -> sw_status {
@@ -220,7 +231,8 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     if (i >= (size_t)sw_bank::NSLOT) {
       // slot s is free once chunk i - NSLOT's copy (enqueued by the launch thread) landed
       if (lz && (st = lz->wait(i - sw_bank::NSLOT + 1)) != SW_OK) return fail_sync(st);
-      HIPOK(b, hipEventSynchronize(b->h2d_done[s]));
+      if ((st = hip_sync(hipEventSynchronize(b->h2d_done[s]), i, "slot wait")) != SW_OK)
+        return st;
     }
     trace_mark("gather<");
     const auto t0 = std::chrono::steady_clock::now();
@@ -238,8 +250,11 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   }
   if (lz && (st = lz->wait_all()) != SW_OK) return fail_sync(st);
   if (overlap) {  // the bank stream (the multi-device gather, the next call) after stream2
-    HIPOK(b, hipEventRecord(b->ev_s2, b->stream2));
-    HIPOK(b, hipStreamWaitEvent(b->stream, b->ev_s2, 0));
+    if ((st = hip_sync(hipEventRecord(b->ev_s2, b->stream2), chunks.size(), "stream join")) !=
+            SW_OK ||
+        (st = hip_sync(hipStreamWaitEvent(b->stream, b->ev_s2, 0), chunks.size(),
+                       "stream join")) != SW_OK)
+      return st;
   }
   if (!out) return SW_OK;
   // scores into the caller's buffer as they land, with the best hit: per pool part the lowest
@@ -250,7 +265,9 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   size_t best = 0;
   for (size_t i = 0; i < chunks.size(); ++i) {
     const Chunk& c = chunks[i];
-    HIPOK(b, hipEventSynchronize(b->out_ev[i]));
+    if ((st = hip_sync(hipEventSynchronize(b->out_ev[i]), chunks.size() + i, "scores wait")) !=
+        SW_OK)
+      return st;
     trace_mark("landed");
     const size_t cnt = c.c1 - c.c0;
     const unsigned parts = cnt >= 4096 ? T : 1;
@@ -275,7 +292,8 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   b->best_id = best;
   b->best_score = hs[best];
   b->best_kind = 1;
-  HIPOK(b, hipStreamSynchronize(b->stream));
+  if ((st = hip_sync(hipStreamSynchronize(b->stream), 2 * chunks.size(), "final sync")) != SW_OK)
+    return st;
   trace_mark("done");
   return SW_OK;
 }
@@ -830,12 +848,14 @@ extern "C" sw_status sw_score_records_device(sw_bank* b, const void* d_records, 
   if (b && b->qset.size() > 1)
     return fail(b, SW_ERR_STATE, "a query set is loaded: score it with sw_score_batch_device");
   if (!b) return SW_ERR_ARG;
-  if (b->is_multi())
-    return fail(b, SW_ERR_UNSUPPORTED, "device buffers need a single-device bank");
   b->best_kind = 0;
+  b->best_root = false;
   if (n == 0) return SW_OK;
   if (!d_records || !d_scores) return fail(b, SW_ERR_ARG, "null device buffer");
   if (b->alpha != SW_DNA_ALPHA) return fail(b, SW_ERR_UNSUPPORTED, "records carry DNA only");
+  if (b->is_multi())
+    return multi_device(b, static_cast<const uint8_t*>(d_records), nullptr, nullptr, nullptr, n,
+                        0, SWB_RECORD_MAX, d_scores, reinterpret_cast<hipStream_t>(stream), true);
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
   // lengths live on the device: the kernels clamp them to the record capacity

@@ -1464,38 +1464,14 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
 // generated row blocks as the tile kernel with the lane's own LUT words / profile words in
 // VGPRs.  K = 4: one 4-row block; K = 8, 16: 8-row blocks.
 #define SWK_CLAMP(x, n) ((x) < (n) ? (x) : (n) - 1)
-#ifndef SWK_RING_SPLIT
-#define SWK_RING_SPLIT 0  // the split tail's segment waves use the code ring too (A/B)
-#endif
 #ifndef SWK_RING_PF
 #define SWK_RING_PF 1  // wave kernel, f16 profile: read the code ring one step ahead
-#endif
-// (A/B toggles of the f16 profile wave kernel's main loop)
-#ifndef SWK_GROUP8
-#define SWK_GROUP8 0  // steps in groups of 8 (ring reads at immediate offsets)
-#endif
-#ifndef SWK_CODE_AHEAD
-#define SWK_CODE_AHEAD 0  // the next 64-column block's codes loaded one block ahead
-#endif
-#ifndef SWK_UNIFORM_PTR
-#define SWK_UNIFORM_PTR 0  // target pointers in SGPRs
 #endif
 #ifndef SWK_HALF_UNROLL
 #define SWK_HALF_UNROLL 4  // two-pairs wave kernel: steps per loop iteration (2 or 4)
 #endif
-#ifndef SWK_HALF_PRIO
-#define SWK_HALF_PRIO 0  // two-pairs wave kernel: issue priority of the main waves (split tail: 0)
-#endif
-#ifndef SWK_TAIL_PRIO
-#define SWK_TAIL_PRIO 0  // ... and of the split tail's segment waves (A/B)
-#endif
 #ifndef SWK_HALF_AHEAD
 #define SWK_HALF_AHEAD 1  // two-pairs wave kernel: profile words one step ahead
-#endif
-#ifndef SWK_PROF_AHEAD
-// wave kernel, f16 profile (with SWK_RING_PF): a step's profile words are loaded during the
-// step before (the letters two steps ahead), so no step waits on its own LDS reads
-#define SWK_PROF_AHEAD 0
 #endif
 #define SWK_W_HT(B)                                                                           \
   [h0] "+v"(Hl[B]), [h1] "+v"(Hl[SWK_CLAMP(B + 1, K)]), [h2] "+v"(Hl[SWK_CLAMP(B + 2, K)]),    \
@@ -1601,17 +1577,12 @@ __device__ __forceinline__ void column_f16_lane_asm(const LK& lk, u16x2& diag_, 
   best_ = best;
 }
 
-// A global-memory pointer every lane holds the same value of, moved to SGPRs (loads then take
-// it as the scalar base, and it costs no VGPRs).  The result is typed global (address space 1):
-// a generic pointer rebuilt from an integer would make its loads flat loads, which count on
-// the LDS counter too, so every LDS wait after one would wait for global memory.
+// A target pointer typed global (address space 1): its code loads are global loads, which
+// count on the vector-memory counter only (a flat load counts on the LDS counter too, so every
+// LDS wait after one would wait for global memory).
 template <class T>
-__device__ __forceinline__ __attribute__((address_space(1))) T* uniform_ptr(T* p) {
-  if (!SWK_UNIFORM_PTR) return (__attribute__((address_space(1))) T*)p;
-  const uint64_t v = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return (__attribute__((address_space(1))) T*)((uint64_t)hi << 32 | lo);
+__device__ __forceinline__ __attribute__((address_space(1))) T* global_ptr(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
 }
 
 // wave_pair's loop flavours: row -1 from a previous segment (in), bottom row written (out)
@@ -1649,7 +1620,7 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
                                            size_t pair, int lane, const uint2* lin = nullptr,
                                            uint2* lout = nullptr, int nph = 0, int seg = 0,
                                            int P = 1, uint8_t* cring = nullptr) {
-  constexpr bool RING = F16 && PROF && SWK_RING_SPLIT >= (SPLIT ? 1 : 0);
+  constexpr bool RING = F16 && PROF && !SPLIT;
   constexpr bool PF = SWK_RING_PF != 0;  // ring letters read one step ahead
   const size_t tA = 2 * pair, tB = tA + 1;
   const size_t n = a.n;
@@ -1661,11 +1632,10 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
                       : rec ? record_len(a.res + tB * SWB_RECORD)
                       : uni ? a.ulen
                             : a.lens[tB];
-  // (wave-uniform: kept in SGPRs, so each code load is one scalar base + a lane offset)
-  const auto pA = uniform_ptr(rec ? a.res + tA * SWB_RECORD + 6
+  const auto pA = global_ptr(rec ? a.res + tA * SWB_RECORD + 6
                                   : uni ? a.res + tA * a.ustride
                                         : a.res + (LA ? a.offs[tA] : 0));
-  const auto pB = uniform_ptr(rec ? a.res + (tB < n ? tB : tA) * SWB_RECORD + 6
+  const auto pB = global_ptr(rec ? a.res + (tB < n ? tB : tA) * SWB_RECORD + 6
                                   : uni ? a.res + (tB < n ? tB : tA) * a.ustride
                                         : a.res + (LB ? a.offs[tB] : 0));
   const int Lmax = (int)__builtin_amdgcn_readfirstlane(max(LA, LB));
@@ -1751,88 +1721,29 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
     ringprev = nc;
   };
   uint32_t nra = 0, nrb = 0;  // RING && PF: the letters of the next step's column
-  // RING && PF: this lane's ring position of step 0 (step T + j reads ring byte 64 + j - lane),
-  // and the codes of the next 64-column block, loaded one block ahead (global latency off the
-  // block boundary, where every wave of a SIMD would wait on it at about the same time)
+  // RING && PF: this lane's ring position of step 0 (step T + j reads ring byte 64 + j - lane)
   const uint8_t* const cring_l = RING && PF ? cring + 64 - lane : nullptr;
-  uint32_t ncode = 0;
-  // RING && PA: the next step's profile words, loaded one step ahead (nra / nrb then hold the
-  // letters of the step after it)
-  constexpr bool PA = RING && PF && SWK_PROF_AHEAD != 0;
-  ProfLookupK16<K> lkn;
-  const uint8_t* const plds = prof + lane * 2 * K;  // this lane's rows of letter 0 (RING)
-  const auto load_prof = [&](ProfLookupK16<K>& lk, uint32_t olo, uint32_t ohi)
-      __attribute__((always_inline)) {
-    if constexpr (K == 2) {
-      lk.lo[0] = *reinterpret_cast<const uint32_t*>(plds + olo);
-      lk.hi[0] = *reinterpret_cast<const uint32_t*>(plds + ohi);
-    } else if constexpr (K == 4) {
-      const uint2 x = *reinterpret_cast<const uint2*>(plds + olo);
-      const uint2 y = *reinterpret_cast<const uint2*>(plds + ohi);
-      lk.lo[0] = x.x; lk.lo[1] = x.y; lk.hi[0] = y.x; lk.hi[1] = y.y;
-    } else {
-#pragma unroll
-      for (int q = 0; q < K / 8; ++q) {
-        const uint4 x = reinterpret_cast<const uint4*>(plds + olo)[q];
-        const uint4 y = reinterpret_cast<const uint4*>(plds + ohi)[q];
-        lk.lo[4 * q] = x.x; lk.lo[4 * q + 1] = x.y; lk.lo[4 * q + 2] = x.z; lk.lo[4 * q + 3] = x.w;
-        lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z; lk.hi[4 * q + 3] = y.w;
-      }
-    }
-  };
   if constexpr (RING && PF) {
     ring_write(load_codes((uint32_t)lane));
-    if (SWK_CODE_AHEAD) ncode = load_codes(64u + lane);
-    if constexpr (PA) {
-      load_prof(lkn, __umul24((uint32_t)cring_l[0], PSb), __umul24((uint32_t)cring_l[128], PSb));
-      nra = cring_l[1];
-      nrb = cring_l[129];
-    } else {
-      nra = cring_l[0];
-      nrb = cring_l[128];
-    }
+    nra = cring_l[0];
+    nrb = cring_l[128];
   }
-  (void)load_prof;
-  // step t of the lane pipeline; J = t % 8 when the caller runs groups of 8 steps (RING && PF:
-  // the ring reads take immediate offsets from the group's base gb), else -1
-  const auto step = [&](const int t, const bool even, auto segc, auto jc,
-                        const uint8_t* gb) __attribute__((always_inline)) {
+  // step t of the lane pipeline
+  const auto step = [&](const int t, const bool even, auto segc) __attribute__((always_inline)) {
     constexpr bool SEG = decltype(segc)::in;  // query segment: row -1 from edge_in
-    // false: this loop never writes a bottom row (no per-step branch around the store, so the
-    // steps of a group stay one basic block); true: seg_out decides at run time
+    // false: this loop never writes a bottom row (no per-step branch around the store);
+    // true: seg_out decides at run time
     constexpr bool SEGO = decltype(segc)::out;
-    constexpr int J = decltype(jc)::value;
-    if ((J < 0 ? even : J == 0) && (t & 63) == 0) {  // next 64 columns, one code pair per lane
+    if (even && (t & 63) == 0) {  // next 64 columns, one code pair per lane
       const uint32_t c = (uint32_t)t + lane;
       if constexpr (RING && !PF) ring_write(load_codes(c));
       else if constexpr (!RING) buf = load_codes(c);
       if (SEG) ebuf = c < (uint32_t)Lmax ? ein[c & rmask] : make_uint2(as_u32(H0), as_u32(X0));
     }
     // prefetching ring: the next block's codes go in before step T + 64's codes are read
-    // (PA: two steps ahead, so at step T + 62)
     if constexpr (RING && PF) {
-      if ((J < 0 ? (PA ? even : !even) : J == (PA ? 6 : 7)) && (t & 63) == (PA ? 62 : 63)) {
-        if (SWK_CODE_AHEAD) {
-          ring_write(ncode);
-          ncode = load_codes((uint32_t)t + (PA ? 66u : 65u) + lane);
-        } else {
-          ring_write(load_codes((uint32_t)t + (PA ? 2u : 1u) + lane));
-        }
-      }
+      if (!even && (t & 63) == 63) ring_write(load_codes((uint32_t)t + 1u + lane));
     }
-    // PA: this step's profile words came in during the last step; first issue the next step's
-    // loads (its letters were read then) and read the letters of the step after.  They go
-    // ahead of the bottom-row DPP moves, which then need no wait states after the last column
-    ProfLookupK16<K> lkc;
-    if constexpr (F16 && PROF && PA) {
-      lkc = lkn;
-      load_prof(lkn, __umul24(nra, PSb), __umul24(nrb, PSb));
-      const uint8_t* np = J >= 0 && J + 2 < 8 ? gb + (J + 2) : cring_l + ((t + 2) & 63);
-      nra = np[0];
-      nrb = np[128];
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    (void)lkc;
     const uint32_t inj = RING ? 0u : __builtin_amdgcn_readlane(buf, t & 63);
     u16x2 upH, upX;
     if constexpr (SEG) {
@@ -1864,13 +1775,7 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (F16) {
       const bool z = COL0 && t == lane;
-      if constexpr (PROF && PA) {
-        const ProfLookupK16<K>& lk = lkc;
-        if constexpr (COL0)
-          column_merged_f16_mask<K, 4>(lk, diag, upX, Hl, Xl, best, NOE2, NE2, z);
-        else
-          column_f16_lane_asm<K, GOTOH>(lk, diag, upX, Hl, Xl, best, noe, ne, no);
-      } else if constexpr (PROF) {
+      if constexpr (PROF) {
         ProfLookupK16<K> lk;
         const uint8_t* lds = RING ? prof + lane * 2 * K : prof;
         const uint32_t olo = RING ? __umul24(rca, PSb) : let & 0xFFFFu;
@@ -1894,7 +1799,7 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
           }
         }
         if constexpr (RING && PF) {  // the next step's letters (block start: the new block)
-          const uint8_t* np = J >= 0 && J < 7 ? gb + (J + 1) : cring_l + ((t + 1) & 63);
+          const uint8_t* np = cring_l + ((t + 1) & 63);
           nra = np[0];
           nrb = np[128];
         }
@@ -1955,20 +1860,6 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
     if (SEGO && seg_out && lane == 63 && t >= 63 && t - 63 < Lmax)
       eout[(uint32_t)(t - 63) & rmask] = make_uint2(botH, botX);
   };
-  using JN = std::integral_constant<int, -1>;
-  // RING && PF: groups of 8 steps (a ring read's offset is an immediate from the group's base;
-  // up to 7 trailing all-padding steps change no score)
-  const auto group8 = [&](const int t, auto segc) __attribute__((always_inline)) {
-    const uint8_t* gb = cring_l + (t & 63);
-    step(t, true, segc, std::integral_constant<int, 0>{}, gb);
-    step(t + 1, false, segc, std::integral_constant<int, 1>{}, gb);
-    step(t + 2, true, segc, std::integral_constant<int, 2>{}, gb);
-    step(t + 3, false, segc, std::integral_constant<int, 3>{}, gb);
-    step(t + 4, true, segc, std::integral_constant<int, 4>{}, gb);
-    step(t + 5, false, segc, std::integral_constant<int, 5>{}, gb);
-    step(t + 6, true, segc, std::integral_constant<int, 6>{}, gb);
-    step(t + 7, false, segc, std::integral_constant<int, 7>{}, gb);
-  };
   if constexpr (SPLIT) {
     // every wave of the block takes part in every phase's barrier (wave-uniform branches)
     const int lag = 2 * seg;
@@ -1977,37 +1868,27 @@ __device__ __forceinline__ uint2 wave_pair(const ScoreArgs& a, const uint8_t* pr
       if (blk >= 0 && blk < nph) {
         if (seg_in) {
           for (int t = 64 * blk; t < 64 * blk + 64; t += 2) {
-            step(t, true, SegT<true, true>{}, JN{}, nullptr);
-            step(t + 1, false, SegT<true, true>{}, JN{}, nullptr);
+            step(t, true, SegT<true, true>{});
+            step(t + 1, false, SegT<true, true>{});
           }
         } else {
           for (int t = 64 * blk; t < 64 * blk + 64; t += 2) {
-            step(t, true, SegT<false, true>{}, JN{}, nullptr);
-            step(t + 1, false, SegT<false, true>{}, JN{}, nullptr);
+            step(t, true, SegT<false, true>{});
+            step(t + 1, false, SegT<false, true>{});
           }
         }
       }
       __syncthreads();
     }
-  } else if constexpr (RING && PF && SWK_GROUP8) {
-    if (seg_in && seg_out) {
-      for (int t = 0; t < nsteps; t += 8) group8(t, SegT<true, true>{});
-    } else if (seg_in) {
-      for (int t = 0; t < nsteps; t += 8) group8(t, SegT<true, false>{});
-    } else if (seg_out) {
-      for (int t = 0; t < nsteps; t += 8) group8(t, SegT<false, true>{});
-    } else {
-      for (int t = 0; t < nsteps; t += 8) group8(t, SegT<false, false>{});
-    }
   } else if (seg_in) {
     for (int t = 0; t < nsteps; t += 2) {
-      step(t, true, SegT<true, true>{}, JN{}, nullptr);
-      step(t + 1, false, SegT<true, true>{}, JN{}, nullptr);
+      step(t, true, SegT<true, true>{});
+      step(t + 1, false, SegT<true, true>{});
     }
   } else {
     for (int t = 0; t < nsteps; t += 2) {
-      step(t, true, SegT<false, true>{}, JN{}, nullptr);
-      step(t + 1, false, SegT<false, true>{}, JN{}, nullptr);
+      step(t, true, SegT<false, true>{});
+      step(t + 1, false, SegT<false, true>{});
     }
   }
   // max over the wave's rows, per target (f16: non-negative integers -> int)
@@ -2065,10 +1946,8 @@ __device__ __forceinline__ void wave_split_block(const ScoreArgs& a, uint32_t* s
   }
   const uint8_t* sprof = PROF ? prof + (size_t)seg * a.split_words * 4 : nullptr;
   const uint32_t* sq = a.split_qtab + (size_t)seg * a.split_words;
-  uint8_t* cring = F16 && PROF && SWK_RING_SPLIT
-                       ? prof + (size_t)P * a.split_words * 4 + 256 * wave : nullptr;
   uint2 b = wave_pair<KS, COL0, PROF, GOTOH, F16, true>(a, sprof, sq, a.nv, a.split_PS, p, lane,
-                                                         lin, lout, nph, seg, P, cring);
+                                                         lin, lout, nph, seg, P);
   // LDS is free again (the last phase ended with a barrier): combine the pair's segments
   uint32_t blockmax = 0;
   const auto combine = [&](uint2 v) -> uint2 {
@@ -2116,11 +1995,7 @@ __device__ __forceinline__ void wave_split_block(const ScoreArgs& a, uint32_t* s
 }
 
 template <int K, bool COL0, bool PROF, bool GOTOH, bool F16>
-// (SWK_PROF_AHEAD: the K = 8 f16 profile kernel must stay at <= 80 VGPRs, i.e. 6 waves per SIMD,
-// the occupancy its LDS allows; it needs 85 uncapped)
-__global__ void __launch_bounds__(512)
-    __attribute__((amdgpu_waves_per_eu(K == 8 && F16 && PROF && SWK_PROF_AHEAD ? 6 : 1)))
-    score_wave(const ScoreArgs a) {
+__global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
   const int lane = threadIdx.x & 63;
@@ -2178,9 +2053,7 @@ static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream
   size_t lds = PROF ? prof_bytes : 0;
   if (F16 && PROF) lds += 256 * wpb;  // the waves' code rings
   if (a.split_blocks)  // every segment's profile, or the 8 words of the segment combine
-    lds = std::max<size_t>(lds, PROF ? (size_t)a.split_words * 4 * a.split_P +
-                                           (F16 && SWK_RING_SPLIT ? 256 * 4 : 0)
-                                     : 64);
+    lds = std::max<size_t>(lds, PROF ? (size_t)a.split_words * 4 * a.split_P : 64);
   auto fn = &score_wave<K, COL0, PROF, GOTOH, F16>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -2375,7 +2248,6 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
   uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
   const int lane = threadIdx.x & 63;
   if (blockIdx.x < a.split_blocks) {  // block-uniform
-    if (SWK_TAIL_PRIO > 0) __builtin_amdgcn_s_setprio(SWK_TAIL_PRIO);
     if (a.split_P == 4) wave_split_block<2, 4, false, true, GOTOH, true>(a, smem, lane);
     else wave_split_block<4, 2, false, true, GOTOH, true>(a, smem, lane);
     return;
@@ -2388,9 +2260,6 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
       reinterpret_cast<uint4*>(prof)[(i & ~63u) | (i & 1u) << 5 | (i & 63u) >> 1] = src[i];
     __syncthreads();
   }
-  // SWK_HALF_PRIO > 0: the main waves issue ahead of the split tail's segment waves, which then
-  // fill the issue slots the main waves leave idle instead of stretching their SIMDs
-  if (SWK_HALF_PRIO > 0) __builtin_amdgcn_s_setprio(SWK_HALF_PRIO);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const size_t p0 = 2 * ((size_t)(blockIdx.x - a.split_blocks) * (blockDim.x >> 6) + wave);
   const size_t n = a.n;

@@ -331,8 +331,8 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
 }
 
 // Record the batch best hit on the device (sw_batch_best reads it after best_ev).
-static sw_status track_best_device(sw_bank* b, const int32_t* d_scores, const uint64_t* d_ids,
-                                   size_t n, hipStream_t st) {
+sw_status track_best_device(sw_bank* b, const int32_t* d_scores, const uint64_t* d_ids, size_t n,
+                            hipStream_t st) {
   if (n > 0xFFFFFFFFull) return SW_OK;  // the key holds a 32-bit index: not tracked
   HIPOK(b, b->best_key.reserve(1));
   HIPOK(b, b->best_dev.reserve(3));
@@ -349,9 +349,9 @@ static sw_status track_best_device(sw_bank* b, const int32_t* d_scores, const ui
 // once); row-LUT tables only, exact 16-bit arithmetic.  Otherwise (profiles, the column-0 rule,
 // optimistic f16, int32 re-scores, a wave-kernel shape; SWBANK_MQ=0) the queries run one after
 // the other through launch().
-static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
-                            const uint32_t* d_lens, size_t n, uint32_t min_len, uint32_t max_len,
-                            int32_t* d_scores, hipStream_t st) {
+sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
+                     const uint32_t* d_lens, size_t n, uint32_t min_len, uint32_t max_len,
+                     int32_t* d_scores, hipStream_t st, size_t sstride) {
   const size_t nq = b->qset.size();
   const uint64_t smax = (uint64_t)std::max(0, b->smax);
   const uint64_t top = std::min<uint64_t>(b->query.size(), max_len) * smax + smax;
@@ -372,7 +372,7 @@ static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_
       b->dirty = true;
       rs = prepare(b);
       if (rs == SW_OK)
-        rs = launch(b, d_res, d_offs, d_lens, n, max_len, d_scores + i * n, st, SWK_PACK_BYTES,
+        rs = launch(b, d_res, d_offs, d_lens, n, max_len, d_scores + i * sstride, st, SWK_PACK_BYTES,
                     nullptr, nullptr, true, true, nullptr, nullptr, 0, 0, min_len);
     }
     b->query = longest;
@@ -453,7 +453,7 @@ static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_
                                   eout, ecols, sg > 0 ? 1 : 0, (int)SWK_PACK_BYTES,
                                   perm ? perm + p0 : nullptr, perm_n, (uint32_t)p0, ident, 1,
                                   b->mq_pS1, b->mq_pS2, 0, 0, (uint32_t)nq,
-                                  (uint32_t)b->mq_pair_words, n, st));
+                                  (uint32_t)b->mq_pair_words, sstride, st));
         continue;
       }
       HIPOK(b, swk_launch_score(b->R, b->RB, 0, 0, gotoh ? 1 : 0, use_f16 ? 1 : 0, d_res, offs,
@@ -461,7 +461,7 @@ static sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_
                                 b->S, b->O, b->E, 0, b->pad, b->segs[sg].W, scores, ein, eout,
                                 ecols, sg > 0 ? 1 : 0, (int)SWK_PACK_BYTES,
                                 perm ? perm + p0 : nullptr, perm_n, (uint32_t)p0, ident, 0, 0, 0,
-                                0, 0, (uint32_t)nq, (uint32_t)b->mq_words, n, st));
+                                0, 0, (uint32_t)nq, (uint32_t)b->mq_words, sstride, st));
     }
   }
   HIPOK(b, hipEventRecord(b->ev_used, st));
@@ -487,18 +487,22 @@ extern "C" sw_status sw_score_batch_device_range(sw_bank* b, const uint8_t* d_re
                                                  int32_t* d_scores, void* stream) {
   if (!b) return SW_ERR_ARG;
   if (min_len > max_len) return fail(b, SW_ERR_ARG, "min_len %u > max_len %u", min_len, max_len);
-  if (b->is_multi())
-    return fail(b, SW_ERR_UNSUPPORTED, "device buffers need a single-device bank");
   b->best_kind = 0;
+  b->best_root = false;
   if (n == 0) return SW_OK;
   if (!d_res || !d_offs || !d_lens || !d_scores) return fail(b, SW_ERR_ARG, "null device buffer");
+  if (b->is_multi()) {
+    if (b->qset.size() > 1 && d_ids) return fail(b, SW_ERR_UNSUPPORTED, "best hit over a query set");
+    return multi_device(b, d_res, d_offs, d_lens, d_ids, n, min_len, max_len, d_scores,
+                        reinterpret_cast<hipStream_t>(stream), false);
+  }
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
   HIPOK(b, hipSetDevice(b->device));
   hipStream_t hs = stream ? reinterpret_cast<hipStream_t>(stream) : b->stream;
   if (b->qset.size() > 1) {  // a query set: nq x n scores; the best hit is not tracked
     if (d_ids) return fail(b, SW_ERR_UNSUPPORTED, "best hit over a query set");
-    return launch_set(b, d_res, d_offs, d_lens, n, min_len, max_len, d_scores, hs);
+    return launch_set(b, d_res, d_offs, d_lens, n, min_len, max_len, d_scores, hs, n);
   }
   if ((st = launch(b, d_res, d_offs, d_lens, n, max_len, d_scores, hs, SWK_PACK_BYTES, nullptr,
                    nullptr, true, true, nullptr, nullptr, 0, 0, min_len)) != SW_OK)
@@ -509,6 +513,7 @@ extern "C" sw_status sw_score_batch_device_range(sw_bank* b, const uint8_t* d_re
 extern "C" sw_status sw_batch_best(sw_bank* b, uint64_t* best_id, int32_t* best_score,
                                    uint64_t* best_index) {
   if (!b) return SW_ERR_ARG;
+  if (b->is_multi() && b->best_root) return sw_batch_best(b->kids[0], best_id, best_score, best_index);
   if (b->best_kind == 2) {
     uint64_t h[3];
     HIPOK(b, hipSetDevice(b->device));

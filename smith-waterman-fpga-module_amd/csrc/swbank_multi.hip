@@ -197,6 +197,7 @@ static void host_best(sw_bank* b, const int32_t* scores, size_t n) {
   b->best_id = bi;
   b->best_score = scores[bi];
   b->best_kind = 1;
+  b->best_root = false;
 }
 
 sw_status multi_batch(sw_bank* b, const uint8_t* residues, size_t nres,
@@ -261,3 +262,89 @@ sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_t* scor
   return SW_OK;
 }
 
+// Device buffers on a multi-device bank (the caller's buffers live on the root device,
+// devices[0]; ≙ the ScoreBank's MODULES all reading the one target stream, ScoreBank_v2.v:76-148):
+// device d scores the contiguous range [n d / D, n (d + 1) / D) straight from the root's buffers
+// (peer access over xGMI) and writes its scores into the root's d_scores, so nothing is staged
+// or gathered.  Asynchronous: every device's work waits for the caller's stream (an event) and
+// the caller's stream waits for every device's (one event each).  A query set is scored by every
+// device against its range (rows n apart in d_scores, as on one device).  With d_ids the batch
+// best hit is tracked on the root after all ranges (sw_batch_best).
+sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
+                       const uint32_t* d_lens, const uint64_t* d_ids, size_t n, uint32_t min_len,
+                       uint32_t max_len, int32_t* d_scores, hipStream_t hs, bool records) {
+  const size_t D = b->kids.size();
+  sw_bank* root = b->kids[0];
+  const bool set = b->qset.size() > 1;
+  if (!b->peer_ready) {
+    for (sw_bank* k : b->kids) {
+      if (k->device == root->device) continue;
+      int can = 0;
+      HIPOK(b, hipDeviceCanAccessPeer(&can, k->device, root->device));
+      if (!can)
+        return fail(b, SW_ERR_UNSUPPORTED, "device %d cannot access device %d's memory (peer)",
+                    k->device, root->device);
+      HIPOK(b, hipSetDevice(k->device));
+      const hipError_t e = hipDeviceEnablePeerAccess(root->device, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+        return fail(b, SW_ERR_HIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", k->device,
+                    root->device, hipGetErrorString(e));
+      (void)hipGetLastError();
+    }
+    b->peer_ready = true;
+  }
+  HIPOK(b, hipSetDevice(root->device));
+  if (!hs) hs = root->stream;
+  if (!b->ev_join) HIPOK(b, hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
+  HIPOK(b, hipEventRecord(b->ev_join, hs));  // the caller's inputs are ready
+  sw_status st = SW_OK;
+  size_t launched = 0;
+  for (size_t d = 0; d < D && st == SW_OK; ++d) {
+    sw_bank* k = b->kids[d];
+    const size_t lo = n * d / D, cnt = n * (d + 1) / D - lo;
+    if (!cnt) continue;
+    if ((st = prepare(k)) != SW_OK) break;
+    if (hipSetDevice(k->device) != hipSuccess) {
+      st = fail(k, SW_ERR_HIP, "hipSetDevice(%d)", k->device);
+      break;
+    }
+    if (!k->ev_join && hipEventCreateWithFlags(&k->ev_join, hipEventDisableTiming) != hipSuccess) {
+      st = fail(k, SW_ERR_HIP, "event");
+      break;
+    }
+    // device 0 runs on the caller's stream itself; the others on their own, behind it
+    hipStream_t ks = d == 0 ? hs : k->stream;
+    if (d > 0 && hipStreamWaitEvent(ks, b->ev_join, 0) != hipSuccess) {
+      st = fail(k, SW_ERR_HIP, "stream wait");
+      break;
+    }
+    if (records)
+      st = launch(k, d_res + lo * SWB_RECORD, nullptr, nullptr, cnt, SWB_RECORD_MAX,
+                  d_scores + lo, ks, SWK_PACK_RECORDS);
+    else if (set)
+      st = launch_set(k, d_res, d_offs + lo, d_lens + lo, cnt, min_len, max_len, d_scores + lo,
+                      ks, n);
+    else
+      st = launch(k, d_res, d_offs + lo, d_lens + lo, cnt, max_len, d_scores + lo, ks,
+                  SWK_PACK_BYTES, nullptr, nullptr, true, true, nullptr, nullptr, 0, 0, min_len);
+    // (recorded even after a failed launch: the caller's stream must not run ahead of what
+    // was enqueued)
+    if (d > 0 && hipEventRecord(k->ev_join, ks) == hipSuccess) launched |= (size_t)1 << d;
+  }
+  (void)hipSetDevice(root->device);
+  for (size_t d = 1; d < D; ++d)
+    if (launched >> d & 1) HIPOK(b, hipStreamWaitEvent(hs, b->kids[d]->ev_join, 0));
+  if (st != SW_OK) {
+    for (sw_bank* k : b->kids)
+      if (k->err[0]) return fail(b, st, "device %d: %s", k->device, k->err);
+    return st;
+  }
+  snprintf(b->last_kernel, sizeof(b->last_kernel), "multi[%zu] device ranges: %s", D,
+           root->last_kernel);
+  if (d_ids && !records) {
+    if ((st = track_best_device(root, d_scores, d_ids, n, hs)) != SW_OK)
+      return fail(b, st, "device %d: %s", root->device, root->err);
+    b->best_root = true;
+  }
+  return SW_OK;
+}

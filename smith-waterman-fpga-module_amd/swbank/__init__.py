@@ -43,7 +43,7 @@ EXPORTS = (
     "sw_best_hit_device", "sw_batch_best", "sw_bank_devices", "sw_load_queries",
     "sw_query_count", "sw_score_batch_device_range", "sw_bank_counters",
 )
-ABI_VERSION = 3
+ABI_VERSION = 4
 COUNTERS = ("stream_calls", "stream_reruns", "stream_declined", "chunked_calls", "device_sorts",
             "gather_timeouts", "mixed_chunks", "mixed_runs")
 MAX_DEVICES = 16
@@ -102,7 +102,7 @@ def lib() -> ctypes.CDLL:
         "sw_score_batch": (i32, [P, P, sz, P, P, P, sz, P]),
         "sw_score_batch_device": (i32, [P, P, P, P, P, sz, u32, P, P]),
         "sw_score_batch_device_range": (i32, [P, P, P, P, P, sz, u32, u32, P, P]),
-        "sw_bank_counters": (i32, [P, P]),
+        "sw_bank_counters": (i32, [P, P, sz]),
         "sw_batch_best": (i32, [P, P, P, P]),
         "sw_bank_devices": (i32, [P, P, i32]),
         "sw_best_hit": (i32, [P, P, P, sz, P, P]),
@@ -375,7 +375,7 @@ class ScoreBank:
     def counters(self) -> dict:
         """sw_bank_counters: feeder / fallback counts since the bank was created."""
         c = (ctypes.c_uint64 * len(COUNTERS))()
-        self._check(lib().sw_bank_counters(self._h, ctypes.byref(c)))
+        self._check(lib().sw_bank_counters(self._h, ctypes.byref(c), ctypes.sizeof(c)))
         return dict(zip(COUNTERS, (int(x) for x in c)))
 
     # CAPI record path (sequence_t arrays, 2-bit codes)

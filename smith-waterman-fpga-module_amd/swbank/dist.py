@@ -87,9 +87,11 @@ class StepGather:
     ``dist.gather(..., async_op=True)`` of it; the gather of step i-1 may still be reading the
     other buffer, and a buffer is handed out again only after the gather that read it has
     completed (``work.wait()``, which on RCCL orders the compute stream after the collective).
-    ``stage_cpu``: gather a host copy (gloo cannot gather device tensors); the copy is kept
-    until its gather completes.  On rank ``dst``, ``gathered`` holds every rank's vector of the
-    last completed step after ``drain()``."""
+    Each buffer has its own gather list: RCCL runs the two gathers in order on one stream, but
+    gloo completes async work on several threads in any order, so one shared list could end up
+    holding step i-1's vectors for some ranks.  ``stage_cpu``: gather a host copy (gloo cannot
+    gather device tensors); the copy is kept until its gather completes.  On rank ``dst``,
+    ``gathered`` is every rank's vector of the last submitted step, valid after ``drain()``."""
 
     def __init__(self, like, dst: int = 0, group=None, stage_cpu: bool = False):
         import torch
@@ -100,8 +102,8 @@ class StepGather:
         self.group, self.dst, self.stage_cpu = group, dst, stage_cpu
         self.bufs = [like, torch.empty_like(like)]
         gdev = torch.device("cpu") if stage_cpu else like.device
-        self.gathered = ([torch.empty_like(like, device=gdev) for _ in range(self.world)]
-                         if self.world > 1 and self.rank == dst else None)
+        self.lists = ([[torch.empty_like(like, device=gdev) for _ in range(self.world)]
+                       for _ in range(2)] if self.world > 1 and self.rank == dst else None)
         self.pending = [None, None]  # (work, staged tensor) per buffer
         self.steps = 0
 
@@ -119,8 +121,8 @@ class StepGather:
         b = self.steps % 2
         if self.world > 1:
             t = self.bufs[b].cpu() if self.stage_cpu else self.bufs[b]
-            work = dist.gather(t, gather_list=self.gathered, dst=self.dst, group=self.group,
-                               async_op=True)
+            work = dist.gather(t, gather_list=self.lists[b] if self.lists else None,
+                               dst=self.dst, group=self.group, async_op=True)
             self.pending[b] = (work, t)
         self.steps += 1
 
@@ -129,6 +131,14 @@ class StepGather:
             if self.pending[b] is not None:
                 self.pending[b][0].wait()
                 self.pending[b] = None
+
+    @property
+    def gathered(self):
+        """Rank dst: the last submitted step's vectors of every rank (None elsewhere, or before
+        the first step)."""
+        if self.lists is None or self.steps == 0:
+            return None
+        return self.lists[(self.steps - 1) % 2]
 
     def last(self):
         """The buffer of the last submitted step."""

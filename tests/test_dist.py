@@ -95,7 +95,7 @@ def _stepgather_worker(rank, world, port, ret):
         bank = _OracleBank(q)
         last = None
         seen_bufs = set()
-        for step in range(5):
+        for step in range(7):
             seqs = [rng.integers(0, 4, int(rng.integers(1, 120)), dtype=np.uint8) for _ in range(n)]
             res, offs, lens = O.pack_residues(seqs)
             buf = sg.buffer()
@@ -109,7 +109,10 @@ def _stepgather_worker(rank, world, port, ret):
         allv = [torch.empty_like(last) for _ in range(world)] if rank == 0 else None
         dist.gather(last, gather_list=allv, dst=0)
         if rank == 0:
-            ret.put(all(torch.equal(g, v) for g, v in zip(sg.gathered, allv)))
+            # the last step's vectors (every step scores a different batch, so a list holding
+            # step 5's vector for some rank would differ)
+            ret.put(all(torch.equal(g, v) for g, v in zip(sg.gathered, allv))
+                    and sg.lists[0] is not sg.lists[1])
         else:
             ret.put(sg.gathered is None)
     finally:

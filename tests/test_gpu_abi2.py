@@ -290,12 +290,63 @@ def test_multi_device_bank_equals_single(devices, gather, monkeypatch):
         # records through the same bank
         short = [s[:232] for s in seqs]
         r_multi = multi.score_records(S.make_records(short))
-        with pytest.raises(S.SwbankError) as e:  # device buffers need a single-device bank
-            multi.score_batch_device(0, 0, 0, 1, 1, 0)
-        assert e.value.status == S.ERR_UNSUPPORTED
     res2, offs2, lens2 = O.pack_residues(short)
     assert (r_multi == O.score_batch(q, res2, offs2, lens2, O.dna_matrix(), -12, -4)).all()
     assert (want == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0], [0]])
+def test_multi_device_bank_device_api(devices, poisoned_buffers):
+    """ABI 4: a multi-device bank takes device buffers (on the root device): every device scores
+    a contiguous range straight from the caller's buffers and writes into the caller's score
+    buffer, asynchronous on the caller's stream.  Bit-exact against a single bank for a ragged
+    batch (each device sorts its own range), with the best hit, for a query set (every query
+    broadcast to every device, ScoreBank_v2.v:101-102), and for device records."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    q, seqs = _ragged_batch(40 + len(devices), 6000)
+    res, offs, lens = O.pack_residues(seqs)
+    n = len(seqs)
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    d_ids = torch.from_numpy((np.arange(n, dtype=np.uint64) + 7).view(np.int64)).to(dev)
+    qs = [q, q[:90].copy(), _codes(np.random.default_rng(9), 300)]
+    short = [t[:232] for t in seqs]
+    d_rec = torch.from_numpy(S.make_records(short).reshape(-1)).to(dev)
+    L = int(lens.max())
+
+    def run(bank):
+        st = torch.cuda.Stream()
+        one = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,
+                                one.data_ptr(), st.cuda_stream, d_ids=d_ids.data_ptr())
+        best = bank.best()
+        rec = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        bank.score_records_device(d_rec.data_ptr(), n, rec.data_ptr(), st.cuda_stream)
+        bank.load_queries(qs)
+        assert bank.query_count() == len(qs)
+        sets = torch.full((len(qs), n), -1, dtype=torch.int32, device=dev)
+        bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,
+                                sets.data_ptr(), st.cuda_stream, min_len=int(lens.min()))
+        st.synchronize()
+        return one.cpu().numpy(), best, rec.cpu().numpy(), sets.cpu().numpy()
+
+    with S.ScoreBank() as single:
+        want = run(single)
+    with S.ScoreBank(devices=devices) as multi:
+        got = run(multi)
+        assert multi.last_kernel().startswith(f"multi[{len(devices)}] device ranges"), \
+            multi.last_kernel()
+    assert (got[0] == want[0]).all() and got[1] == want[1]
+    assert (got[2] == want[2]).all() and (got[3] == want[3]).all()
+    assert (want[0] == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
+    res2, offs2, lens2 = O.pack_residues(short)
+    assert (want[2] == O.score_batch(q, res2, offs2, lens2, O.dna_matrix(), -12, -4)).all()
+    for i, qq in enumerate(qs):
+        assert (want[3][i] == O.score_batch(qq, res, offs, lens, O.dna_matrix(), -12, -4)).all()
 
 
 def test_multi_device_bank_bad_input_leaves_bank_usable(monkeypatch):

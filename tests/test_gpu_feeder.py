@@ -102,6 +102,29 @@ def test_feeder_bad_code_in_late_chunk(monkeypatch):
         assert np.array_equal(got, _device_scores(bank, res, offs, lens))
 
 
+@pytest.mark.parametrize("point", [3, 5])
+def test_feeder_hip_failure_mid_call(monkeypatch, point):
+    """a HIP failure reported while chunk jobs are still queued on the launch thread
+    (SWBANK_FEED_FAULT=k, a test hook: sync point k fails) returns SW_ERR_HIP after draining
+    the launch thread and the streams, and the bank scores the next batch exactly"""
+    monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
+    rng = np.random.default_rng(14)
+    res, offs, lens = _ragged(rng, 60000, 40, 180)  # ~6.6 MB of codes: 7 chunks
+    q = rng.integers(0, 4, 64, dtype=np.uint8)
+    k = point
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        want = _device_scores(bank, res, offs, lens)
+        monkeypatch.setenv("SWBANK_FEED_FAULT", str(k))
+        with pytest.raises(S.SwbankError) as ei:
+            bank.score_batch(res, offs, lens)
+        assert ei.value.status == S.ERR_HIP, str(ei.value)
+        monkeypatch.delenv("SWBANK_FEED_FAULT")
+        for _ in range(2):
+            assert np.array_equal(bank.score_batch(res, offs, lens), want)
+
+
 def test_feeder_records_many_chunks(monkeypatch):
     monkeypatch.setenv("SWBANK_CHUNK_MB", "1")
     rng = np.random.default_rng(14)
