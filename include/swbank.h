@@ -227,7 +227,8 @@ sw_status sw_bank_timing(sw_bank *bank, uint64_t *launches, double *pack_ms, dou
  * declined for the memory cap (SWBANK_STREAM_MB) or a failed allocation, chunked host calls,
  * device-side length sorts, multi-device gathers abandoned after their time limit, chunks
  * of chunked calls sent as mixed 2-bit / 4-bit codes (ragged DNA), and the pool parts of those
- * chunks packed as one run (targets back to back in the caller's residues). */
+ * chunks packed as one run (targets back to back in the caller's residues), device calls
+ * with balanced chunk ranges. */
 /* out_size = sizeof(sw_counters) as the caller compiled it: the library writes that many bytes
  * (its counters first, zeros past them), so a struct that grows in a later ABI never overflows
  * an older caller's buffer. */
@@ -240,6 +241,10 @@ typedef struct sw_counters {
   uint64_t gather_timeouts;
   uint64_t mixed_chunks;
   uint64_t mixed_runs;
+  /* ABI 4: device calls run with balanced chunk ranges (tiles handed between workgroups),
+   * and hand-off waits that ran out (0 unless a workgroup never started) */
+  uint64_t balanced_calls;
+  uint64_t balanced_timeouts;
 } sw_counters;
 sw_status sw_bank_counters(const sw_bank *bank, sw_counters *out, size_t out_size);
 

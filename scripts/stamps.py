@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Where the headline tile kernel's wave time goes: runs the headline
+batch once through a measurement build of the library (scripts/build_variant.sh stamps
+"-DSWK_STAMPS=1"; selected with SWBANK_LIB) that records per wave, with s_memtime, its entry
+and exit, the cycles of its active phases (column work), of its fill/drain phases (phases
+without a chunk of its own, spent at the barrier) and of the per-phase barrier wait.
+
+Prints one JSON object: the kernel span, and summed over all waves, the shares of
+  ramp     entry after the first wave's entry (dispatch skew)
+  active   phases with a chunk of the wave's own (compute + its waits inside the phase)
+  barrier  waiting at the per-phase barrier after an active phase
+  filldrain phases of the pipeline fill / drain (no chunk of its own, barrier included)
+  exit     from the wave's exit to the last wave's exit (the end-of-kernel quantisation)
+which sum to 100 % of (waves x span); plus the per-SIMD spread of active cycles.
+usage: SWBANK_LIB=.../libswbank_stamps.so python scripts/stamps.py [--targets N] [--bal 0|1]"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "smith-waterman-fpga-module_amd"))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--targets", type=int, default=499 * 2048)
+    ap.add_argument("--L", type=int, default=128)
+    ap.add_argument("--bal", default="1")
+    args = ap.parse_args()
+    os.environ["SWBANK_BAL"] = args.bal
+    import torch
+    import swbank as S
+    from bench import PEN, load_query, make_codes
+
+    L, n = args.L, args.targets
+    q = load_query()
+    res = make_codes(1000, n, L).reshape(-1)
+    dev = torch.device("cuda", 0)
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = (torch.arange(n, dtype=torch.int64, device=dev) * L)
+    d_lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+    d_sc = torch.zeros(n, dtype=torch.int32, device=dev)
+    stamps = torch.zeros(4096 * 16 * 8, dtype=torch.int64, device=dev)
+    lib = S.lib()
+    lib.swk_set_stamps.argtypes = [ctypes.c_void_p]
+    with S.ScoreBank(device=0) as bank:
+        bank.set_penalties(*PEN)
+        bank.load_query(q)
+        call = lambda: bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(),
+                                               d_lens.data_ptr(), n, L, d_sc.data_ptr(),
+                                               min_len=L)
+        call()
+        torch.cuda.synchronize()
+        lib.swk_set_stamps(stamps.data_ptr())
+        call()
+        torch.cuda.synchronize()
+        lib.swk_set_stamps(None)
+        kern = bank.last_kernel()
+    st = stamps.cpu().numpy().reshape(-1, 8).astype(np.int64)
+    st = st[st[:, 1] > 0]
+    t0, t1, act, idle, bar, hw, xcc = (st[:, 0], st[:, 1], st[:, 2], st[:, 3], st[:, 4], st[:, 5],
+                                       st[:, 7])
+    span = int(t1.max() - t0.min())
+    waves = len(st)
+    tot = float(waves) * span
+    ramp = float((t0 - t0.min()).sum())
+    exit_ = float((t1.max() - t1).sum())
+    # the barrier after an active phase vs. the fill/drain phases' whole time
+    inner = (t1 - t0) - act - idle - bar  # loop set-up and the epilogue
+    out = {"kernel": kern, "targets": n, "waves": waves, "span_ticks": span,
+           "share": {"ramp": round(ramp / tot, 4), "active": round(act.sum() / tot, 4),
+                     "barrier": round(bar.sum() / tot, 4),
+                     "filldrain": round(idle.sum() / tot, 4),
+                     "setup": round(inner.sum() / tot, 4),
+                     "exit": round(exit_ / tot, 4)}}
+    # per SIMD: active ticks of its waves (HW_ID: simd 5:4, cu 11:8, sh 12, se 15:13) and XCC
+    key = (xcc * 10000 + ((hw >> 13) & 7) * 1000 + ((hw >> 12) & 1) * 100 + ((hw >> 8) & 15) * 10
+           + ((hw >> 4) & 3))
+    per = {}
+    for k, a in zip(key.tolist(), act.tolist()):
+        per[k] = per.get(k, 0) + a
+    v = np.array(list(per.values()), dtype=np.float64)
+    out["simds_seen"] = len(per)
+    out["simd_active_spread"] = {"min": round(v.min() / span, 4), "median": round(float(np.median(v)) / span, 4),
+                                 "max": round(v.max() / span, 4)}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

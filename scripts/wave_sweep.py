@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Wave-kernel GCUPS vs batch size and block size (tuning aid: occupancy / tail effects).
-usage: python scripts/wave_sweep.py [--qlen 512] [--L 1000] [--ns 8192,12500,...] [--wpb 4,8]"""
+"""Wave-kernel GCUPS vs batch size and split-tail segment count (tuning aid: occupancy / tail
+effects; SWBANK_WAVE_SPLIT_P: 0 = the policy's choice, 2 or 4 forced).
+usage: python scripts/wave_sweep.py [--qlen 512] [--L 1000] [--ns 8192,12500,...] [--split 0,2,4]"""
 import argparse
 import json
 import os
@@ -18,7 +19,7 @@ def main():
     ap.add_argument("--qlen", type=int, default=512)
     ap.add_argument("--L", type=int, default=1000)
     ap.add_argument("--ns", default="6144,8192,10240,12288,12500,14336,16384,24576,25000")
-    ap.add_argument("--wpb", default="4,8")
+    ap.add_argument("--split", default="0,2,4")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--kernel", default="wave")
     args = ap.parse_args()
@@ -44,8 +45,8 @@ def main():
         d_lens = torch.full((n,), L, dtype=torch.int32, device=dev)
         d_sc = torch.zeros(n, dtype=torch.int32, device=dev)
         out = {"qlen": args.qlen, "L": L, "n": n}
-        for w in args.wpb.split(","):
-            os.environ["SWBANK_WAVE_BLOCK"] = w
+        for w in args.split.split(","):
+            os.environ["SWBANK_WAVE_SPLIT_P"] = w
             call = lambda: bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(),
                                                    d_lens.data_ptr(), n, L, d_sc.data_ptr(),
                                                    stream)
@@ -58,7 +59,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.iters
-            out[f"w{w}"] = round(args.qlen * L * n / ms / 1e6, 1)
+            out[f"P{w}"] = round(args.qlen * L * n / ms / 1e6, 1)
         out["kernel"] = bank.last_kernel()
         print(json.dumps(out), flush=True)
 

@@ -59,6 +59,15 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        const uint32_t* ident, int pair, uint32_t pS1,
                                        uint32_t pS2, uint32_t ulen, uint32_t ustride, uint32_t nq,
                                        uint32_t qwords, size_t sstride, hipStream_t st);
+extern "C" unsigned swk_bal_slots(int W, uint32_t PS);
+extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* offs,
+                                          const uint32_t* lens, size_t n, const uint32_t* qtab,
+                                          uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
+                                          uint32_t PS, uint32_t pad, int W, int32_t* scores,
+                                          uint32_t pS1, uint32_t pS2, uint32_t ulen,
+                                          uint32_t ustride, uint32_t K, uint32_t* flag,
+                                          uint32_t* state, uint32_t gen, unsigned grid,
+                                          hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
                                    hipStream_t st);
@@ -72,7 +81,6 @@ extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max
 extern "C" size_t swk_sort_scratch_bytes(void);
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
                                     uint32_t* idx, uint32_t* count, hipStream_t st);
-extern "C" void swk_set_occ_cap(int per_cu);
 extern "C" size_t swk_i32_waves(size_t n, uint32_t scols, size_t budget_bytes);
 extern "C" hipError_t swk_launch_i32(int gotoh, const uint8_t* res, const uint64_t* offs,
                                      const uint32_t* lens, size_t n, int packed,
@@ -192,10 +200,6 @@ struct PinBuf {
   }
 };
 
-inline bool spin_yield() {
-  static const bool y = env_int("SWBANK_SPIN_YIELD", 0) != 0;
-  return y;
-}
 
 // Host worker threads for the host-buffer feeder (gather / scatter of a chunk): run(f) calls
 // f(part) for part = 0..size()-1, part 0 on the calling thread, and returns when all are done.
@@ -235,14 +239,10 @@ class HostPool {
   }
 
  private:
-  // SWBANK_SPIN_YIELD=1: a spinning thread yields its core every 64 polls (meant for the
-  // occasional 8-10 ms calls, a preempted worker or launch thread being one suspect; A/B on the
-  // box did not remove them, so off by default)
-  static void relax(unsigned it) {
+  static void relax(unsigned) {
 #if defined(__SSE2__)
     _mm_pause();
 #endif
-    if ((it & 63) == 0 && spin_yield()) std::this_thread::yield();
   }
   void loop(unsigned i) {
     uint64_t seen = 0;
@@ -299,11 +299,10 @@ class Launcher {
   }
   // spins until the first k posted jobs ran; their status
   sw_status wait(size_t k) {
-    for (unsigned it = 1; done_.load(std::memory_order_acquire) < k; ++it) {
+    while (done_.load(std::memory_order_acquire) < k) {
 #if defined(__SSE2__)
       _mm_pause();
 #endif
-      if ((it & 63) == 0 && spin_yield()) std::this_thread::yield();
     }
     return st_.load(std::memory_order_acquire);
   }
@@ -410,12 +409,14 @@ struct sw_bank {
   uint32_t wPS16 = 0;
   // wave kernel split tail (one segment, K >= 8): [i] = the query as P = 2 << i segments of
   // sK = K/P rows per lane (stab: u16, stab16: f16, sseg_words* apart); sring: 256 columns x
-  // uint2 per segment boundary of every tail pair
-  int sK[2] = {0, 0};
-  size_t sseg_words[2] = {0, 0}, sseg_words16[2] = {0, 0};
-  uint32_t sPS[2] = {0, 0}, sPS16[2] = {0, 0};
-  DevBuf<uint32_t> stab[2], stab16[2];
+  // uint2 per segment boundary of every tail pair (P = 8, the two-pairs kernel's segmented
+  // tail: a whole row of columns per boundary, tprog its progress / best words)
+  int sK[3] = {0, 0, 0};
+  size_t sseg_words[3] = {0, 0, 0}, sseg_words16[3] = {0, 0, 0};
+  uint32_t sPS[3] = {0, 0, 0}, sPS16[3] = {0, 0, 0};
+  DevBuf<uint32_t> stab[3], stab16[3];
   DevBuf<uint2> sring;
+  DevBuf<uint32_t> tprog;
 
   // host-buffer feeder (sw_score_batch / sw_score_records): NSLOT pinned staging slots, chunk
   // i gathered on the host while chunk i-1 crosses PCIe on copy_stream and earlier chunks are
@@ -453,7 +454,7 @@ struct sw_bank {
   PinBuf shscores{hipHostMallocCoherent};  // the streamed kernel writes the scores here
   std::vector<hipEvent_t> sev;
   std::unique_ptr<HostPool> pool;
-  std::unique_ptr<Launcher> launcher;  // the feeder's launch thread (SWBANK_LAUNCHER=0: none)
+  std::unique_ptr<Launcher> launcher;  // the feeder's launch thread
 
   // workspaces
   DevBuf<uint8_t> res;
@@ -484,6 +485,10 @@ struct sw_bank {
   // caller's buffers on the root device through peer access, enabled once (peer_ready);
   // ev_join: a child's work on its stream is done (the caller's stream waits on it);
   // best_root: the last device call's best hit is tracked by kids[0]
+  // balanced chunk ranges (swk_launch_pair_bal): the hand-off states and flags, the launch
+  // generation the flags are compared with
+  DevBuf<uint32_t> bal_state, bal_flag;
+  uint32_t bal_gen = 0;
   bool peer_ready = false;
   hipEvent_t ev_join = nullptr;
   bool best_root = false;

@@ -179,9 +179,12 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->i32scr.release();
   b->dperm.release();
   b->dsort.release();
+  b->bal_state.release();
+  b->bal_flag.release();
   b->wtab.release();
   b->wtab16.release();
-  for (int i = 0; i < 2; ++i) {
+  b->tprog.release();
+  for (int i = 0; i < 3; ++i) {
     b->stab[i].release();
     b->stab16[i].release();
   }
@@ -249,6 +252,16 @@ extern "C" sw_status sw_bank_counters(const sw_bank* b, sw_counters* out, size_t
     c.gather_timeouts += k->ctr.gather_timeouts;
     c.mixed_chunks += k->ctr.mixed_chunks;
     c.mixed_runs += k->ctr.mixed_runs;
+    c.balanced_calls += k->ctr.balanced_calls;
+  }
+  // balanced-range hand-off waits that ran out, counted on the device (a snapshot)
+  for (const sw_bank* k : b->kids.empty() ? std::vector<const sw_bank*>{b}
+                                           : std::vector<const sw_bank*>(b->kids.begin(),
+                                                                         b->kids.end())) {
+    uint32_t t = 0;  // bal_flag[0] (workgroup 0's flag slot, never waited on)
+    if (k->bal_flag.cap && hipSetDevice(k->device) == hipSuccess &&
+        hipMemcpy(&t, k->bal_flag.p, 4, hipMemcpyDeviceToHost) == hipSuccess)
+      c.balanced_timeouts += t;
   }
   // a caller built against an older (shorter) struct gets its prefix, a newer one zeroes past ours
   std::memset(out, 0, out_size);
@@ -625,11 +638,11 @@ sw_status prepare(sw_bank* b) {
   const int wsegs = std::max(1, (qlen + wrows - 1) / wrows);
   const uint32_t wPS = prof ? (uint32_t)wrows : 0, wPS16 = prof ? (uint32_t)wrows * 2 : 0;
   wave_tables(wrows, wsegs, wt, wt16);
-  // split tail of the wave kernel (one segment, K >= 8): the query as P = 2 and 4 segments of
-  // K/P rows per lane, tables concatenated like the segments above
-  std::vector<uint32_t> st[2], st16[2];
-  int sK[2] = {0, 0};
-  for (int i = 0; i < 2; ++i) {
+  // split tail of the wave kernel (one segment, K >= 8): the query as P = 2, 4 and 8 segments
+  // of K/P rows per lane, tables concatenated like the segments above
+  std::vector<uint32_t> st[3], st16[3];
+  int sK[3] = {0, 0, 0};
+  for (int i = 0; i < 3; ++i) {
     sK[i] = (wsegs == 1 && wK >= 8) ? wK / (2 << i) : 0;
     if (sK[i]) wave_tables(64 * sK[i], 2 << i, st[i], st16[i]);
   }
@@ -644,7 +657,8 @@ sw_status prepare(sw_bank* b) {
   HIPOK(b, hipEventSynchronize(b->ev_ready));
   const size_t nbytes =
       (wt16.size() + wt.size() + st16[0].size() + st[0].size() + st16[1].size() +
-       st[1].size() + tab.size() + tab16.size() + tpair.size()) * 4;
+       st[1].size() + st16[2].size() + st[2].size() + tab.size() + tab16.size() + tpair.size()) *
+      4;
   HIPOK(b, b->stage.reserve(nbytes));
   // earlier launches (any stream) must be done reading the tables this upload overwrites
   HIPOK(b, hipStreamWaitEvent(b->stream, b->ev_used, 0));
@@ -665,7 +679,7 @@ sw_status prepare(sw_bank* b) {
   b->wsegs = wsegs;
   b->wseg_words = wt.size() / wsegs;
   b->wseg_words16 = wt16.empty() ? 0 : wt16.size() / wsegs;
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < 3; ++i) {
     if (!st16[i].empty()) HIPOK(b, upload(b->stab16[i], st16[i]));
     HIPOK(b, upload(b->stab[i], st[i]));
     b->sK[i] = sK[i];
@@ -737,12 +751,14 @@ sw_status prepare_multi(sw_bank* b) {
   // letter-pair tables (DNA merged f16 without the column-0 rule), one per (segment, query):
   // 512-row segments (16 waves of 32 rows with 4-column chunks: a 1-kbp query is 2 segments,
   // one bottom-row hand-off through HBM instead of 7 with 128-row segments) unless
-  // SWBANK_MQ_PAIR_ROWS=128 (4 waves, 8-column chunks, 4 workgroups per CU)
+  // SWBANK_MQ_PAIR_ROWS=128 (4 waves, 8-column chunks, 4 workgroups per CU) or 256 (8 waves,
+  // 4-column chunks, 2 workgroups per CU)
   std::vector<uint32_t> tp;
   b->mq_pair_segs = 0;
   if (b->f16 && !b->prof && !b->gotoh() && !b->col0 && A == SW_DNA_ALPHA &&
       env_int("SWBANK_MQ_PAIR", 1) != 0) {
-    const uint32_t NR = env_int("SWBANK_MQ_PAIR_ROWS", 512) == 128 ? 128 : 512;
+    const int want = env_int("SWBANK_MQ_PAIR_ROWS", 512);
+    const uint32_t NR = want == 128 ? 128 : want == 256 ? 256 : 512;
     b->mq_pair_rows = (int)NR;
     pair_strides(NR, b->mq_pS1, b->mq_pS2);
     const int qmax = (int)b->query.size();

@@ -93,20 +93,8 @@ static size_t chunk_target(size_t total) {
 static std::vector<size_t> chunk_bounds(size_t total) {
   std::vector<size_t> bounds;
   const size_t cap = chunk_target(total);
-  const int first_kb = env_int("SWBANK_CHUNK_FIRST_KB", 0);
-  size_t sz = first_kb > 0 ? (size_t)first_kb << 10
-              : env_int("SWBANK_CHUNK_MB", 0) > 0 ? cap : std::max<size_t>(1 << 20, cap / 4);
+  size_t sz = env_int("SWBANK_CHUNK_MB", 0) > 0 ? cap : std::max<size_t>(1 << 20, cap / 4);
   for (size_t at = sz; at < total; at += sz, sz = std::min(cap, sz * 2)) bounds.push_back(at);
-  // SWBANK_CHUNK_TAIL=k: the last chunk cut in halves k + 1 times (k = 1: a half and two
-  // quarters), so the call's final copy, sort and launch (which nothing overlaps) are short
-  const size_t last = bounds.empty() ? 0 : bounds.back();
-  const int tail = env_int("SWBANK_CHUNK_TAIL", 0);
-  for (size_t at = last, rem = total - last, i = 0;
-       tail > 0 && i < (size_t)tail + 1 && rem >= ((size_t)2 << 20); ++i) {
-    at += rem / 2;
-    rem -= rem / 2;
-    bounds.push_back(at);
-  }
   return bounds;
 }
 
@@ -115,8 +103,8 @@ static sw_status feeder_init(sw_bank* b) {
   if (!b->pool) b->pool.reset(new (std::nothrow) HostPool(b->pool_threads ? b->pool_threads
                                                                           : host_threads()));
   if (!b->pool) return fail(b, SW_ERR_NOMEM, "host worker pool");
-  if (!b->launcher && env_int("SWBANK_LAUNCHER", 1) != 0)
-    b->launcher.reset(new (std::nothrow) Launcher(b->device));
+  if (!b->launcher) b->launcher.reset(new (std::nothrow) Launcher(b->device));
+  if (!b->launcher) return fail(b, SW_ERR_NOMEM, "feeder launch thread");
   if (b->copy_stream) return SW_OK;
   HIPOK(b, hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
   HIPOK(b, hipStreamCreateWithFlags(&b->out_stream, hipStreamNonBlocking));
@@ -152,10 +140,9 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   ++b->ctr.chunked_calls;
   size_t slot_bytes = 0;
   for (const Chunk& c : chunks) slot_bytes = std::max(slot_bytes, c.bytes);
-  // device slots: NDSLOT while they take at most 1 GiB (SWBANK_DSLOTS overrides), else NSLOT
-  const int nds = std::max(1, std::min(sw_bank::NDSLOT,
-      env_int("SWBANK_DSLOTS", slot_bytes * sw_bank::NDSLOT <= ((size_t)1 << 30)
-                                   ? sw_bank::NDSLOT : sw_bank::NSLOT)));
+  // device slots: NDSLOT while they take at most 1 GiB, else NSLOT
+  const int nds = slot_bytes * sw_bank::NDSLOT <= ((size_t)1 << 30) ? sw_bank::NDSLOT
+                                                                    : sw_bank::NSLOT;
   b->feed_dslots = nds;
   for (int i = 0; i < std::min<int>(sw_bank::NSLOT, (int)chunks.size()); ++i)
     HIPOK(b, b->hslot[i].reserve(slot_bytes));
@@ -170,14 +157,9 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
       b->out_ev.push_back(e);
     }
   }
-  // overlapped chunk launches may run two at a time; SWBANK_CHUNK_OCC=m caps each at m
-  // workgroups per CU so the two streams share the chip (a per-thread setting: set by the
-  // thread that launches)
-  // (round 3: no cap by default.  With the launch thread and 6 device slots the chunk kernels
-  // are paced by the gather and mostly run one at a time, and a half-chip kernel running alone
-  // took ~220 us per 1/8 chunk against ~175 at full occupancy; SWBANK_CHUNK_OCC=2 restores the
-  // cap)
-  const int occ = overlap ? std::max(0, env_int("SWBANK_CHUNK_OCC", 0)) : 0;
+  // (overlapped chunk launches run at full occupancy: with the launch thread and 6 device slots
+  // they are paced by the gather and mostly run one at a time, and a half-chip kernel running
+  // alone took ~220 us per 1/8 chunk against ~175 at full occupancy)
   Launcher* lz = b->launcher.get();
   if (lz) lz->reset();
   const auto fail_sync = [&](sw_status s) {
@@ -210,10 +192,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     HIPOK(b, hipEventRecord(b->h2d_done[s], b->copy_stream));
     hipStream_t ks = overlap && (i & 1) ? b->stream2 : b->stream;
     HIPOK(b, hipStreamWaitEvent(ks, b->h2d_done[s], 0));
-    // the last chunk has no later launch to share the chip with: the whole GPU
-    swk_set_occ_cap(i + 1 == chunks.size() ? 0 : occ);
     const sw_status sst = score(b->dslot[d].p, c, b->scores.p + c.c0, ks);
-    swk_set_occ_cap(0);
     if (sst != SW_OK) return sst;
     if (tr) tr->mark("launched");
     HIPOK(b, hipEventRecord(b->kern_done[d], ks));
@@ -309,14 +288,13 @@ static SlotTail slot_tail(size_t tail_at, size_t cnt) {
 
 // True when launches for targets of at most max_len use no bank scratch (one query segment,
 // no optimistic f16 re-score list, no int32 re-score), so host-feeder chunks may run on two
-// streams (SWBANK_OVERLAP=0 disables).  Mirrors launch()'s choices.
+// streams.  Mirrors launch()'s choices.
 bool scratch_free(const sw_bank* b, uint32_t max_len) {
-  if (env_int("SWBANK_OVERLAP", 1) == 0) return false;
   const uint64_t s = (uint64_t)std::max(0, b->smax);
   const uint64_t top = std::min<uint64_t>(b->query.size(), max_len) * s + s;
   const bool need32 = top > 65535u || env_int("SWBANK_I32", 0) != 0;
   const bool f16_ok = b->f16 && b->f16_neg >= -2048 && env_int("SWBANK_F16", 1) != 0;
-  const bool opt16 = f16_ok && top > 2048u && env_int("SWBANK_F16_OPT", 1) != 0;
+  const bool opt16 = f16_ok && top > 2048u;
   return b->segs.size() == 1 && b->wsegs == 1 && !need32 && !opt16;
 }
 
@@ -663,7 +641,8 @@ sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     }
     uint32_t mode = SWK_PACK_BYTES;
     const uint64_t ctop = std::min<uint64_t>(b->query.size(), chunk_max[gi]) * smax0 + smax0;
-    const bool cf16 = f16_ok && (ctop <= 2048u || env_int("SWBANK_F16_OPT", 1) != 0);
+    const bool cf16 = f16_ok;  // (exact, or optimistic past 2048)
+    (void)ctop;
     const size_t ca32 = align16(cnt * 8);
     if (mixed_ok && !uni && (host_dsort || cnt <= SWB_TILE) &&
         ca32 + align16(psz[T] + part4[T] + 3 * cnt + 32) + align16(cnt * 4 + 8) <= c.bytes &&

@@ -41,6 +41,11 @@ typedef struct SwkWaveSplit {
   const unsigned* fb_qtab;
   unsigned words, fb_words, PS, fb_PS;
   void* ring;
+  /* P = 8 (two-pairs kernel only): the segmented tail, one 64-row segment per wave in blocks
+   * after the main ones; ring = pairs x 7 x cols columns of 8 B, prog = pairs x 8 x 3 + 1
+   * words zeroed before the launch (progress, bests, poll time-outs) */
+  unsigned cols;
+  unsigned* prog;
 } SwkWaveSplit;
 
 /* One chunk of a streamed host batch (uploaded before the launch): its first tile and the

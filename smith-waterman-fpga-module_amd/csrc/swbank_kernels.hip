@@ -35,8 +35,15 @@
 
 #include "swbank_internal.h"
 
+#ifndef SWK_STAMPS
+#define SWK_STAMPS 0  // measurement builds: per-wave phase timing of the tile kernel (swk_set_stamps)
+#endif
+
 namespace swk {
 
+#if SWK_STAMPS
+static uint64_t* g_stamps_host = nullptr;  // the buffer launch_score hands the tile kernel
+#endif
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
@@ -697,8 +704,26 @@ struct ScoreArgs {
   uint32_t* dflag;
   uint32_t* tctr;
   uint32_t nsc;
+  // balanced chunk ranges (BAL variants, uniform batches: every tile bal_K chunks): workgroup g
+  // scores chunks [A_g, A_g+1) of the tile-major chunk sequence, A_g = g x tiles x bal_K / G, so
+  // every resident slot gets the same work whatever tiles / slots is.  A tile cut by a range
+  // boundary is scored in two visits: workgroup g - 1 scores its first chunks first (its "head")
+  // and hands each wave's column state over through bal_state (sc1 stores, then the flag
+  // bal_flag[g][wave] = bal_gen); workgroup g scores the rest last (its "tail").
+  uint32_t* bal_flag;
+  uint32_t* bal_state;
+  uint32_t bal_K, bal_gen;
+  // two-pairs wave kernel, segmented tail (tail_pairs > 0; split_P = 8, the split_* tables and
+  // split_ring): the last tail_pairs pairs run as split_P row segments of 64 rows, one wave
+  // each, in 4-wave blocks after the main blocks; segment s hands its bottom row to s + 1
+  // through split_ring (a whole row of columns per boundary) and tail_prog (64-column blocks
+  // done, zeroed by the host before the launch) instead of a barrier, so a pair's segments sit
+  // on different CUs.  tail_prog: [pair][segment] progress | [pair][segment] best (uint2) |
+  // poll time-outs.
+  uint32_t* tail_prog;
+  uint32_t tail_pairs, tail_cols;
 };
-static_assert(sizeof(ScoreArgs) == 296, "ScoreArgs layout (kernel argument block) changed");
+static_assert(sizeof(ScoreArgs) == 336, "ScoreArgs layout (kernel argument block) changed");
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) void* glob_void_ptr;
@@ -787,8 +812,9 @@ __device__ __forceinline__ uint32_t stream_mode(const uint32_t* hflag, uint32_t*
 // C: columns per chunk (one barrier per chunk); 4 for the 16-wave query-set pair kernel, whose
 // hand-off ring would not fit LDS beside a 512-row pair table at 8.
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
-          bool MQ = false, bool STREAM = false, int C = 8>
+          bool MQ = false, bool STREAM = false, int C = 8, bool BAL = false>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
+  static_assert(!BAL || (!MQ && !STREAM && !COL0), "balanced ranges: one query, resident batch");
   static_assert(!MQ || !PROF, "several queries: row-LUT or pair-table variants");
   static_assert(!STREAM || (!MQ && !PROF), "streamed batches: single-query LUT / pair variants");
   static_assert(C == 8 || (C == 4 && PAIR && !STREAM), "4-column chunks: pair tables only");
@@ -825,7 +851,35 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   // STREAM: tiles taken dynamically, so the total is open until wave 0 finds no tile left
   // (it then stores it in sq[W]; every wave reads sq[W] at each phase)
   int* sq = reinterpret_cast<int*>(prof);  // STREAM: next tile of ordinal k at [k % W] | total
-  if constexpr (STREAM) {
+  // BAL: this workgroup's chunk range [A0, A1) as visits: the head (tile be, chunks [0, bf)),
+  // the whole tiles [bfirst, be), the tail (tile bs, chunks [bo, K)); a range holds >= 2 tiles
+  // (the host checks), so the head and the tail are different tiles.  Visit v (= the tile
+  // ordinal k) -> (tile, first chunk, end chunk), recomputed from blockIdx at each visit's end
+  // (nothing of the plan stays live across the column loop)
+  const auto bal_visit = [&](int v, int& t, int& c0, int& c1) {
+    const int bK = (int)a.bal_K;
+    const uint64_t at = (uint64_t)ntiles * (uint64_t)bK;
+    const uint64_t A0 = at * blockIdx.x / G, A1 = at * (blockIdx.x + 1) / G;
+    const int bs = (int)(A0 / bK), bo = (int)(A0 % bK), be = (int)(A1 / bK), bf = (int)(A1 % bK);
+    const int bfirst = bo ? bs + 1 : bs;
+    const int hh = bf > 0 ? 1 : 0;
+    if (v < hh) {
+      t = be, c0 = 0, c1 = bf;
+    } else if (v - hh < be - bfirst) {
+      t = bfirst + v - hh, c0 = 0, c1 = bK;
+    } else if (v - hh == be - bfirst && bo > 0) {
+      t = bs, c0 = bo, c1 = bK;
+    } else {
+      t = nunits, c0 = 0, c1 = 1;  // no more visits
+    }
+    t = __builtin_amdgcn_readfirstlane(t);
+    c0 = __builtin_amdgcn_readfirstlane(c0);
+    c1 = __builtin_amdgcn_readfirstlane(c1);
+  };
+  if constexpr (BAL) {
+    const uint64_t at = (uint64_t)ntiles * (uint64_t)a.bal_K;
+    total = (int)(at * (blockIdx.x + 1) / G - at * blockIdx.x / G);
+  } else if constexpr (STREAM) {
     total = (int)blockIdx.x < ntiles ? (1 << 30) : 0;
   } else {
     for (int u = blockIdx.x; u < nunits; u += G)  // (the unit's tile: see the MQ order below)
@@ -896,6 +950,11 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   // a workgroup keeps one query and loads its LDS table once
   int unit = blockIdx.x, q = 0;
   int tile = unit;
+  int vc0 = 0, vend = 0;  // BAL: the first visit's first and end chunk
+  if constexpr (BAL) {
+    bal_visit(0, tile, vc0, vend);
+    unit = tile;
+  }
   if constexpr (MQ) {
     if (unit < nunits) {
       q = PAIR ? unit % (int)a.nq : unit / ntiles;
@@ -914,6 +973,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   int nch, nfull;
   tile_chunks<C>(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
               nfull);
+  if constexpr (BAL) nch = vend;  // BAL: nch = the visit's end chunk (a head's: < bal_K)
   const uint32_t S = a.S;
 
   for (int i = threadIdx.x; i < W * SWB_TILE; i += blockDim.x) bestsh[i] = 0;
@@ -965,7 +1025,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   u16x2 best = {0, 0};
   u16x2 prevUpH = H0;  // H(row above, column -1)
   uint2 rlo, rhi;      // raw codes of the next chunk (prefetched one phase ahead)
-  load_raw<C, !MQ>(cur, 0, nfull > 0, a.pad, packed, rlo, rhi);
+  load_raw<C, !MQ>(cur, vc0, vc0 < nfull, a.pad, packed, rlo, rhi);
   if (STREAM && threadIdx.x == 0) sq[W] = total;
   __syncthreads();
 
@@ -1013,9 +1073,68 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   const int istride = (wave > 0 || seg_in) ? 64 : 0, ostride = (wave < W - 1 || seg_out) ? 64 : 0;
   const uint32_t pbase = (uint32_t)wave * R;
   const uint32_t padc = a.pad;
-  int c = 0, k = 0;           // chunk within the current tile, tile ordinal in this workgroup
+  // BAL hand-off of one wave's column state {H, T of its R rows, the diagonal H above, best}
+  // at a head's end / a tail's start: word i of lane l at state[((g W + wave) (2R + 2) + i) 64
+  // + l] (coalesced), written and read with sc1 (write-through / L2) accesses and a flag
+  // (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores, vmcnt(0), sc1 flag; sc1 poll,
+  // sc1 loads).  The consumer's tail is its last visit and the producer's head its first, so
+  // the flag is normally long set; the poll is bounded (about 4 s) and counts a time-out in
+  // bal_flag[0] rather than hanging.
+  // (the state addresses go through an opaque copy: loop-invariant, LLVM would otherwise hoist
+  // all 2R + 2 of them out of the phase loop, 2 VGPRs each, and spill)
+  const auto bal_store = [&](int g_to) {
+    uint32_t* sp = a.bal_state + ((size_t)g_to * W + wave) * (2 * R + 2) * 64 + lane;
+    asm volatile("" : "+v"(sp));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      __hip_atomic_store(sp + r * 64, as_u32(Hl[r]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sp + (R + r) * 64, as_u32(Xl[r]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __hip_atomic_store(sp + 2 * R * 64, as_u32(prevUpH), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(sp + (2 * R + 1) * 64, as_u32(best), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_store(a.bal_flag + (size_t)g_to * W + wave, a.bal_gen, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  };
+  const auto bal_load = [&]() {
+    const uint32_t* fl = a.bal_flag + (size_t)blockIdx.x * W + wave;
+    int it = 0;
+    for (; it < (1 << 23); ++it) {
+      if (__builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == a.bal_gen)
+        break;
+      __builtin_amdgcn_s_sleep(8);
+    }
+    if (it == (1 << 23) && lane == 0) atomicAdd(a.bal_flag, 1u);  // (workgroup 0 never waits)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t* sp = a.bal_state + ((size_t)blockIdx.x * W + wave) * (2 * R + 2) * 64 + lane;
+    asm volatile("" : "+v"(sp));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      Hl[r] = as_u16x2(__hip_atomic_load(sp + r * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      Xl[r] = as_u16x2(
+          __hip_atomic_load(sp + (R + r) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    prevUpH = as_u16x2(
+        __hip_atomic_load(sp + 2 * R * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    best = as_u16x2(
+        __hip_atomic_load(sp + (2 * R + 1) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  };
+  (void)bal_store; (void)bal_load;
+  // chunk within the current tile, tile ordinal in this workgroup (BAL: the visit ordinal; a
+  // first visit is a head or a whole tile, never a tail)
+  int c = vc0, k = 0;
   int nch_n = 1, nfull_n = 0;  // the next tile's chunk counts
   uint32_t packed_n = packed;  // STREAM: the next tile's code layout
+#if SWK_STAMPS
+  // (measurement builds only) per wave: kernel entry / exit, cycles in active phases (the
+  // column work), in fill/drain phases (no chunk of its own) and in the per-phase barrier
+  uint64_t st_t0 = __builtin_amdgcn_s_memtime(), st_act = 0, st_idle = 0, st_bar = 0;
+  uint64_t st_p = st_t0;
+#endif
   for (int ph = 0;; ++ph) {
     if constexpr (STREAM) total = __builtin_amdgcn_readfirstlane(sq[W]);
     if (ph >= total + W - 1) break;
@@ -1024,6 +1143,10 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       const uint2 clo = rlo, chi = rhi;
       const bool last = c + 1 == nch;
       int nunit = (MQ ? unit : tile) + G;
+      int nc0 = 0, nvend = 0;  // BAL: the next visit's first and end chunk
+      if constexpr (BAL) {
+        if (last) bal_visit(k + 1, nunit, nc0, nvend);
+      }
       if constexpr (STREAM) {  // wave 0 takes the next tile; the others read it W-1 phases on
         if (last) {
           if (wave == 0) {
@@ -1063,7 +1186,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
                                   a.ustride);
         tile_chunks<C>(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
                     n, nch_n, nfull_n);
-        load_raw<C, !MQ>(cur, 0, nfull_n > 0, a.pad, STREAM ? packed_n : packed, rlo, rhi);
+        load_raw<C, !MQ>(cur, nc0, nc0 < nfull_n, a.pad, STREAM ? packed_n : packed, rlo, rhi);
       }
       const int slot = g & 1;
       // next chunk's boundary row (never past the last unit's edge rows)
@@ -1241,7 +1364,10 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
 #pragma unroll
         for (int jj = 0; jj < C; ++jj) dst[jj * 64] = sink[jj * 64 + lane];
       }
-      if (last) {  // this wave's part of tile k is done
+      if (last) {
+        if (BAL && nch < (int)a.bal_K) {  // BAL: a head visit ends: hand its state over
+          bal_store((int)blockIdx.x + 1);
+        } else {  // this wave's part of tile k is done
         uint32_t* bs = bestsh + (k % W) * SWB_TILE;
         atomicMax(&bs[lane], (uint32_t)best.x);
         atomicMax(&bs[lane + 64], (uint32_t)best.y);
@@ -1271,6 +1397,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           if (tlo < n) qsc[slo] = blo;
           if (thi < n) qsc[shi] = bhi;
         }
+        }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           Hl[r] = H0;
@@ -1297,21 +1424,52 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         nch = nch_n;
         nfull = nfull_n;
         c = 0;
+        if constexpr (BAL) {
+          c = nc0;
+          nch = nvend;
+          if (nc0 > 0) bal_load();  // a tail: the head's state
+        }
         ++k;
       } else {
         ++c;
       }
     }
+#if SWK_STAMPS
+    const bool st_own = g >= 0 && g < total;  // (fill / drain phases: all of it to st_idle)
+    const uint64_t st_b = __builtin_amdgcn_s_memtime();
+    (st_own ? st_act : st_idle) += st_b - st_p;
+#endif
     __syncthreads();
+#if SWK_STAMPS
+    st_p = __builtin_amdgcn_s_memtime();
+    (st_own ? st_bar : st_idle) += st_p - st_b;
+#endif
   }
+#if SWK_STAMPS
+  // (the non-streamed variants never read tctr: measurement builds pass the buffer there)
+  uint64_t* const g_stamps = STREAM ? nullptr : reinterpret_cast<uint64_t*>(a.tctr);
+  if (lane == 0 && g_stamps) {
+    uint64_t* o = g_stamps + ((size_t)blockIdx.x * 16 + wave) * 8;
+    unsigned hw = 0;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    o[0] = st_t0;
+    o[1] = __builtin_amdgcn_s_memtime();
+    o[2] = st_act;
+    o[3] = st_idle;
+    o[4] = st_bar;
+    o[5] = hw;
+    unsigned xcc = 0;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    o[6] = (uint64_t)total;
+    o[7] = (uint64_t)(xcc & 15);
+  }
+#endif
 }
 
 // Workgroups for a persistent launch: as many as fit on the device at once (occupancy x CUs),
-// then evened out so every workgroup gets the same number of tiles (+-1).  SWBANK_GRID=0 gives
-// one workgroup per tile; SWBANK_GRID=m caps the resident workgroups per CU at m (tuning).
-// Per-thread cap on resident workgroups per CU for the next score launches (0 = none): the host
-// feeder's overlapped chunk launches take half the chip each (swk_set_occ_cap).
-static thread_local int t_occ_cap = 0;
+// then evened out so every workgroup gets the same number of tiles (+-1).  (Every resident
+// slot with the last round partial measured +0.1 %: a SIMD whose workgroup finished early does
+// not speed its other waves up enough; the balanced chunk ranges of BAL launches do)
 
 // Occupancy per (kernel, block size, LDS bytes, device), queried once: the runtime query costs
 // microseconds, and the host feeder launches a kernel per chunk.
@@ -1334,37 +1492,26 @@ static int cached_occupancy(const void* fn, int threads, size_t lds, int dev, in
   return occ;
 }
 
-// (tuning) SWBANK_GRID_EVEN=0: every resident slot, the last round partial
-static bool env_flag_off(const char* name) {
-  const char* v = std::getenv(name);
-  return v && v[0] == '0' && v[1] == 0;
-}
-
 static unsigned persistent_grid(const void* fn, size_t ntiles, int threads, size_t lds) {
   int dev = 0, cus = 0;
-  const char* env = std::getenv("SWBANK_GRID");
-  const int cap = (env && *env) ? std::atoi(env) : -1;
-  if (cap == 0) return (unsigned)ntiles;
   if (hipGetDevice(&dev) != hipSuccess) return (unsigned)ntiles;
-  int occ = cached_occupancy(fn, threads, lds, dev, &cus);
+  const int occ = cached_occupancy(fn, threads, lds, dev, &cus);
   if (cus <= 0 || occ <= 0) return (unsigned)ntiles;
-  if (cap > 0) occ = std::min(occ, cap);
-  if (t_occ_cap > 0) occ = std::min(occ, t_occ_cap);
   const size_t slots = (size_t)cus * occ;
-  if (env_flag_off("SWBANK_GRID_EVEN")) return (unsigned)std::min(ntiles, slots);
   const size_t rounds = (ntiles + slots - 1) / slots;
   return (unsigned)((ntiles + rounds - 1) / rounds);
 }
 
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
-          bool MQ = false, bool STREAM = false, int C = 8>
-static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st) {
+          bool MQ = false, bool STREAM = false, int C = 8, bool BAL = false>
+static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st,
+                               unsigned bal_grid = 0) {
   const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE * (MQ ? a.nq : 1);  // units
   const size_t lds = (size_t)W * SWB_TILE * 4 +
                      (size_t)(64 + (a.edge_out ? C * 64 : 64) + (a.edge_in ? 2 * C * 64 : 0) +
                               (W > 1 ? W - 1 : 0) * 2 * C * 64) * 8 +
                      (PROF ? prof_bytes : 0) + (PAIR ? a.PS : 0) + (STREAM ? 256 : 0);
-  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR, MQ, STREAM, C>;
+  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR, MQ, STREAM, C, BAL>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -1373,8 +1520,18 @@ static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, h
     attr_set = true;
   }
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
-  unsigned grid = persistent_grid(reinterpret_cast<const void*>(fn), ntiles, 64 * W, lds);
+  unsigned grid = BAL ? bal_grid
+                      : persistent_grid(reinterpret_cast<const void*>(fn), ntiles, 64 * W, lds);
+#if SWK_STAMPS
+  if (!STREAM && g_stamps_host) {
+    ScoreArgs b = a;
+    b.tctr = reinterpret_cast<uint32_t*>(g_stamps_host);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * W), (unsigned)lds, st, b);
+    return hipGetLastError();
+  }
+#endif
   if (MQ && PAIR) grid = std::max(a.nq, grid / a.nq * a.nq);  // one query per workgroup
+  if (BAL && (grid == 0 || ntiles < 2 * (size_t)grid)) return hipErrorInvalidConfiguration;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * W), (unsigned)lds, st, a);
   return hipGetLastError();
 }
@@ -2042,13 +2199,9 @@ __global__ void __launch_bounds__(512) score_wave(const ScoreArgs a) {
 
 template <int K, bool COL0, bool PROF, bool GOTOH, bool F16>
 static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream_t st) {
-  // 4 waves (pairs) per block, sharing one LDS copy of the profile; SWBANK_WAVE_BLOCK=1..8
-  // for tuning (measured on 12.5k protein targets: 4 and 5 best, 8 -11 %, 2 -25 %); a split
-  // tail (split_blocks > 0) needs 4-wave blocks
-  const char* wenv = std::getenv("SWBANK_WAVE_BLOCK");
-  const unsigned wpb = a.split_blocks ? 4u
-                       : wenv && *wenv ? (unsigned)std::min(std::max(std::atoi(wenv), 1), 8)
-                                       : 4u;
+  // 4 waves (pairs) per block, sharing one LDS copy of the profile (measured on 12.5k protein
+  // targets: 4 and 5 best, 8 -11 %, 2 -25 %); the split tail needs 4-wave blocks
+  const unsigned wpb = 4u;
   const size_t blocks = a.split_blocks + ((size_t)a.main_pairs + wpb - 1) / wpb;
   size_t lds = PROF ? prof_bytes : 0;
   if (F16 && PROF) lds += 256 * wpb;  // the waves' code rings
@@ -2238,6 +2391,170 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   return make_uint2(bx, by);
 }
 
+// A tail segment wave of the two-pairs kernel (ScoreArgs.tail_*): pair main_pairs + ti, rows
+// [64 s, 64 s + 64) of the query, lane l = row 64 s + l (one row per lane), the one-pair wave
+// walk (step t: lane l computes column t - l).  Row -1 of the segment (s > 0) is segment s - 1's
+// bottom row from split_ring, read 64 columns at a time once segment s - 1 has finished the
+// 64-column block after them (lane 63 of segment s - 1 writes column c at step c + 63); lane
+// 63 writes this segment's bottom row.  Hand-offs: sc1 stores, vmcnt(0), an sc1 progress word;
+// sc1 polls and sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility).  The ring holds
+// every column, so no segment waits for the one below it: waits point only to lower block
+// numbers (dispatched earlier).  The last segment combines the segments' bests, re-scores the
+// pair in u16 when it crossed the optimistic f16 threshold, and writes the scores.
+template <bool GOTOH>
+__device__ __forceinline__ void wave_tail_seg(const ScoreArgs& a, uint8_t* wlds, int lane,
+                                           unsigned u) {
+  const unsigned T = a.tail_pairs, P = a.split_P;
+  const unsigned s = u / T, ti = u % T;
+  const size_t pair = (size_t)a.main_pairs + ti;
+  const size_t n = a.n, tA = 2 * pair, tB = tA + 1;
+  // this segment's f16 profile (letters x 64 rows x 2 B) into the wave's LDS slice
+  {
+    const uint32_t words = a.split_words;
+    const uint32_t* src = a.split_qtab + (size_t)s * words;
+    for (uint32_t i = lane; i < words; i += 64) reinterpret_cast<uint32_t*>(wlds)[i] = src[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  const bool packed = a.packed != SWK_PACK_BYTES, rec = a.packed == SWK_PACK_RECORDS;
+  const bool nib = a.packed == SWK_PACK_NIBBLE, uni = a.ustride != 0;
+  const uint32_t LA = rec ? record_len(a.res + tA * SWB_RECORD) : uni ? a.ulen : a.lens[tA];
+  const uint32_t LB = tB >= n ? 0u : rec ? record_len(a.res + tB * SWB_RECORD) : uni ? a.ulen
+                                                                                   : a.lens[tB];
+  const uint8_t* pA = rec ? a.res + tA * SWB_RECORD + 6 : uni ? a.res + tA * a.ustride
+                                                              : a.res + (LA ? a.offs[tA] : 0);
+  const uint8_t* pB = rec ? a.res + (tB < n ? tB : tA) * SWB_RECORD + 6
+                      : uni ? a.res + (tB < n ? tB : tA) * a.ustride
+                            : a.res + (LB ? a.offs[tB] : 0);
+  const int Lmax = (int)__builtin_amdgcn_readfirstlane(max(LA, LB));
+  const int nblk = (Lmax + 63 + 63) / 64;
+  const uint32_t pad = a.pad, PSb = a.split_PS;
+  const f16x2 NOE2 = as_f16x2(as_u16x2(a.f16_noe)), NE2 = as_f16x2(as_u16x2(a.f16_ne));
+  const u16x2 H0 = {0, 0};
+  const u16x2 X0 = GOTOH ? (u16x2){0, 0} : as_u16x2(NOE2);  // F / T of row -1
+  const auto code_word = [&](uint32_t c) -> uint32_t {  // letter offsets of column c
+    uint32_t x = pad, y = pad;
+    if (nib) {
+      if (c < LA) x = (pA[c >> 1] >> (4 * (c & 1))) & 15u;
+      if (c < LB) y = (pB[c >> 1] >> (4 * (c & 1))) & 15u;
+    } else if (packed) {
+      if (c < LA) x = (pA[c >> 2] >> (2 * (c & 3))) & 3u;
+      if (c < LB) y = (pB[c >> 2] >> (2 * (c & 3))) & 3u;
+    } else {
+      if (c < LA) x = pA[c];
+      if (c < LB) y = pB[c];
+    }
+    return min(x, pad) * PSb | (min(y, pad) * PSb) << 16;
+  };
+  uint32_t* prog = a.tail_prog + (size_t)ti * P;
+  uint2* bests = reinterpret_cast<uint2*>(a.tail_prog + (size_t)T * P) + (size_t)ti * P;
+  uint32_t* timeouts = a.tail_prog + (size_t)T * P * 3;
+  const auto wait_for = [&](const uint32_t* w, uint32_t v) {
+    for (int it = 0; it < (1 << 24); ++it) {
+      if (__builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= v)
+        return;
+      __builtin_amdgcn_s_sleep(4);
+    }
+    if (lane == 0) atomicAdd(timeouts, 1u);
+  };
+  const uint2* rin = s > 0 ? a.split_ring + ((size_t)ti * (P - 1) + (s - 1)) * a.tail_cols
+                           : nullptr;
+  uint2* rout = s + 1 < P ? a.split_ring + ((size_t)ti * (P - 1) + s) * a.tail_cols : nullptr;
+  u16x2 Hl[1] = {H0}, Xl[1] = {X0};
+  u16x2 best = {0, 0}, prevUpH = H0;
+  uint32_t botH = as_u32(H0), botX = as_u32(X0);
+  uint32_t let = code_word(~0u) + lane * (2u | 2u << 16);  // (padding, plus the row hop)
+  const uint8_t* plds = wlds;
+  for (int blk = 0; blk < nblk; ++blk) {
+    const uint32_t c0 = 64u * (uint32_t)blk + (uint32_t)lane;
+    const uint32_t buf = code_word(c0);
+    uint2 ebuf = make_uint2(as_u32(H0), as_u32(X0));
+    if (s > 0) {  // segment s - 1 finished block blk + 1 (or all of its blocks)
+      wait_for(prog + s - 1, (uint32_t)min(blk + 2, nblk));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (c0 < (uint32_t)Lmax) {
+        const uint64_t v =
+            __hip_atomic_load(reinterpret_cast<const uint64_t*>(rin + c0), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+        ebuf = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+      }
+    }
+    for (int j = 0; j < 64; ++j) {
+      const int t = 64 * blk + j;
+      const uint32_t injH = s > 0 ? __builtin_amdgcn_readlane(ebuf.x, j) : as_u32(H0);
+      const uint32_t injX = s > 0 ? __builtin_amdgcn_readlane(ebuf.y, j) : as_u32(X0);
+      u16x2 upH = as_u16x2(__builtin_amdgcn_update_dpp(injH, botH, 0x138, 0xF, 0xF, false));
+      u16x2 upX = as_u16x2(__builtin_amdgcn_update_dpp(injX, botX, 0x138, 0xF, 0xF, false));
+      let = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(buf, j), let + (2u | 2u << 16),
+                                        0x138, 0xF, 0xF, false);
+      u16x2 diag = prevUpH;
+      prevUpH = upH;
+      // (let carries both letters' profile offsets plus this lane's row, 2 B per hop)
+      const uint32_t eA = *reinterpret_cast<const uint16_t*>(plds + (let & 0xFFFFu));
+      const uint32_t eB = *reinterpret_cast<const uint16_t*>(plds + (let >> 16));
+      struct One {
+        uint32_t w;
+        __device__ __forceinline__ u16x2 operator()(int) const { return as_u16x2(w); }
+      } lk{eA | eB << 16};
+      if constexpr (GOTOH)
+        column_gotoh_f16<1, 1>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+      else
+        column_merged_f16<1, 1, false>(lk, diag, upX, Hl, Xl, best, NOE2, NE2);
+      botH = as_u32(Hl[0]);
+      botX = as_u32(GOTOH ? upX : Xl[0]);
+      if (rout && lane == 63 && t >= 63 && t - 63 < Lmax) {
+        const uint64_t v = (uint64_t)botX << 32 | botH;
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(rout + (t - 63)), v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (rout) {  // this block's ring columns are out
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_store(prog + s, (uint32_t)(blk + 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  uint32_t bx = (uint32_t)f16_unscore(best.x), by = (uint32_t)f16_unscore(best.y);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    bx = max(bx, (uint32_t)__shfl_xor((int)bx, off));
+    by = max(by, (uint32_t)__shfl_xor((int)by, off));
+  }
+  if (s + 1 < P) {  // hand the segment's bests to the last segment
+    if (lane == 0) {
+      const uint64_t v = (uint64_t)by << 32 | bx;
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(bests + s), v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_store(prog + s, (uint32_t)nblk + 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  for (unsigned k = 0; k + 1 < P; ++k) {
+    wait_for(prog + k, (uint32_t)nblk + 1u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(bests + k),
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bx = max(bx, (uint32_t)v);
+    by = max(by, (uint32_t)(v >> 32));
+  }
+  uint2 b = make_uint2(bx, by);
+  // optimistic f16: a pair above 2048 - max(s) is re-scored in u16 (one-pair K = 8 walk, the
+  // u16 profile from HBM)
+  if (a.fb_qtab && (int32_t)max(bx, by) > a.fb_thresh)
+    b = wave_pair<8, false, true, GOTOH, false>(a, reinterpret_cast<const uint8_t*>(a.fb_qtab),
+                                                a.fb_qtab, a.fb_nv, a.fb_PS, pair, lane);
+  if (lane == 0) {
+    a.scores[tA] = (int32_t)b.x;
+    if (tB < n) a.scores[tB] = (int32_t)b.y;
+  }
+}
+
 // configs[4]'s kernel: the wave kernel's split tail (blocks [0, split_blocks), as in
 // score_wave<8>) and main blocks of 4 waves scoring two pairs each (wave_two_pairs).  A pair
 // above the optimistic f16 threshold is re-scored in u16 by the whole wave with the one-pair
@@ -2251,6 +2568,16 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
     if (a.split_P == 4) wave_split_block<2, 4, false, true, GOTOH, true>(a, smem, lane);
     else wave_split_block<4, 2, false, true, GOTOH, true>(a, smem, lane);
     return;
+  }
+  if (a.tail_pairs) {  // the segmented tail: blocks after the main ones, one unit per wave
+    const unsigned mb = (a.main_pairs + 7) / 8;
+    if (blockIdx.x >= a.split_blocks + mb) {
+      const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      const unsigned u = (blockIdx.x - a.split_blocks - mb) * 4 + wave;
+      if (u < a.tail_pairs * a.split_P)
+        wave_tail_seg<GOTOH>(a, prof + (size_t)wave * a.split_words * 4, lane, u);
+      return;
+    }
   }
   {  // the K = 8 profile (64 16-byte row groups per letter, PS = 1024) with group 2l + q at
      // 32 q + l: lane l of a half reads its rows 16 l .. 16 l + 15 as 16 + 16 bytes, 512 apart
@@ -2293,9 +2620,11 @@ template <bool GOTOH>
 static hipError_t launch_wave_half(const ScoreArgs& a, uint32_t prof_bytes, hipStream_t st) {
   // 4 waves per block = 8 pairs, sharing one LDS copy of the profile; the split tail's blocks
   // hold every segment's profile
-  const size_t blocks = a.split_blocks + ((size_t)a.main_pairs + 7) / 8;
+  const size_t blocks = a.split_blocks + ((size_t)a.main_pairs + 7) / 8 +
+                        ((size_t)a.tail_pairs * a.split_P + 3) / 4;
   size_t lds = (size_t)prof_bytes + 1024 * 4;  // + each wave's code rings (2 x 128 u32)
   if (a.split_blocks) lds = std::max<size_t>(lds, (size_t)a.split_words * 4 * a.split_P);
+  if (a.tail_pairs) lds = std::max<size_t>(lds, (size_t)a.split_words * 4 * 4);  // a slice a wave
   auto fn = &score_wave_half<GOTOH>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -2324,7 +2653,6 @@ static hipError_t launch_wave_half(const ScoreArgs& a, uint32_t prof_bytes, hipS
   X(16, 4, 0, 0, 1, 1)                                                                        \
   X(16, 4, 0, 1, 0, 1) X(16, 4, 1, 1, 0, 1) X(16, 4, 0, 1, 1, 1) X(32, 4, 0, 0, 1, 1)
 
-extern "C" void swk_set_occ_cap(int per_cu) { swk::t_occ_cap = per_cu; }
 
 extern "C" int swk_has_variant(int R, int RB, int col0, int prof, int gotoh, int f16) {
 #define SWK_HAS(RR, BB, C0, PF, GT, FH) \
@@ -2404,6 +2732,59 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
   SWK_VARIANTS(SWK_CASE)
 #undef SWK_CASE
   return hipErrorInvalidValue;
+}
+
+#if SWK_STAMPS
+// (measurement builds) per-wave phase timing of the next tile-kernel launches into p:
+// [block][16 waves][8] u64 = entry, exit, active, fill/drain, barrier cycles, HW_ID, chunks, XCC
+extern "C" void swk_set_stamps(void* p) { swk::g_stamps_host = static_cast<uint64_t*>(p); }
+#endif
+
+// Balanced chunk ranges (ScoreArgs.bal_*) for the DNA merged f16 pair-table kernel (the
+// headline shape): a uniform batch of `ntiles` tiles of K chunks, codes one byte each (or
+// ustride / ulen), one query segment of W <= 4 waves.  swk_bal_slots gives the grid (every
+// resident slot); the host sizes bal_state ((grid + 1) x W x (2R + 2) x 64 words) and bal_flag
+// ((grid + 1) x W words, zeroed once; bal_flag[0] counts poll time-outs).
+extern "C" unsigned swk_bal_slots(int W, uint32_t PS) {
+  auto fn = &swk::score_kernel<32, 4, false, false, false, true, true, false, false, 8, true>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return 0;
+    attr_set = true;
+  }
+  const size_t lds = (size_t)W * SWB_TILE * 4 + (size_t)(64 + 64 + (W - 1) * 2 * 8 * 64) * 8 + PS;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  const int occ = swk::cached_occupancy(reinterpret_cast<const void*>(fn), 64 * W, lds, dev, &cus);
+  return occ > 0 && cus > 0 ? (unsigned)(occ * cus) : 0u;
+}
+
+extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* offs,
+                                          const uint32_t* lens, size_t n, const uint32_t* qtab,
+                                          uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
+                                          uint32_t PS, uint32_t pad, int W, int32_t* scores,
+                                          uint32_t pS1, uint32_t pS2, uint32_t ulen,
+                                          uint32_t ustride, uint32_t K, uint32_t* flag,
+                                          uint32_t* state, uint32_t gen, unsigned grid,
+                                          hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (W > 4 || !flag || !state || K == 0) return hipErrorInvalidValue;
+  swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
+                   O,    E,    PS,   pad, scores, nullptr, nullptr, 0u, 0u, (uint32_t)SWK_PACK_BYTES,
+                   nullptr, nullptr, 0u, nullptr, pS1, pS2,
+                   swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
+                   swk::f16_pair(-(int)O), nullptr, 0u, 0u, 0};
+  a.ulen = ulen;
+  a.ustride = ustride;
+  a.nq = 1;
+  a.bal_flag = flag;
+  a.bal_state = state;
+  a.bal_K = K;
+  a.bal_gen = gen;
+  return swk::launch_score<32, 4, false, false, false, true, true, false, false, 8, true>(
+      a, W, 0, st, grid);
 }
 
 // Streamed host batch (the feeder's one-launch path): equal-length targets (ulen codes), or
@@ -2557,7 +2938,21 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
   a.ustride = ustride;
   const size_t pairs = (n + 1) / 2;
   a.main_pairs = (uint32_t)pairs;
-  if (split && split->pairs > 0) {
+  if (split && split->pairs > 0 && split->P == 8) {
+    // the segmented tail of the two-pairs kernel (ScoreArgs.tail_*)
+    if (!half || K != 8 || edge_in || edge_out || accum || split->pairs > pairs ||
+        pairs > 0xFFFFFFFFull || !split->prog || split->cols == 0)
+      return hipErrorInvalidValue;
+    a.split_P = 8;
+    a.tail_pairs = split->pairs;
+    a.tail_cols = split->cols;
+    a.tail_prog = split->prog;
+    a.main_pairs = (uint32_t)(pairs - split->pairs);
+    a.split_qtab = split->qtab;
+    a.split_words = split->words;
+    a.split_PS = split->PS;
+    a.split_ring = static_cast<uint2*>(split->ring);
+  } else if (split && split->pairs > 0) {
     // the split tail is the last split->pairs pairs (K >= 8, one segment); with an odd count
     // the last block's second pair lies past the batch end
     if (K < 8 || edge_in || edge_out || accum || split->pairs > pairs || pairs > 0xFFFFFFFFull ||

@@ -116,11 +116,10 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   // Past that bound the f16 pass is still exact for every pair whose computed score stays
   // <= 2048 - max(s): a first rounded value needs an exact H > 2048 - max(s) on its
   // diagonal, and the running max keeps it.  Optimistic mode scores all pairs in f16, then
-  // re-scores the pairs above that threshold in u16 (SWBANK_F16_OPT=0 disables).
+  // re-scores the pairs above that threshold in u16.
   const bool f16_ok = b->f16 && b->f16_neg >= -2048 && env_int("SWBANK_F16", 1) != 0;
   const bool exact16 = f16_ok && top <= 2048u;
-  const bool opt16 = f16_ok && !exact16 && env_int("SWBANK_F16_OPT", 1) != 0 &&
-                     n <= 0xFFFFFFFFull;  // the re-score list holds 32-bit target numbers
+  const bool opt16 = f16_ok && !exact16 && n <= 0xFFFFFFFFull;  // the re-score list holds 32-bit target numbers
   const bool use_f16 = exact16 || opt16;
   bool use_wave = wave_preferred(b, n, max_len, use_f16);
   if (packed == SWK_PACK_MIXED) use_wave = false;  // (the feeder's mixed chunks: tile kernel)
@@ -134,7 +133,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
     // f16 profile, one segment of <= 512 rows (configs[4]): two pairs per wave, 16 rows per
     // lane (swk wave_two_pairs); SWBANK_WAVE_HALF=0 keeps one pair per wave
     const bool half = use_f16 && b->prof && !b->col0 && b->wK == 8 && b->wsegs == 1 &&
-                      env_int("SWBANK_WAVE_HALF", 1) != 0 && env_int("SWBANK_WAVE_BLOCK", 4) == 4;
+                      env_int("SWBANK_WAVE_HALF", 1) != 0;
     snprintf(b->last_kernel, sizeof(b->last_kernel), "wave %s%s K=%d segs=%d%s", arith,
              b->prof ? "-profile" : "", b->wK, b->wsegs, half ? " pairs/wave=2" : "");
     // segments hand the bottom row on through HBM: pairs x ecols x 8 B per edge buffer,
@@ -149,7 +148,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
     }
     // optimistic f16 with one query segment: the wave re-scores a flagged pair in u16 itself
     // (no flag kernel, no re-score launches)
-    wave_fb = opt16 && b->wsegs == 1 && env_int("SWBANK_WAVE_FB", 1) != 0;
+    wave_fb = opt16 && b->wsegs == 1;
     // Split tail: pairs beyond a whole number of waves per SIMD (one wave per pair, all
     // resident) would put one more wave on some SIMDs and set the kernel's length; the last
     // pairs % SIMDs pairs (when at most half the SIMDs) run instead as P row segments of K/P
@@ -159,16 +158,33 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
     SwkWaveSplit sp{};
     const size_t pairs = (n + 1) / 2;
     const int sforce = env_int("SWBANK_WAVE_SPLIT", -1);
-    if (b->sK[0] && b->wsegs == 1 && n == wspan && env_int("SWBANK_WAVE_BLOCK", 4) == 4 &&
-        pairs <= 0xFFFFFFFFull) {
+    if (b->sK[0] && b->wsegs == 1 && n == wspan && pairs <= 0xFFFFFFFFull) {
       const size_t simds = 4 * (size_t)std::max(b->cus, 1);
       const size_t units = half ? 2 * simds : simds;  // pairs per layer of one wave per SIMD
       size_t T = 0;
       if (sforce >= 0) T = std::min(pairs, (size_t)sforce);
       else if (pairs >= units && pairs % units <= units / 2) T = pairs % units;
       const int pforce = env_int("SWBANK_WAVE_SPLIT_P", 0);
+      // two pairs per wave (f16): a tail of at most SIMDs / 8 pairs runs as 8 segments of 64
+      // rows, one wave each on its own SIMD, handed on through global memory
+      const bool seg8 = half && b->sK[2] == 1 && T && (pforce == 8 || (!pforce && 8 * T <= simds));
       const int i = pforce == 2 ? 0 : pforce == 4 ? 1 : (4 * T <= simds ? 1 : 0);
-      if (T && b->sK[i]) {
+      if (seg8) {
+        HIPOK(b, b->sring.reserve(std::max<size_t>(1, T * 7 * (size_t)ecols)));
+        const size_t pw = T * 8 * 3 + 1;  // progress, bests (uint2), poll time-outs
+        HIPOK(b, b->tprog.reserve(pw));
+        HIPOK(b, hipMemsetAsync(b->tprog.p, 0, pw * 4, st));
+        sp.pairs = (unsigned)T;
+        sp.P = 8;
+        sp.qtab = b->stab16[2].p;
+        sp.words = (unsigned)b->sseg_words16[2];
+        sp.PS = b->sPS16[2];
+        sp.ring = b->sring.p;
+        sp.cols = ecols;
+        sp.prog = b->tprog.p;
+        const size_t L = strlen(b->last_kernel);
+        snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " tail=%zu/8", T);
+      } else if (T && b->sK[i]) {
         const unsigned P = 2u << i;
         HIPOK(b, b->sring.reserve((T + 4 / P - 1) / (4 / P) * (4 / P) * (P - 1) * 256));
         sp.pairs = (unsigned)T;
@@ -285,6 +301,34 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
         idx = b->fb_idx.p + p0;
         nidx = b->fb_cnt.p;
       }
+      // Balanced chunk ranges (the headline shape: a uniform batch through the pair-table
+      // kernel): every resident workgroup slot scores the same number of 8-column chunks, tiles
+      // cut by a range boundary handed between workgroups (ScoreArgs.bal_*).  Persistent
+      // workgroups with whole tiles leave the slots past tiles mod slots idle in the last round
+      // (998 of 1,024 on the headline batch, -2.4 %).  SWBANK_BAL=0 disables.
+      if (pass == 0 && f16 && use_pair && !gotoh && nseg == 1 && !idx && wait_prev &&
+          packed == SWK_PACK_BYTES && min_len == max_len && max_len > 0 && span == n &&
+          !opt16 && b->R == 32 && b->segs[0].W <= 4 && env_int("SWBANK_BAL", 1) != 0) {
+        const int Wl = b->segs[0].W;
+        const unsigned grid = swk_bal_slots(Wl, b->pair_bytes);
+        if (grid && ntiles >= 2 * (size_t)grid) {
+          const size_t sw = (size_t)(grid + 1) * Wl * (2 * 32 + 2) * 64;
+          HIPOK(b, b->bal_state.reserve(sw));
+          if (b->bal_flag.cap < (size_t)(grid + 1) * Wl) {  // zeroed once: flags carry bal_gen
+            HIPOK(b, b->bal_flag.reserve((size_t)(grid + 1) * Wl));
+            HIPOK(b, hipMemsetAsync(b->bal_flag.p, 0, b->bal_flag.cap * 4, st));
+          }
+          const uint32_t K = (max_len + 7) / 8;
+          HIPOK(b, swk_launch_pair_bal(res, offs, lens, np, b->qpair.p, b->nv16, b->S, b->O, b->E,
+                                       b->pair_bytes, b->pad, Wl, scores, b->pS1, b->pS2, ulen,
+                                       ustride, K, b->bal_flag.p, b->bal_state.p, ++b->bal_gen,
+                                       grid, st));
+          ++b->ctr.balanced_calls;
+          const size_t L = strlen(b->last_kernel);
+          snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " balanced grid=%u", grid);
+          continue;
+        }
+      }
       for (size_t s = 0; s < nseg; ++s) {
         const void* ein = s > 0 ? b->edge[(s - 1) & 1].p : nullptr;
         void* eout = s + 1 < nseg ? b->edge[s & 1].p : nullptr;
@@ -387,9 +431,10 @@ sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   // pair tables (5.5 instead of 6.5 VALU per row) when the set has them, the batch is f16-exact
   // and a grid that is a multiple of nq (one query per workgroup) loses at most 1/8 of the
   // resident slots
-  // (resident workgroups: 4 per CU for 128-row tables, 1 for the 16-wave 512-row ones)
+  // (resident workgroups: 4 per CU for 128-row tables, 2 for 256-row, 1 for the 16-wave
+  // 512-row ones)
   const int prow = std::max(b->mq_pair_rows, 32);
-  const size_t slots = (prow > 128 ? 1 : 4) * (size_t)std::max(b->cus, 1);
+  const size_t slots = (prow > 256 ? 1 : prow > 128 ? 2 : 4) * (size_t)std::max(b->cus, 1);
   const bool mpair = b->mq_pair_segs > 0 && use_f16 && nq <= slots &&
                      8 * (slots - slots / nq * nq) <= slots;
   const size_t nseg = mpair ? (size_t)b->mq_pair_segs : b->segs.size();

@@ -47,20 +47,6 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
   const size_t cap = std::max<size_t>(1, T / 8);
   for (size_t t = 0, sz = std::max<size_t>(1, T / 64); t < T; t += sz, sz = std::min(cap, 2 * sz))
     tile0.push_back(t);
-  // SWBANK_STREAM_TAPER=k: the last chunk cut into halves k times (1/2, 1/4, .., the rest), so
-  // the kernel's work after the last copy landed is a small chunk
-  const int taper = env_int("SWBANK_STREAM_TAPER", 0);
-  if (taper > 0 && tile0.size() > 1) {
-    const size_t last = tile0.back();
-    size_t rem = T - last, at = last;
-    tile0.pop_back();
-    tile0.push_back(at);
-    for (int k = 0; k < taper && rem / 2 >= 8; ++k) {
-      at += rem / 2;
-      rem -= rem / 2;
-      tile0.push_back(at);
-    }
-  }
   const size_t nsc = tile0.size();
   tile0.push_back(T);
   const size_t nib = (L + 1) / 2;  // 4-bit bytes per target (the 2-bit stream needs fewer)

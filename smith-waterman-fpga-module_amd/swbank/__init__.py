@@ -45,7 +45,8 @@ EXPORTS = (
 )
 ABI_VERSION = 4
 COUNTERS = ("stream_calls", "stream_reruns", "stream_declined", "chunked_calls", "device_sorts",
-            "gather_timeouts", "mixed_chunks", "mixed_runs")
+            "gather_timeouts", "mixed_chunks", "mixed_runs", "balanced_calls",
+            "balanced_timeouts")
 MAX_DEVICES = 16
 RECORD_BYTES, RECORD_MAX_BASES = 64, 232
 

@@ -1,0 +1,105 @@
+"""GPU: balanced chunk ranges.  A uniform device batch through the pair-table
+kernel gives every resident workgroup slot the same number of 8-column chunks; a tile cut by a
+range boundary is scored in two visits by two workgroups, the column state (H and T of every
+row, the diagonal above, the running best) handed over through global memory and a flag.
+
+Checked: bit-exact against the same bank with SWBANK_BAL=0 (whole tiles per workgroup) on every
+target, and against the oracle on every target of every cut tile (the cut positions follow from
+the grid the call reports), over query lengths that give 1-4 waves, target lengths that give 1-16
+chunks (a partial last chunk included), batch ends inside a tile, back-to-back calls (the flags'
+generation), poisoned device buffers."""
+import re
+
+import numpy as np
+import pytest
+
+import swbank as S
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+REF = (5, -4, -12, -4)
+
+
+def _cut_tiles(ntiles, K, grid):
+    """Tiles whose chunks a range boundary splits (A_g = g * ntiles * K // grid)."""
+    at = ntiles * K
+    cuts = {(at * g // grid) // K for g in range(1, grid) if (at * g // grid) % K}
+    return np.array(sorted(cuts), dtype=np.int64)
+
+
+@pytest.mark.parametrize("qlen,L,n", [(128, 128, 340_000), (100, 100, 300_001), (40, 9, 600_000),
+                                      (77, 64, 400_000), (128, 1, 300_000)])
+def test_balanced_ranges_exact(qlen, L, n, poisoned_buffers, monkeypatch):
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    q = O.random_codes(500 + qlen, qlen, 4)
+    res = O.random_codes(600 + L, n * L, 4)
+    # homologous targets past the first chunks, so a cut tile's best often lies after the cut
+    rng = np.random.default_rng(L)
+    for k in rng.choice(n, n // 50, replace=False):
+        m = min(L, qlen)
+        res[k * L:k * L + m] = q[:m]
+    offs = np.arange(n, dtype=np.uint64) * L
+    lens = np.full(n, L, np.uint32)
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+
+    def run(bal):
+        monkeypatch.setenv("SWBANK_BAL", bal)
+        st = torch.cuda.Stream()
+        out = []
+        with S.ScoreBank() as bank:
+            bank.set_penalties(*REF)
+            bank.load_query(q)
+            for _ in range(2):  # back to back: the second call's flags carry a new generation
+                sc = torch.full((n,), -7, dtype=torch.int32, device=dev)
+                bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(),
+                                        n, L, sc.data_ptr(), st.cuda_stream, min_len=L)
+                out.append(sc)
+            st.synchronize()
+            kern, ctr = bank.last_kernel(), bank.counters()
+        return [x.cpu().numpy() for x in out], kern, ctr
+
+    (a1, a2), kern, ctr = run("1")
+    (b1, _), kern0, _ = run("0")
+    assert "balanced" in kern and "balanced" not in kern0, (kern, kern0)
+    assert ctr["balanced_calls"] == 2 and ctr["balanced_timeouts"] == 0, ctr
+    assert np.array_equal(a1, b1) and np.array_equal(a2, b1)
+    grid = int(re.search(r"grid=(\d+)", kern).group(1))
+    ntiles = (n + 127) // 128
+    cut = _cut_tiles(ntiles, (L + 7) // 8, grid)
+    if L > 8:
+        assert len(cut) > grid // 2  # most range boundaries fall inside a tile
+    rows = np.concatenate([np.arange(t * 128, min(n, t * 128 + 128)) for t in cut]) \
+        if len(cut) else np.arange(0)
+    rows = np.unique(np.concatenate([rows, np.arange(min(n, 256)), np.arange(n - 256, n)]))
+    want = O.score_batch(q, res, np.ascontiguousarray(offs[rows]), np.ascontiguousarray(lens[rows]),
+                         O.dna_matrix(*REF[:2]), *REF[2:])
+    assert np.array_equal(a1[rows], want)
+
+
+def test_balanced_needs_uniform_lengths(monkeypatch):
+    """A ragged batch (min_len < max_len) or a batch of fewer than two tiles per slot keeps whole
+    tiles per workgroup."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    n, L = 200_000, 128
+    q = O.random_codes(1, 128, 4)
+    res = O.random_codes(2, n * L, 4)
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy((np.arange(n, dtype=np.uint64) * L).view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(np.full(n, L, np.int32)).to(dev)
+    sc = torch.empty(n, dtype=torch.int32, device=dev)
+    with S.ScoreBank() as bank:
+        bank.set_penalties(*REF)
+        bank.load_query(q)
+        bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), 1000, L,
+                                sc.data_ptr(), min_len=L)
+        assert "balanced" not in bank.last_kernel()  # 8 tiles
+        bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,
+                                sc.data_ptr(), min_len=L - 1)
+        assert "balanced" not in bank.last_kernel()
+        torch.cuda.synchronize()
+        assert bank.counters()["balanced_calls"] == 0

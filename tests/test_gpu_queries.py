@@ -162,7 +162,7 @@ def test_query_set_api_rules():
     assert np.array_equal(got, O.score_batch(queries[1], res, offs, lens, O.dna_matrix(), -12, -4))
 
 
-@pytest.mark.parametrize("rows", [512, 128])
+@pytest.mark.parametrize("rows", [512, 256, 128])
 @pytest.mark.parametrize("nq", [2, 5, 16, 33])
 def test_query_set_pair_tables(monkeypatch, nq, rows):
     """DNA merged f16 sets run on letter-pair tables, one query per workgroup (the grid a

@@ -59,11 +59,15 @@ def test_half_protein(monkeypatch, model, qlen, n):
     assert np.array_equal(one, want)
 
 
+@pytest.mark.parametrize("P", [4, 8])
 @pytest.mark.parametrize("split", [1, 2, 5, 64])
-def test_half_with_split_tail(monkeypatch, split):
-    """The split tail's blocks (one pair per 2 or 4 waves) ahead of the two-pairs blocks."""
+def test_half_with_split_tail(monkeypatch, split, P):
+    """The split tail beside the two-pairs blocks: P = 4, one pair per block of 4 segment waves
+    ahead of them (barrier hand-off), or P = 8, 64-row segments one wave each after them (hand-off
+    through global memory; the policy's choice for a tail of at most SIMDs / 8 pairs)."""
     monkeypatch.setenv("SWBANK_KERNEL", "wave")
     monkeypatch.setenv("SWBANK_WAVE_SPLIT", str(split))
+    monkeypatch.setenv("SWBANK_WAVE_SPLIT_P", str(P))
     rng = np.random.default_rng(split)
     q = rng.integers(0, 20, 512, dtype=np.uint8)
     seqs = _targets(rng, 301, 1, 1000, 20, q, homologs=3)
@@ -71,10 +75,55 @@ def test_half_with_split_tail(monkeypatch, split):
         bank.set_matrix(O.BLOSUM62, -11, -1)
         bank.load_query(q)
         got, one, kern = _both(monkeypatch, bank, lambda: bank.score_targets(seqs))
-    assert "pairs/wave=2" in kern and f"split={split}/" in kern, kern
+    tag = f"tail={split}/8" if P == 8 else f"split={split}/4"
+    assert "pairs/wave=2" in kern and tag in kern, kern
     res, offs, lens = O.pack_residues(seqs)
     want = O.score_batch(q, res, offs, lens, O.BLOSUM62, -11, -1, O.GAP_GOTOH)
     assert np.array_equal(got, want) and np.array_equal(one, want), kern
+
+
+@pytest.mark.parametrize("model", [S.GAP_GOTOH, S.GAP_MERGED])
+@pytest.mark.parametrize("n,qlen", [(12500, 512), (2300, 480), (4127, 300)])
+def test_half_segmented_tail_policy(monkeypatch, poisoned_buffers, model, n, qlen):
+    """The policy's own tail (configs[4]'s shape: 6,250 pairs = 3 two-pair waves per SIMD + 106
+    pairs as 8 x 64-row segments), ragged and empty targets among the tail pairs, near-copies of
+    the query past 2048 in the tail (the last segment re-scores its pair in u16), both gap
+    models, poisoned device buffers; device API (no host chunking)."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("SWBANK_KERNEL", "wave")
+    rng = np.random.default_rng(n + qlen + model)
+    q = rng.integers(0, 20, qlen, dtype=np.uint8)
+    seqs = _targets(rng, n, 900, 1000, 20)
+    for k in range(n - 220, n, 7):  # the tail's pairs: ragged, empty, homologous
+        seqs[k] = rng.integers(0, 20, int(rng.integers(0, 1000)), dtype=np.uint8)
+    seqs[n - 3] = np.zeros(0, np.uint8)
+    for k in (n - 5, n - 40, n - 150):
+        t = np.resize(q, 1000).copy()
+        t[::13] = rng.integers(0, 20, len(t[::13]))
+        seqs[k] = t
+    res, offs, lens = O.pack_residues(seqs)
+    dev = torch.device("cuda", 0)
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    d_sc = torch.full((n,), -9, dtype=torch.int32, device=dev)
+    with S.ScoreBank(alphabet=S.ALPHABET_PROTEIN, gap_model=model) as bank:
+        bank.set_matrix(O.BLOSUM62, -11, -1)
+        bank.load_query(q)
+        bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n,
+                                int(lens.max()), d_sc.data_ptr())
+        torch.cuda.synchronize()
+        kern = bank.last_kernel()
+    got = d_sc.cpu().numpy()
+    assert "pairs/wave=2" in kern, kern
+    if n == 12500:
+        assert "tail=106/8" in kern, kern
+    want = O.score_batch(q, res, offs, lens, O.BLOSUM62, -11, -1,
+                         O.GAP_GOTOH if model == S.GAP_GOTOH else O.GAP_MERGED)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (kern, [(int(i), int(lens[i]), int(got[i]), int(want[i]))
+                                  for i in bad[:8]])
+    assert want[n - 5] > 2048
 
 
 @pytest.mark.parametrize("layout", ["2bit", "nibble", "records"])
