@@ -102,6 +102,10 @@ def parse():
                     help="wall budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--profile-only", action="store_true",
                     help="run warmup+steps and exit without the CPU leg (for rocprofv3)")
+    ap.add_argument("--emulate-ingest", type=float, default=0.0, metavar="MB",
+                    help="(rehearsal, N=1) each step also copies MB of device memory on a second "
+                         "stream beside the kernel: rank 0's share of the score gather at N>1 "
+                         "(N-1 ranks x 4 B per target); reported as a separate field")
     return ap.parse_args()
 
 
@@ -311,8 +315,24 @@ def main():
     from swbank.dist import StepGather
     sg = StepGather(wl.d_sc, dst=0, stage_cpu=backend != "nccl")
 
+    # (rehearsal) rank 0's ingest of the other ranks' score vectors at N>1, as concurrent
+    # device-to-device copies on another stream: the collective's traffic and its copy kernels
+    # share rank 0's CUs with the score kernel, and `value` divides by the max over ranks
+    ingest = None
+    if args.emulate_ingest > 0:
+        nb = int(args.emulate_ingest * 2**20) // 4 * 4
+        ingest = (torch.cuda.Stream(), torch.empty(nb // 4, dtype=torch.int32, device=dev),
+                  torch.empty(nb // 4, dtype=torch.int32, device=dev))
+
     def step():
+        if ingest is not None:
+            s2, src, dst = ingest
+            s2.wait_stream(stream)
+            with torch.cuda.stream(s2):
+                dst.copy_(src, non_blocking=True)
         wl.run(stream.cuda_stream, sg.buffer())
+        if ingest is not None:
+            stream.wait_stream(ingest[0])  # the next step starts after this step's ingest
         sg.submit()
 
     def drain():
@@ -395,6 +415,7 @@ def main():
             "parallelism": f"dp{world}: pairs sharded, RCCL gather of scores to rank 0",
         },
         "kernel": kernel,
+        **({"emulated_ingest_mb": args.emulate_ingest} if args.emulate_ingest > 0 else {}),
         "kernel_ms": {"pack": round(pack_s * 1e3, 4), "score": round(score_s * 1e3, 4)},
         "roofline": {
             "bound": "valu",

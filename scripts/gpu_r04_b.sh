@@ -16,3 +16,16 @@ for bal in 0 1; do
     python scripts/stamps.py --bal $bal > gpurun_out/stamps_bal$bal.json || exit $?
   cat gpurun_out/stamps_bal$bal.json
 done
+# rank 0's N = 8 ingest (7 ranks x 4 B x 1,021,952 targets = 28.6 MB per step) as concurrent
+# device-to-device copies beside the headline kernel, against none
+for i in 1 2; do
+for mb in 0 28.6; do
+  timeout -k 10 300 python bench.py --cpu-seconds 0 --emulate-ingest $mb > gpurun_out/ingest.json 2> gpurun_out/ingest.err || { tail -5 gpurun_out/ingest.err; exit 3; }
+  python -c "import json; d=json.load(open('gpurun_out/ingest.json')); print('ingest', '$mb', d['value'], d['ms_per_step'], d['kernel_ms'])"
+done; done
+# the ragged device batch: wave-time attribution, with the permutation and presorted
+for extra in "--ragged" "--ragged --presorted"; do
+  SWBANK_LIB=$PWD/smith-waterman-fpga-module_amd/lib/libswbank_stamps.so timeout -k 10 300 \
+    python scripts/stamps.py $extra > gpurun_out/stamps_r.json || exit $?
+  cat gpurun_out/stamps_r.json
+done

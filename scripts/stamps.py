@@ -31,19 +31,43 @@ def main():
     ap.add_argument("--targets", type=int, default=499 * 2048)
     ap.add_argument("--L", type=int, default=128)
     ap.add_argument("--bal", default="1")
+    ap.add_argument("--ragged", action="store_true",
+                    help="bench.py's ragged batch (64-150 bp, 0.1 %% N; the device sort)")
+    ap.add_argument("--presorted", action="store_true",
+                    help="with --ragged: the batch physically reordered longest first, so the "
+                         "kernel reads it without the permutation (its gathered loads)")
     args = ap.parse_args()
     os.environ["SWBANK_BAL"] = args.bal
+    if args.presorted:  # caller's order = longest first: no device sort, no permutation
+        os.environ["SWBANK_DSORT"] = "0"
     import torch
     import swbank as S
     from bench import PEN, load_query, make_codes
 
     L, n = args.L, args.targets
     q = load_query()
-    res = make_codes(1000, n, L).reshape(-1)
     dev = torch.device("cuda", 0)
+    lens = np.full(n, L, np.uint32)
+    if args.ragged:
+        from bench import ragged_batch
+        res, offs, lens = ragged_batch(1000, n)
+        if args.presorted:  # longest first, stable (the device sort's order)
+            order = np.argsort(-lens.astype(np.int64), kind="stable")
+            seqs = [res[int(offs[k]):int(offs[k] + lens[k])] for k in order]
+            lens = lens[order]
+            offs = np.zeros(n, np.uint64)
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+            res = np.concatenate(seqs)
+        L = int(lens.max())
+        d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+        d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+        min_len = int(lens.min())
+    else:
+        res = make_codes(1000, n, L).reshape(-1)
+        d_offs = (torch.arange(n, dtype=torch.int64, device=dev) * L)
+        d_lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+        min_len = L
     d_res = torch.from_numpy(res).to(dev)
-    d_offs = (torch.arange(n, dtype=torch.int64, device=dev) * L)
-    d_lens = torch.full((n,), L, dtype=torch.int32, device=dev)
     d_sc = torch.zeros(n, dtype=torch.int32, device=dev)
     stamps = torch.zeros(4096 * 16 * 8, dtype=torch.int64, device=dev)
     lib = S.lib()
@@ -53,7 +77,7 @@ def main():
         bank.load_query(q)
         call = lambda: bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(),
                                                d_lens.data_ptr(), n, L, d_sc.data_ptr(),
-                                               min_len=L)
+                                               min_len=min_len)
         call()
         torch.cuda.synchronize()
         lib.swk_set_stamps(stamps.data_ptr())
@@ -88,6 +112,17 @@ def main():
     out["simds_seen"] = len(per)
     out["simd_active_spread"] = {"min": round(v.min() / span, 4), "median": round(float(np.median(v)) / span, 4),
                                  "max": round(v.max() / span, 4)}
+    # the work a tile does beyond its targets' cells: lanes past their target's end (a tile runs
+    # to its longest lane) and the last chunk's padding columns (8-column chunks); tiles in the
+    # longest-first order the device sort visits
+    srt = np.sort(lens.astype(np.int64))[::-1]
+    nt = (n + 127) // 128
+    tmax = srt[::128][:nt]
+    cells = float(srt.sum())
+    lane_cols = float(np.minimum(tmax, 10**9).sum()) * 128
+    chunk_cols = float((np.maximum(1, (tmax + 7) // 8) * 8).sum()) * 128
+    out["tile_work"] = {"idle_lanes": round((lane_cols - cells) / chunk_cols, 4),
+                        "chunk_padding": round((chunk_cols - lane_cols) / chunk_cols, 4)}
     print(json.dumps(out))
 
 

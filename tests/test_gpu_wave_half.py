@@ -123,7 +123,8 @@ def test_half_segmented_tail_policy(monkeypatch, poisoned_buffers, model, n, qle
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, (kern, [(int(i), int(lens[i]), int(got[i]), int(want[i]))
                                   for i in bad[:8]])
-    assert want[n - 5] > 2048
+    if qlen == 512:  # (a 300-row query's near-copies stay below 2048)
+        assert want[n - 5] > 2048
 
 
 @pytest.mark.parametrize("layout", ["2bit", "nibble", "records"])
