@@ -9,6 +9,7 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_wave_half.py tests/test_gpu
   "tests/test_gpu_queries.py::test_query_set_pair_tables" -x -q -p no:cacheprovider --timeout 300 \
   --timeout-method thread > gpurun_out/pytest_r04b.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_r04b.log; [ $rc -ne 0 ] && exit $rc
+ENVS="SWBANK_BAL_RAGGED=0|SWBANK_BAL_RAGGED=1" W=ragged bash scripts/gpu_env_ab.sh || exit $?
 ENVS="SWBANK_WAVE_SPLIT_P=4|-" W=protein512x1k bash scripts/gpu_env_ab.sh || exit $?
 ENVS="SWBANK_MQ_PAIR_ROWS=512|SWBANK_MQ_PAIR_ROWS=256" W=reads150x1k bash scripts/gpu_env_ab.sh || exit $?
 for bal in 0 1; do
@@ -24,7 +25,7 @@ for mb in 0 28.6; do
   python -c "import json; d=json.load(open('gpurun_out/ingest.json')); print('ingest', '$mb', d['value'], d['ms_per_step'], d['kernel_ms'])"
 done; done
 # the ragged device batch: wave-time attribution, with the permutation and presorted
-for extra in "--ragged" "--ragged --presorted"; do
+for extra in "--ragged" "--ragged --presorted" "--ragged --bal-ragged"; do
   SWBANK_LIB=$PWD/smith-waterman-fpga-module_amd/lib/libswbank_stamps.so timeout -k 10 300 \
     python scripts/stamps.py $extra > gpurun_out/stamps_r.json || exit $?
   cat gpurun_out/stamps_r.json

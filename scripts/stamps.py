@@ -36,8 +36,11 @@ def main():
     ap.add_argument("--presorted", action="store_true",
                     help="with --ragged: the batch physically reordered longest first, so the "
                          "kernel reads it without the permutation (its gathered loads)")
+    ap.add_argument("--bal-ragged", action="store_true",
+                    help="with --ragged: balanced chunk ranges over the sorted tiles")
     args = ap.parse_args()
     os.environ["SWBANK_BAL"] = args.bal
+    os.environ["SWBANK_BAL_RAGGED"] = "1" if args.bal_ragged else "0"
     if args.presorted:  # caller's order = longest first: no device sort, no permutation
         os.environ["SWBANK_DSORT"] = "0"
     import torch

@@ -67,6 +67,8 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           uint32_t pS1, uint32_t pS2, uint32_t ulen,
                                           uint32_t ustride, uint32_t K, uint32_t* flag,
                                           uint32_t* state, uint32_t gen, unsigned grid,
+                                          const uint32_t* idx, const uint32_t* nidx,
+                                          const uint32_t* ident, const void* plan,
                                           hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
@@ -77,7 +79,8 @@ extern "C" hipError_t swk_best_finalize(const unsigned long long* key, const uin
                                         uint64_t* out, uint64_t* out_index, hipStream_t st);
 extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max_len,
                                     uint32_t* perm, uint32_t* perm_n, uint32_t* ident,
-                                    uint32_t* scratch, hipStream_t st);
+                                    uint32_t* scratch, hipStream_t st, void* plan = nullptr,
+                                    unsigned G = 0);
 extern "C" size_t swk_sort_scratch_bytes(void);
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
                                     uint32_t* idx, uint32_t* count, hipStream_t st);
@@ -488,6 +491,7 @@ struct sw_bank {
   // balanced chunk ranges (swk_launch_pair_bal): the hand-off states and flags, the launch
   // generation the flags are compared with
   DevBuf<uint32_t> bal_state, bal_flag;
+  DevBuf<uint32_t> bal_plan;  // a ragged batch's range starts (4 words each, the device sort's)
   uint32_t bal_gen = 0;
   bool peer_ready = false;
   hipEvent_t ev_join = nullptr;

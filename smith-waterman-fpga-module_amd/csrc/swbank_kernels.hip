@@ -722,8 +722,12 @@ struct ScoreArgs {
   // poll time-outs.
   uint32_t* tail_prog;
   uint32_t tail_pairs, tail_cols;
+  // BAL over a ragged batch (bal_K == 0): tiles of different chunk counts in the device sort's
+  // longest-first order; workgroup g's range starts at {tile, chunk, chunk index} bal_plan[g]
+  // and ends at bal_plan[g + 1] (swk_sort_lens computes them with the sort)
+  const uint4* bal_plan;
 };
-static_assert(sizeof(ScoreArgs) == 336, "ScoreArgs layout (kernel argument block) changed");
+static_assert(sizeof(ScoreArgs) == 344, "ScoreArgs layout (kernel argument block) changed");
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) void* glob_void_ptr;
@@ -856,11 +860,24 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   // (the host checks), so the head and the tail are different tiles.  Visit v (= the tile
   // ordinal k) -> (tile, first chunk, end chunk), recomputed from blockIdx at each visit's end
   // (nothing of the plan stays live across the column loop)
-  const auto bal_visit = [&](int v, int& t, int& c0, int& c1) {
+  // (ragged batches, bal_plan: the range ends come from the plan and a visit's end chunk is the
+  // tile's own chunk count, c1 = -1 until the tile's lengths are read)
+  const auto bal_ends = [&](int& bs, int& bo, int& be, int& bf) {
+    if (a.bal_plan) {
+      const uint4 p0 = a.bal_plan[blockIdx.x], p1 = a.bal_plan[blockIdx.x + 1];
+      bs = (int)__builtin_amdgcn_readfirstlane(p0.x), bo = (int)__builtin_amdgcn_readfirstlane(p0.y);
+      be = (int)__builtin_amdgcn_readfirstlane(p1.x), bf = (int)__builtin_amdgcn_readfirstlane(p1.y);
+      return;
+    }
     const int bK = (int)a.bal_K;
     const uint64_t at = (uint64_t)ntiles * (uint64_t)bK;
     const uint64_t A0 = at * blockIdx.x / G, A1 = at * (blockIdx.x + 1) / G;
-    const int bs = (int)(A0 / bK), bo = (int)(A0 % bK), be = (int)(A1 / bK), bf = (int)(A1 % bK);
+    bs = (int)(A0 / bK), bo = (int)(A0 % bK), be = (int)(A1 / bK), bf = (int)(A1 % bK);
+  };
+  const auto bal_visit = [&](int v, int& t, int& c0, int& c1) {
+    const int bK = a.bal_plan ? -1 : (int)a.bal_K;
+    int bs, bo, be, bf;
+    bal_ends(bs, bo, be, bf);
     const int bfirst = bo ? bs + 1 : bs;
     const int hh = bf > 0 ? 1 : 0;
     if (v < hh) {
@@ -877,8 +894,13 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     c1 = __builtin_amdgcn_readfirstlane(c1);
   };
   if constexpr (BAL) {
-    const uint64_t at = (uint64_t)ntiles * (uint64_t)a.bal_K;
-    total = (int)(at * (blockIdx.x + 1) / G - at * blockIdx.x / G);
+    if (a.bal_plan) {
+      total = (int)__builtin_amdgcn_readfirstlane(a.bal_plan[blockIdx.x + 1].z -
+                                                  a.bal_plan[blockIdx.x].z);
+    } else {
+      const uint64_t at = (uint64_t)ntiles * (uint64_t)a.bal_K;
+      total = (int)(at * (blockIdx.x + 1) / G - at * blockIdx.x / G);
+    }
   } else if constexpr (STREAM) {
     total = (int)blockIdx.x < ntiles ? (1 << 30) : 0;
   } else {
@@ -973,7 +995,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   int nch, nfull;
   tile_chunks<C>(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
               nfull);
-  if constexpr (BAL) nch = vend;  // BAL: nch = the visit's end chunk (a head's: < bal_K)
+  if constexpr (BAL) nch = vend < 0 ? nch : vend;  // BAL: nch = the visit's end chunk
   const uint32_t S = a.S;
 
   for (int i = threadIdx.x; i < W * SWB_TILE; i += blockDim.x) bestsh[i] = 0;
@@ -1186,6 +1208,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
                                   a.ustride);
         tile_chunks<C>(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
                     n, nch_n, nfull_n);
+        if (BAL && nvend < 0) nvend = nch_n;
         load_raw<C, !MQ>(cur, nc0, nc0 < nfull_n, a.pad, STREAM ? packed_n : packed, rlo, rhi);
       }
       const int slot = g & 1;
@@ -1365,7 +1388,14 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         for (int jj = 0; jj < C; ++jj) dst[jj * 64] = sink[jj * 64 + lane];
       }
       if (last) {
-        if (BAL && nch < (int)a.bal_K) {  // BAL: a head visit ends: hand its state over
+        int bfh = 0;  // BAL: the first visit is a head when the range ends inside a tile
+        if constexpr (BAL) {
+          if (k == 0) {
+            int x0, x1, x2;
+            bal_ends(x0, x1, x2, bfh);
+          }
+        }
+        if (BAL && bfh > 0) {  // BAL: a head visit ends: hand its state over
           bal_store((int)blockIdx.x + 1);
         } else {  // this wave's part of tile k is done
         uint32_t* bs = bestsh + (k % W) * SWB_TILE;
@@ -2744,7 +2774,9 @@ extern "C" void swk_set_stamps(void* p) { swk::g_stamps_host = static_cast<uint6
 // headline shape): a uniform batch of `ntiles` tiles of K chunks, codes one byte each (or
 // ustride / ulen), one query segment of W <= 4 waves.  swk_bal_slots gives the grid (every
 // resident slot); the host sizes bal_state ((grid + 1) x W x (2R + 2) x 64 words) and bal_flag
-// ((grid + 1) x W words, zeroed once; bal_flag[0] counts poll time-outs).
+// ((grid + 1) x W words, zeroed once; bal_flag[0] counts poll time-outs).  A ragged batch
+// visited longest first through the device sort's permutation (idx / nidx / ident) passes the
+// sort's plan (swk_sort_lens with the same grid) instead of K.
 extern "C" unsigned swk_bal_slots(int W, uint32_t PS) {
   auto fn = &swk::score_kernel<32, 4, false, false, false, true, true, false, false, 8, true>;
   static bool attr_set = false;
@@ -2768,12 +2800,15 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           uint32_t pS1, uint32_t pS2, uint32_t ulen,
                                           uint32_t ustride, uint32_t K, uint32_t* flag,
                                           uint32_t* state, uint32_t gen, unsigned grid,
+                                          const uint32_t* idx, const uint32_t* nidx,
+                                          const uint32_t* ident, const void* plan,
                                           hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (W > 4 || !flag || !state || K == 0) return hipErrorInvalidValue;
+  if (W > 4 || !flag || !state || (plan ? false : K == 0) || (idx && !nidx))
+    return hipErrorInvalidValue;
   swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                    O,    E,    PS,   pad, scores, nullptr, nullptr, 0u, 0u, (uint32_t)SWK_PACK_BYTES,
-                   nullptr, nullptr, 0u, nullptr, pS1, pS2,
+                   idx, nidx, 0u, ident, pS1, pS2,
                    swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
                    swk::f16_pair(-(int)O), nullptr, 0u, 0u, 0};
   a.ulen = ulen;
@@ -2781,8 +2816,9 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
   a.nq = 1;
   a.bal_flag = flag;
   a.bal_state = state;
-  a.bal_K = K;
+  a.bal_K = plan ? 0u : K;
   a.bal_gen = gen;
+  a.bal_plan = static_cast<const uint4*>(plan);
   return swk::launch_score<32, 4, false, false, false, true, true, false, false, 8, true>(
       a, W, 0, st, grid);
 }
@@ -3216,10 +3252,17 @@ __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
 // Histogram of the bins, then (the last block to finish) exclusive offsets in place,
 // *perm_n = n, and *ident = 1 when at most one bin is non-empty (the caller's order is kept:
 // the scatter and the score kernel's indirection are skipped, and the hist is zeroed here).
+// plan != nullptr (balanced chunk ranges of a ragged batch, shift == 0 so a bin is one length):
+// the last block also writes, for g = 0..G, plan[g] = {tile, chunk, floor(g A / G), 0} of chunk
+// floor(g A / G) of
+// the longest-first tile sequence (A = its chunk count, tile t's chunk count ceil(len / 8) of the
+// bin holding its first, longest target), i.e. where each of the score kernel's G workgroups
+// starts.
 __global__ void __launch_bounds__(SORT_BLOCK) sort_hist_scan(const uint32_t* lens, size_t n,
                                                              uint32_t max_len, uint32_t shift,
                                                              uint32_t nb, uint32_t* hist,
-                                                             uint32_t* perm_n, uint32_t* ident) {
+                                                             uint32_t* perm_n, uint32_t* ident,
+                                                             uint4* plan, uint32_t G) {
   __shared__ uint32_t h[SORT_BINS];
   __shared__ uint32_t part[SORT_BLOCK];
   __shared__ int last;
@@ -3266,6 +3309,49 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_hist_scan(const uint32_t* len
     *perm_n = (uint32_t)n;
     *ident = one ? 1u : 0u;
     done[0] = 0;
+  }
+  if (!plan) return;
+  // tiles whose first position falls in bin b: [ceil(off_b / 128), ceil((off_b + cnt_b) / 128)),
+  // each of K_b = max(1, ceil(len_b / 8)) chunks (the bin's length is the tile's longest);
+  // h[] <- first tile of the bin, part[] <- chunks before the bin's first tile (exclusive scan
+  // of tiles x K over the bins, 2 bins per thread)
+  const auto kb = [&](uint32_t b) { return max(1u, ((max_len - b) + 7u) / 8u); };
+  const uint32_t t0 = (ex + 127) / 128, t1 = (ex + a + 127) / 128, t2 = (ex + a + c + 127) / 128;
+  const uint32_t w0 = i0 < nb ? (t1 - t0) * kb(i0) : 0u, w1 = i0 + 1 < nb ? (t2 - t1) * kb(i0 + 1) : 0u;
+  __syncthreads();
+  part[threadIdx.x] = w0 + w1;
+  if (i0 < nb) h[i0] = t0;
+  if (i0 + 1 < nb) h[i0 + 1] = t1;
+  __syncthreads();
+  for (uint32_t off = 1; off < SORT_BLOCK; off <<= 1) {
+    const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const uint32_t total = part[SORT_BLOCK - 1];  // chunks of all tiles
+  // chunks before bin b: part[b / 2 - 1] (inclusive prefix of the pairs before) plus, for an odd
+  // b, the even bin's weight
+  const auto before = [&](uint32_t b) -> uint32_t {
+    const uint32_t pr = b >= 2 ? part[b / 2 - 1] : 0u;
+    if ((b & 1) == 0) return pr;
+    return pr + ((b < nb ? h[b] : (uint32_t)((n + 127) / 128)) - h[b - 1]) * kb(b - 1);
+  };
+  const uint32_t ntiles = (uint32_t)((n + 127) / 128);
+  for (uint32_t g = threadIdx.x; g <= G; g += SORT_BLOCK) {
+    const uint32_t A = (uint32_t)((uint64_t)total * g / G);
+    uint4 r = make_uint4(ntiles, 0u, A, 0u);
+    if (A < total) {
+      uint32_t lo = 0, hi = nb;  // the last bin with before(bin) <= A (and a tile in it)
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (before(mid) <= A) lo = mid; else hi = mid;
+      }
+      while (lo + 1 < nb && before(lo + 1) <= A) ++lo;  // (bins without tiles have no width)
+      const uint32_t d = A - before(lo), K = kb(lo);
+      r = make_uint4(h[lo] + d / K, d % K, A, 0u);
+    }
+    plan[g] = r;
   }
 }
 
@@ -3314,15 +3400,16 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_scatter(const uint32_t* lens,
 // swk_sort_scratch_bytes(), zero on entry and on return.
 extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max_len,
                                     uint32_t* perm, uint32_t* perm_n, uint32_t* ident,
-                                    uint32_t* scratch, hipStream_t st) {
+                                    uint32_t* scratch, hipStream_t st, void* plan, unsigned G) {
   if (n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
   uint32_t shift = 0;
   while ((max_len >> shift) >= (uint32_t)swk::SORT_BINS) ++shift;
   const uint32_t nb = (max_len >> shift) + 1;
+  if (plan && (shift != 0 || G == 0)) return hipErrorInvalidValue;
   const unsigned blocks =
       (unsigned)((n + swk::SORT_BLOCK * swk::SORT_ITEMS - 1) / (swk::SORT_BLOCK * swk::SORT_ITEMS));
   hipLaunchKernelGGL(swk::sort_hist_scan, dim3(blocks), dim3(swk::SORT_BLOCK), 0, st, lens, n,
-                     max_len, shift, nb, scratch, perm_n, ident);
+                     max_len, shift, nb, scratch, perm_n, ident, static_cast<uint4*>(plan), G);
   hipLaunchKernelGGL(swk::sort_scatter, dim3(blocks), dim3(swk::SORT_BLOCK), 0, st, lens, n,
                      max_len, shift, nb, scratch, perm, ident);
   return hipGetLastError();

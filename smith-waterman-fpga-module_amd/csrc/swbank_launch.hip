@@ -225,6 +225,21 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   // A device batch (dsort) visits its targets longest first, sorted on the device, so every
   // tile holds similar lengths (a tile runs to its longest lane); SWBANK_DSORT=0 disables.
   const uint32_t* ident = nullptr;  // device sort: 1 when the lengths share one bin
+  // Balanced chunk ranges over a ragged device batch: the sort's last block also
+  // writes where each workgroup's range starts in the longest-first tile sequence, so the choice
+  // is made before the sort.  Every range must hold two of the longest tiles' chunks (the head
+  // and the tail of a range are different tiles): checked with the caller's length bounds.
+  unsigned rbal_grid = 0;
+  if (dsort && !sort_out && !use_wave && !perm && use_f16 && use_pair && !gotoh && nseg == 1 &&
+      wait_prev && packed == SWK_PACK_BYTES && min_len < max_len && max_len < 2048 && !opt16 &&
+      b->R == 32 && b->segs[0].W <= 4 && n <= 0xFFFFFFFFull && env_int("SWBANK_DSORT", 1) != 0 &&
+      env_int("SWBANK_BAL", 1) != 0 && env_int("SWBANK_BAL_RAGGED", 0) != 0 &&
+      !one_len_bin(min_len, max_len)) {
+    const unsigned grid = swk_bal_slots(b->segs[0].W, b->pair_bytes);
+    const size_t kmin = std::max<uint32_t>(1u, (min_len + 7) / 8), kmax = (max_len + 7) / 8;
+    if (grid && ntiles * kmin >= 2 * (size_t)grid * kmax && ntiles * kmax < (1ull << 31))
+      rbal_grid = grid;
+  }
   // (the host feeder passes a chunk's own order (n + 2 words in its slot) and sort scratch, so
   // chunks on two streams do not share them)
   if (dsort && !use_wave && !perm && packed != SWK_PACK_RECORDS && ntiles > 1 &&
@@ -243,7 +258,9 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       }
       scr = b->dsort.p;
     }
-    HIPOK(b, swk_sort_lens(d_lens, n, max_len, order, order + n, order + n + 1, scr, st));
+    if (rbal_grid) HIPOK(b, b->bal_plan.reserve((size_t)(rbal_grid + 1) * 4));
+    HIPOK(b, swk_sort_lens(d_lens, n, max_len, order, order + n, order + n + 1, scr, st,
+                           rbal_grid ? b->bal_plan.p : nullptr, rbal_grid));
     ++b->ctr.device_sorts;
     if (!sort_out) {  // (the host feeder's chunks sort too: not named per chunk)
       const size_t L = strlen(b->last_kernel);
@@ -305,13 +322,15 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       // kernel): every resident workgroup slot scores the same number of 8-column chunks, tiles
       // cut by a range boundary handed between workgroups (ScoreArgs.bal_*).  Persistent
       // workgroups with whole tiles leave the slots past tiles mod slots idle in the last round
-      // (998 of 1,024 on the headline batch, -2.4 %).  SWBANK_BAL=0 disables.
-      if (pass == 0 && f16 && use_pair && !gotoh && nseg == 1 && !idx && wait_prev &&
-          packed == SWK_PACK_BYTES && min_len == max_len && max_len > 0 && span == n &&
-          !opt16 && b->R == 32 && b->segs[0].W <= 4 && env_int("SWBANK_BAL", 1) != 0) {
+      // (998 of 1,024 on the headline batch, -2.4 %).  A ragged device batch (rbal_grid) runs
+      // through the sort's permutation with the sort's plan.  SWBANK_BAL=0 disables.
+      const bool rbal = pass == 0 && rbal_grid && perm && idx == perm && span == n;
+      if (rbal || (pass == 0 && f16 && use_pair && !gotoh && nseg == 1 && !idx && wait_prev &&
+                   packed == SWK_PACK_BYTES && min_len == max_len && max_len > 0 && span == n &&
+                   !opt16 && b->R == 32 && b->segs[0].W <= 4 && env_int("SWBANK_BAL", 1) != 0)) {
         const int Wl = b->segs[0].W;
-        const unsigned grid = swk_bal_slots(Wl, b->pair_bytes);
-        if (grid && ntiles >= 2 * (size_t)grid) {
+        const unsigned grid = rbal ? rbal_grid : swk_bal_slots(Wl, b->pair_bytes);
+        if (grid && (rbal || ntiles >= 2 * (size_t)grid)) {
           const size_t sw = (size_t)(grid + 1) * Wl * (2 * 32 + 2) * 64;
           HIPOK(b, b->bal_state.reserve(sw));
           if (b->bal_flag.cap < (size_t)(grid + 1) * Wl) {  // zeroed once: flags carry bal_gen
@@ -321,8 +340,9 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
           const uint32_t K = (max_len + 7) / 8;
           HIPOK(b, swk_launch_pair_bal(res, offs, lens, np, b->qpair.p, b->nv16, b->S, b->O, b->E,
                                        b->pair_bytes, b->pad, Wl, scores, b->pS1, b->pS2, ulen,
-                                       ustride, K, b->bal_flag.p, b->bal_state.p, ++b->bal_gen,
-                                       grid, st));
+                                       ustride, rbal ? 0u : K, b->bal_flag.p, b->bal_state.p,
+                                       ++b->bal_gen, grid, idx, nidx, ident,
+                                       rbal ? b->bal_plan.p : nullptr, st));
           ++b->ctr.balanced_calls;
           const size_t L = strlen(b->last_kernel);
           snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " balanced grid=%u", grid);

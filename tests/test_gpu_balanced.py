@@ -103,3 +103,53 @@ def test_balanced_needs_uniform_lengths(monkeypatch):
         assert "balanced" not in bank.last_kernel()
         torch.cuda.synchronize()
         assert bank.counters()["balanced_calls"] == 0
+
+
+@pytest.mark.parametrize("qlen,lo,hi,n", [(128, 64, 150, 1_000_003), (40, 30, 61, 1_500_000),
+                                          (100, 1, 24, 2_000_000)])
+def test_balanced_ranges_ragged(qlen, lo, hi, n, poisoned_buffers, monkeypatch):
+    """A ragged device batch: the device sort visits it longest first and also computes where
+    each workgroup's range starts (tiles of different chunk counts); bit-exact against whole
+    tiles per workgroup on every target, and against the oracle on a sample."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(qlen + hi)
+    q = O.random_codes(700 + qlen, qlen, 4)
+    lens = rng.integers(lo, hi + 1, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    res = O.random_codes(800 + hi, int(lens.sum(dtype=np.uint64)), 4)
+    for k in rng.choice(n, n // 50, replace=False):  # homologous targets
+        m = int(min(lens[k], qlen))
+        res[int(offs[k]):int(offs[k]) + m] = q[:m]
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+
+    def run(bal):
+        monkeypatch.setenv("SWBANK_BAL", bal)
+        monkeypatch.setenv("SWBANK_BAL_RAGGED", bal)
+        st = torch.cuda.Stream()
+        out = []
+        with S.ScoreBank() as bank:
+            bank.set_penalties(*REF)
+            bank.load_query(q)
+            for _ in range(2):
+                sc = torch.full((n,), -7, dtype=torch.int32, device=dev)
+                bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(),
+                                        n, hi, sc.data_ptr(), st.cuda_stream, min_len=lo)
+                out.append(sc)
+            st.synchronize()
+            kern, ctr = bank.last_kernel(), bank.counters()
+        return [x.cpu().numpy() for x in out], kern, ctr
+
+    (a1, a2), kern, ctr = run("1")
+    (b1, _), kern0, _ = run("0")
+    assert "balanced" in kern and "dsort" in kern and "balanced" not in kern0, (kern, kern0)
+    assert ctr["balanced_calls"] == 2 and ctr["balanced_timeouts"] == 0, ctr
+    assert np.array_equal(a1, b1) and np.array_equal(a2, b1)
+    rows = np.unique(np.concatenate([rng.choice(n, 3000, replace=False), np.arange(200),
+                                     np.arange(n - 200, n)]))
+    want = O.score_batch(q, res, np.ascontiguousarray(offs[rows]), np.ascontiguousarray(lens[rows]),
+                         O.dna_matrix(*REF[:2]), *REF[2:])
+    assert np.array_equal(a1[rows], want)
