@@ -1,13 +1,10 @@
 #!/bin/bash
-# Round 4: the balanced-range tests and a headline A/B of SWBANK_BAL, the VALU issue-rate
+# Round 4: a headline A/B of SWBANK_BAL, the VALU issue-rate
 # microbenchmark (profiles/r04/valu_rate.jsonl), the in-process host A/B harness on the ragged
 # and uniform host batches.  Each step time-limited; a failure ends the script.
 set -u
 cd ${GRAFT_REPO_ROOT:-$(dirname "$0")/..}
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_balanced.py -x -q -p no:cacheprovider --timeout 300 \
-  --timeout-method thread > gpurun_out/pytest_balanced.log 2>&1
-rc=$?; tail -3 gpurun_out/pytest_balanced.log; [ $rc -ne 0 ] && exit $rc
 ENVS="SWBANK_BAL=0|SWBANK_BAL=1" W=q100xdata500 bash scripts/gpu_env_ab.sh || exit $?
 timeout -k 10 300 ./scripts/ubench/valu_rate > gpurun_out/valu_rate.jsonl || exit $?
 tail -16 gpurun_out/valu_rate.jsonl
