@@ -9,10 +9,10 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_wave_half.py tests/test_gpu
   "tests/test_gpu_queries.py::test_query_set_pair_tables" -x -q -p no:cacheprovider --timeout 300 \
   --timeout-method thread > gpurun_out/pytest_r04b.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_r04b.log; [ $rc -ne 0 ] && exit $rc
-# the last chunk trimmed to its last column holding a code (SWK_TRIM) against whole chunks
-LIBS="main|notrim" W=ragged bash scripts/gpu_lib_ab.sh || exit $?
-LIBS="main|notrim" W=data500 bash scripts/gpu_lib_ab.sh || exit $?
-LIBS="main|notrim" W=q100xdata500 bash scripts/gpu_lib_ab.sh || exit $?
+# a build whose tiles stop at their last column holding a code (SWK_TRIM=1) against the kept one
+LIBS="main|trim" W=ragged bash scripts/gpu_lib_ab.sh || exit $?
+LIBS="main|trim" W=data500 bash scripts/gpu_lib_ab.sh || exit $?
+LIBS="main|trim" W=q100xdata500 bash scripts/gpu_lib_ab.sh || exit $?
 ENVS="SWBANK_BAL_RAGGED=0|SWBANK_BAL_RAGGED=1" W=ragged bash scripts/gpu_env_ab.sh || exit $?
 ENVS="SWBANK_WAVE_SPLIT_P=4|-" W=protein512x1k bash scripts/gpu_env_ab.sh || exit $?
 ENVS="SWBANK_MQ_PAIR_ROWS=512|SWBANK_MQ_PAIR_ROWS=256" W=reads150x1k bash scripts/gpu_env_ab.sh || exit $?

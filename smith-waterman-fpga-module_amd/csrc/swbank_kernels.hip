@@ -36,7 +36,10 @@
 #include "swbank_internal.h"
 
 #ifndef SWK_TRIM
-#define SWK_TRIM 1  // a tile's last chunk stops at its last column holding a code
+// A/B build: a tile's last chunk stops at its last column holding a code (saves the ragged
+// batches' padding columns, but the per-column test costs the headline ~25 VALU per chunk in
+// register copies; a two-copy chunk spills)
+#define SWK_TRIM 0
 #endif
 #ifndef SWK_STAMPS
 #define SWK_STAMPS 0  // measurement builds: per-wave phase timing of the tile kernel (swk_set_stamps)
@@ -1400,7 +1403,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         asm volatile("" : "+v"(best));
         rout[jj * ostride] = make_uint2(as_u32(Hl[R - 1]), as_u32(upX));
       }
-      if constexpr (PAIR) {
+      if constexpr (PAIR && SWK_TRIM) {
         if (trimmed) {  // the next chunk's column 0, read ahead as at a chunk's end
           acur = pair_addr(rlo.x, rhi.x, 0);
           pA0 = ld4(acur + 16);
