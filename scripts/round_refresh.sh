@@ -24,5 +24,7 @@ rc=$?; step profile $rc; if [ $rc -ne 0 ]; then exit $rc; fi
 bash scripts/gpu_profile.sh "${TAG}_protein" --workload protein512x1k
 rc=$?; step profile_protein $rc; if [ $rc -ne 0 ]; then exit $rc; fi
 bash scripts/gpu_profile.sh "${TAG}_reads" --workload reads150x1k
-rc=$?; step profile_reads $rc
+rc=$?; step profile_reads $rc; if [ $rc -ne 0 ]; then exit $rc; fi
+bash scripts/gpu_profile.sh "${TAG}_ragged" --workload ragged
+rc=$?; step profile_ragged $rc
 exit $rc
