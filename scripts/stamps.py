@@ -38,6 +38,7 @@ def main():
                          "kernel reads it without the permutation (its gathered loads)")
     ap.add_argument("--bal-ragged", action="store_true",
                     help="with --ragged: balanced chunk ranges over the sorted tiles")
+    ap.add_argument("--dump", default="", help="save the raw per-wave records (.npy)")
     args = ap.parse_args()
     os.environ["SWBANK_BAL"] = args.bal
     os.environ["SWBANK_BAL_RAGGED"] = "1" if args.bal_ragged else "0"
@@ -72,7 +73,7 @@ def main():
         min_len = L
     d_res = torch.from_numpy(res).to(dev)
     d_sc = torch.zeros(n, dtype=torch.int32, device=dev)
-    stamps = torch.zeros(4096 * 16 * 8, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(4096 * 16 * 16, dtype=torch.int64, device=dev)
     lib = S.lib()
     lib.swk_set_stamps.argtypes = [ctypes.c_void_p]
     with S.ScoreBank(device=0) as bank:
@@ -88,33 +89,44 @@ def main():
         torch.cuda.synchronize()
         lib.swk_set_stamps(None)
         kern = bank.last_kernel()
-    st = stamps.cpu().numpy().reshape(-1, 8).astype(np.int64)
+    st = stamps.cpu().numpy().reshape(-1, 16).astype(np.int64)
     st = st[st[:, 1] > 0]
-    t0, t1, act, idle, bar, hw, xcc = (st[:, 0], st[:, 1], st[:, 2], st[:, 3], st[:, 4], st[:, 5],
-                                       st[:, 7])
-    span = int(t1.max() - t0.min())
+    if args.dump:
+        np.save(args.dump, st)
+    t0, t1, act, idle, bar, hw, xcc, bload = (st[:, 0], st[:, 1], st[:, 2], st[:, 3], st[:, 4],
+                                              st[:, 5], st[:, 7], st[:, 8])
+    # s_memtime counts each XCD's own clock (the XCDs' counters are not aligned): spans, ramps
+    # and exits are taken per XCC, then summed
     waves = len(st)
-    tot = float(waves) * span
-    ramp = float((t0 - t0.min()).sum())
-    exit_ = float((t1.max() - t1).sum())
-    # the barrier after an active phase vs. the fill/drain phases' whole time
+    tot = ramp = exit_ = 0.0
+    spans = {}
+    for x in np.unique(xcc):
+        m = xcc == x
+        sp = float(t1[m].max() - t0[m].min())
+        spans[int(x)] = sp
+        tot += sp * m.sum()
+        ramp += float((t0[m] - t0[m].min()).sum())
+        exit_ += float((t1[m].max() - t1[m]).sum())
     inner = (t1 - t0) - act - idle - bar  # loop set-up and the epilogue
-    out = {"kernel": kern, "targets": n, "waves": waves, "span_ticks": span,
+    out = {"kernel": kern, "targets": n, "waves": waves,
+           "span_ticks_per_xcc": {"min": min(spans.values()), "max": max(spans.values())},
+           "chunks_per_wave": {"min": int(st[:, 6].min()), "max": int(st[:, 6].max())},
            "share": {"ramp": round(ramp / tot, 4), "active": round(act.sum() / tot, 4),
                      "barrier": round(bar.sum() / tot, 4),
                      "filldrain": round(idle.sum() / tot, 4),
                      "setup": round(inner.sum() / tot, 4),
-                     "exit": round(exit_ / tot, 4)}}
+                     "exit": round(exit_ / tot, 4)},
+           "tail_state_load": round(bload.sum() / tot, 5)}
     # per SIMD: active ticks of its waves (HW_ID: simd 5:4, cu 11:8, sh 12, se 15:13) and XCC
     key = (xcc * 10000 + ((hw >> 13) & 7) * 1000 + ((hw >> 12) & 1) * 100 + ((hw >> 8) & 15) * 10
            + ((hw >> 4) & 3))
     per = {}
-    for k, a in zip(key.tolist(), act.tolist()):
-        per[k] = per.get(k, 0) + a
+    for k, a, x in zip(key.tolist(), act.tolist(), xcc.tolist()):
+        per[k] = per.get(k, 0) + a / spans[int(x)]
     v = np.array(list(per.values()), dtype=np.float64)
     out["simds_seen"] = len(per)
-    out["simd_active_spread"] = {"min": round(v.min() / span, 4), "median": round(float(np.median(v)) / span, 4),
-                                 "max": round(v.max() / span, 4)}
+    out["simd_active_spread"] = {"min": round(v.min(), 4), "median": round(float(np.median(v)), 4),
+                                 "max": round(v.max(), 4)}
     # the work a tile does beyond its targets' cells: lanes past their target's end (a tile runs
     # to its longest lane) and the last chunk's padding columns (8-column chunks); tiles in the
     # longest-first order the device sort visits

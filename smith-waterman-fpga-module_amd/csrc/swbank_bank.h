@@ -65,11 +65,10 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
                                           uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                           uint32_t pS1, uint32_t pS2, uint32_t ulen,
-                                          uint32_t ustride, uint32_t K, uint32_t* flag,
-                                          uint32_t* state, uint32_t gen, unsigned grid,
-                                          const uint32_t* idx, const uint32_t* nidx,
-                                          const uint32_t* ident, const void* plan,
-                                          hipStream_t st);
+                                          uint32_t ustride, uint32_t* flag, uint32_t* state,
+                                          uint32_t gen, unsigned grid, const uint32_t* idx,
+                                          const uint32_t* nidx, const uint32_t* ident,
+                                          const void* plan, hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
                                    hipStream_t st);
@@ -491,7 +490,12 @@ struct sw_bank {
   // balanced chunk ranges (swk_launch_pair_bal): the hand-off states and flags, the launch
   // generation the flags are compared with
   DevBuf<uint32_t> bal_state, bal_flag;
-  DevBuf<uint32_t> bal_plan;  // a ragged batch's range starts (4 words each, the device sort's)
+  // range starts, 4 words each: a ragged batch's (the device sort writes them per call) or a
+  // uniform batch's (host-computed for bal_key = {tiles, chunks per tile, grid}, kept while the
+  // key holds; bal_key[0] = 0 when the sort overwrote them)
+  DevBuf<uint32_t> bal_plan;
+  std::vector<uint32_t> bal_plan_host;
+  size_t bal_key[3] = {0, 0, 0};
   uint32_t bal_gen = 0;
   bool peer_ready = false;
   hipEvent_t ev_join = nullptr;

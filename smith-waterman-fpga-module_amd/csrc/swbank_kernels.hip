@@ -713,15 +713,18 @@ struct ScoreArgs {
   uint32_t* dflag;
   uint32_t* tctr;
   uint32_t nsc;
-  // balanced chunk ranges (BAL variants, uniform batches: every tile bal_K chunks): workgroup g
-  // scores chunks [A_g, A_g+1) of the tile-major chunk sequence, A_g = g x tiles x bal_K / G, so
-  // every resident slot gets the same work whatever tiles / slots is.  A tile cut by a range
-  // boundary is scored in two visits: workgroup g - 1 scores its first chunks first (its "head")
-  // and hands each wave's column state over through bal_state (sc1 stores, then the flag
+  // balanced chunk ranges (BAL variants): workgroup g scores chunks [A_g, A_g+1) of the
+  // tile-major chunk sequence, A_g = g x chunks / G, so every resident slot gets the same work
+  // whatever tiles / slots is; its range starts at {tile, chunk, A_g} = bal_plan[g] and ends at
+  // bal_plan[g + 1] (uniform batches: the host's, ragged ones: the device sort's, whose tiles
+  // run longest first with different chunk counts).  A tile cut by a range boundary is scored
+  // in two visits: workgroup g - 1 scores its first chunks first (its "head") and hands each
+  // wave's column state over through bal_state (sc1 stores, then, a phase later, the flag
   // bal_flag[g][wave] = bal_gen); workgroup g scores the rest last (its "tail").
   uint32_t* bal_flag;
   uint32_t* bal_state;
-  uint32_t bal_K, bal_gen;
+  const uint4* bal_plan;
+  uint32_t bal_gen;
   // two-pairs wave kernel, segmented tail (tail_pairs > 0; split_P = 8, the split_* tables and
   // split_ring): the last tail_pairs pairs run as split_P row segments of 64 rows, one wave
   // each, in 4-wave blocks after the main blocks; segment s hands its bottom row to s + 1
@@ -731,10 +734,6 @@ struct ScoreArgs {
   // poll time-outs.
   uint32_t* tail_prog;
   uint32_t tail_pairs, tail_cols;
-  // BAL over a ragged batch (bal_K == 0): tiles of different chunk counts in the device sort's
-  // longest-first order; workgroup g's range starts at {tile, chunk, chunk index} bal_plan[g]
-  // and ends at bal_plan[g + 1] (swk_sort_lens computes them with the sort)
-  const uint4* bal_plan;
 };
 static_assert(sizeof(ScoreArgs) == 344, "ScoreArgs layout (kernel argument block) changed");
 
@@ -869,24 +868,17 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   // (the host checks), so the head and the tail are different tiles.  Visit v (= the tile
   // ordinal k) -> (tile, first chunk, end chunk), recomputed from blockIdx at each visit's end
   // (nothing of the plan stays live across the column loop)
-  // (ragged batches, bal_plan: the range ends come from the plan and a visit's end chunk is the
-  // tile's own chunk count, c1 = -1 until the tile's lengths are read)
-  const auto bal_ends = [&](int& bs, int& bo, int& be, int& bf) {
-    if (a.bal_plan) {
-      const uint4 p0 = a.bal_plan[blockIdx.x], p1 = a.bal_plan[blockIdx.x + 1];
-      bs = (int)__builtin_amdgcn_readfirstlane(p0.x), bo = (int)__builtin_amdgcn_readfirstlane(p0.y);
-      be = (int)__builtin_amdgcn_readfirstlane(p1.x), bf = (int)__builtin_amdgcn_readfirstlane(p1.y);
-      return;
-    }
-    const int bK = (int)a.bal_K;
-    const uint64_t at = (uint64_t)ntiles * (uint64_t)bK;
-    const uint64_t A0 = at * blockIdx.x / G, A1 = at * (blockIdx.x + 1) / G;
-    bs = (int)(A0 / bK), bo = (int)(A0 % bK), be = (int)(A1 / bK), bf = (int)(A1 % bK);
-  };
+  // (a visit's end chunk is the tile's own chunk count, c1 = -1 until the tile's lengths are
+  // read; the plan is read once, into SGPRs: a global load at every visit's end stalls the wave)
+  int bs = 0, bo = 0, be = 0, bf = 0;
+  if constexpr (BAL) {
+    const uint4 p0 = a.bal_plan[blockIdx.x], p1 = a.bal_plan[blockIdx.x + 1];
+    bs = (int)__builtin_amdgcn_readfirstlane(p0.x), bo = (int)__builtin_amdgcn_readfirstlane(p0.y);
+    be = (int)__builtin_amdgcn_readfirstlane(p1.x), bf = (int)__builtin_amdgcn_readfirstlane(p1.y);
+    total = (int)__builtin_amdgcn_readfirstlane(p1.z - p0.z);
+  }
   const auto bal_visit = [&](int v, int& t, int& c0, int& c1) {
-    const int bK = a.bal_plan ? -1 : (int)a.bal_K;
-    int bs, bo, be, bf;
-    bal_ends(bs, bo, be, bf);
+    const int bK = -1;
     const int bfirst = bo ? bs + 1 : bs;
     const int hh = bf > 0 ? 1 : 0;
     if (v < hh) {
@@ -903,13 +895,6 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     c1 = __builtin_amdgcn_readfirstlane(c1);
   };
   if constexpr (BAL) {
-    if (a.bal_plan) {
-      total = (int)__builtin_amdgcn_readfirstlane(a.bal_plan[blockIdx.x + 1].z -
-                                                  a.bal_plan[blockIdx.x].z);
-    } else {
-      const uint64_t at = (uint64_t)ntiles * (uint64_t)a.bal_K;
-      total = (int)(at * (blockIdx.x + 1) / G - at * blockIdx.x / G);
-    }
   } else if constexpr (STREAM) {
     total = (int)blockIdx.x < ntiles ? (1 << 30) : 0;
   } else {
@@ -1116,6 +1101,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   // bal_flag[0] rather than hanging.
   // (the state addresses go through an opaque copy: loop-invariant, LLVM would otherwise hoist
   // all 2R + 2 of them out of the phase loop, 2 VGPRs each, and spill)
+  int bal_pend = 0;  // BAL: phases until the head's flag goes out (0: none pending)
   const auto bal_store = [&](int g_to) {
     uint32_t* sp = a.bal_state + ((size_t)g_to * W + wave) * (2 * R + 2) * 64 + lane;
     asm volatile("" : "+v"(sp));
@@ -1128,12 +1114,21 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     __hip_atomic_store(sp + 2 * R * 64, as_u32(prevUpH), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(sp + (2 * R + 1) * 64, as_u32(best), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
+    bal_pend = 2;  // the flag goes out a phase later, when the stores have long completed
+  };
+  const auto bal_flag_out = [&]() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
-      __hip_atomic_store(a.bal_flag + (size_t)g_to * W + wave, a.bal_gen, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.bal_flag + ((size_t)blockIdx.x + 1) * W + wave, a.bal_gen,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
+#if SWK_STAMPS
+  uint64_t st_bload = 0;  // (measurement builds) cycles in tail state loads
+#endif
   const auto bal_load = [&]() {
+#if SWK_STAMPS
+    const uint64_t sb0 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t* fl = a.bal_flag + (size_t)blockIdx.x * W + wave;
     int it = 0;
     for (; it < (1 << 23); ++it) {
@@ -1156,8 +1151,12 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         __hip_atomic_load(sp + 2 * R * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     best = as_u16x2(
         __hip_atomic_load(sp + (2 * R + 1) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#if SWK_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_bload += __builtin_amdgcn_s_memtime() - sb0;
+#endif
   };
-  (void)bal_store; (void)bal_load;
+  (void)bal_store; (void)bal_load; (void)bal_flag_out;
   // chunk within the current tile, tile ordinal in this workgroup (BAL: the visit ordinal; a
   // first visit is a head or a whole tile, never a tail)
   int c = vc0, k = 0;
@@ -1418,14 +1417,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         for (int jj = 0; jj < C; ++jj) dst[jj * 64] = sink[jj * 64 + lane];
       }
       if (last) {
-        int bfh = 0;  // BAL: the first visit is a head when the range ends inside a tile
-        if constexpr (BAL) {
-          if (k == 0) {
-            int x0, x1, x2;
-            bal_ends(x0, x1, x2, bfh);
-          }
-        }
-        if (BAL && bfh > 0) {  // BAL: a head visit ends: hand its state over
+        // BAL: the first visit is a head when the range ends inside a tile
+        if (BAL && k == 0 && bf > 0) {  // BAL: a head visit ends: hand its state over
           bal_store((int)blockIdx.x + 1);
         } else {  // this wave's part of tile k is done
         uint32_t* bs = bestsh + (k % W) * SWB_TILE;
@@ -1495,6 +1488,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         ++c;
       }
     }
+    if constexpr (BAL) {
+      if (bal_pend > 0 && --bal_pend == 0) bal_flag_out();
+    }
 #if SWK_STAMPS
     const bool st_own = g >= 0 && g < total;  // (fill / drain phases: all of it to st_idle)
     const uint64_t st_b = __builtin_amdgcn_s_memtime();
@@ -1506,11 +1502,14 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     (st_own ? st_bar : st_idle) += st_p - st_b;
 #endif
   }
+  if constexpr (BAL) {
+    if (bal_pend > 0) bal_flag_out();
+  }
 #if SWK_STAMPS
   // (the non-streamed variants never read tctr: measurement builds pass the buffer there)
   uint64_t* const g_stamps = STREAM ? nullptr : reinterpret_cast<uint64_t*>(a.tctr);
   if (lane == 0 && g_stamps) {
-    uint64_t* o = g_stamps + ((size_t)blockIdx.x * 16 + wave) * 8;
+    uint64_t* o = g_stamps + ((size_t)blockIdx.x * 16 + wave) * 16;
     unsigned hw = 0;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     o[0] = st_t0;
@@ -1523,6 +1522,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     o[6] = (uint64_t)total;
     o[7] = (uint64_t)(xcc & 15);
+    o[8] = st_bload;
   }
 #endif
 }
@@ -2797,17 +2797,18 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
 
 #if SWK_STAMPS
 // (measurement builds) per-wave phase timing of the next tile-kernel launches into p:
-// [block][16 waves][8] u64 = entry, exit, active, fill/drain, barrier cycles, HW_ID, chunks, XCC
+// [block][16 waves][16] u64 = entry, exit, active, fill/drain, barrier cycles, HW_ID, chunks,
+// XCC, tail state load cycles
 extern "C" void swk_set_stamps(void* p) { swk::g_stamps_host = static_cast<uint64_t*>(p); }
 #endif
 
 // Balanced chunk ranges (ScoreArgs.bal_*) for the DNA merged f16 pair-table kernel (the
-// headline shape): a uniform batch of `ntiles` tiles of K chunks, codes one byte each (or
-// ustride / ulen), one query segment of W <= 4 waves.  swk_bal_slots gives the grid (every
-// resident slot); the host sizes bal_state ((grid + 1) x W x (2R + 2) x 64 words) and bal_flag
-// ((grid + 1) x W words, zeroed once; bal_flag[0] counts poll time-outs).  A ragged batch
-// visited longest first through the device sort's permutation (idx / nidx / ident) passes the
-// sort's plan (swk_sort_lens with the same grid) instead of K.
+// headline shape): codes one byte each (or ustride / ulen), one query segment of W <= 4 waves.
+// swk_bal_slots gives the grid (every resident slot); the host sizes bal_state ((grid + 1) x W
+// x (2R + 2) x 64 words) and bal_flag ((grid + 1) x W words, zeroed once; bal_flag[0] counts
+// poll time-outs).  plan: grid + 1 entries {tile, chunk, chunk index} (swk_bal_plan_uniform for
+// a uniform batch; a ragged batch visited longest first through the device sort's permutation
+// idx / nidx / ident passes the sort's, swk_sort_lens with the same grid).
 extern "C" unsigned swk_bal_slots(int W, uint32_t PS) {
   auto fn = &swk::score_kernel<32, 4, false, false, false, true, true, false, false, 8, true>;
   static bool attr_set = false;
@@ -2829,14 +2830,12 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
                                           uint32_t PS, uint32_t pad, int W, int32_t* scores,
                                           uint32_t pS1, uint32_t pS2, uint32_t ulen,
-                                          uint32_t ustride, uint32_t K, uint32_t* flag,
-                                          uint32_t* state, uint32_t gen, unsigned grid,
-                                          const uint32_t* idx, const uint32_t* nidx,
-                                          const uint32_t* ident, const void* plan,
-                                          hipStream_t st) {
+                                          uint32_t ustride, uint32_t* flag, uint32_t* state,
+                                          uint32_t gen, unsigned grid, const uint32_t* idx,
+                                          const uint32_t* nidx, const uint32_t* ident,
+                                          const void* plan, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (W > 4 || !flag || !state || (plan ? false : K == 0) || (idx && !nidx))
-    return hipErrorInvalidValue;
+  if (W > 4 || !flag || !state || !plan || (idx && !nidx)) return hipErrorInvalidValue;
   swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                    O,    E,    PS,   pad, scores, nullptr, nullptr, 0u, 0u, (uint32_t)SWK_PACK_BYTES,
                    idx, nidx, 0u, ident, pS1, pS2,
@@ -2847,7 +2846,6 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
   a.nq = 1;
   a.bal_flag = flag;
   a.bal_state = state;
-  a.bal_K = plan ? 0u : K;
   a.bal_gen = gen;
   a.bal_plan = static_cast<const uint4*>(plan);
   return swk::launch_score<32, 4, false, false, false, true, true, false, false, 8, true>(

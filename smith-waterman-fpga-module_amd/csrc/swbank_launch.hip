@@ -165,9 +165,10 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       if (sforce >= 0) T = std::min(pairs, (size_t)sforce);
       else if (pairs >= units && pairs % units <= units / 2) T = pairs % units;
       const int pforce = env_int("SWBANK_WAVE_SPLIT_P", 0);
-      // two pairs per wave (f16): a tail of at most SIMDs / 8 pairs runs as 8 segments of 64
-      // rows, one wave each on its own SIMD, handed on through global memory
-      const bool seg8 = half && b->sK[2] == 1 && T && (pforce == 8 || (!pforce && 8 * T <= simds));
+      // two pairs per wave (f16), SWBANK_WAVE_SPLIT_P=8 only: the tail as 8 segments of 64 rows,
+      // one wave each on its own SIMD, handed on through global memory (measured 12 % slower
+      // than P = 4 on configs[4])
+      const bool seg8 = half && b->sK[2] == 1 && T && pforce == 8;
       const int i = pforce == 2 ? 0 : pforce == 4 ? 1 : (4 * T <= simds ? 1 : 0);
       if (seg8) {
         HIPOK(b, b->sring.reserve(std::max<size_t>(1, T * 7 * (size_t)ecols)));
@@ -258,7 +259,10 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       }
       scr = b->dsort.p;
     }
-    if (rbal_grid) HIPOK(b, b->bal_plan.reserve((size_t)(rbal_grid + 1) * 4));
+    if (rbal_grid) {
+      HIPOK(b, b->bal_plan.reserve((size_t)(rbal_grid + 1) * 4));
+      b->bal_key[0] = 0;  // the uniform plan is overwritten
+    }
     HIPOK(b, swk_sort_lens(d_lens, n, max_len, order, order + n, order + n + 1, scr, st,
                            rbal_grid ? b->bal_plan.p : nullptr, rbal_grid));
     ++b->ctr.device_sorts;
@@ -327,7 +331,8 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       const bool rbal = pass == 0 && rbal_grid && perm && idx == perm && span == n;
       if (rbal || (pass == 0 && f16 && use_pair && !gotoh && nseg == 1 && !idx && wait_prev &&
                    packed == SWK_PACK_BYTES && min_len == max_len && max_len > 0 && span == n &&
-                   !opt16 && b->R == 32 && b->segs[0].W <= 4 && env_int("SWBANK_BAL", 1) != 0)) {
+                   ntiles * ((max_len + 7) / 8) < (1ull << 31) && !opt16 && b->R == 32 &&
+                   b->segs[0].W <= 4 && env_int("SWBANK_BAL", 1) != 0)) {
         const int Wl = b->segs[0].W;
         const unsigned grid = rbal ? rbal_grid : swk_bal_slots(Wl, b->pair_bytes);
         if (grid && (rbal || ntiles >= 2 * (size_t)grid)) {
@@ -337,12 +342,29 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
             HIPOK(b, b->bal_flag.reserve((size_t)(grid + 1) * Wl));
             HIPOK(b, hipMemsetAsync(b->bal_flag.p, 0, b->bal_flag.cap * 4, st));
           }
-          const uint32_t K = (max_len + 7) / 8;
+          if (!rbal) {  // uniform: workgroup g starts at chunk floor(g x tiles x K / grid)
+            const size_t K = (max_len + 7) / 8;
+            if (b->bal_key[0] != ntiles || b->bal_key[1] != K || b->bal_key[2] != grid) {
+              std::vector<uint32_t>& h = b->bal_plan_host;
+              h.assign((size_t)(grid + 1) * 4, 0u);
+              for (size_t g = 0; g <= grid; ++g) {
+                const size_t A = ntiles * K * g / grid;
+                h[4 * g] = (uint32_t)(A / K);
+                h[4 * g + 1] = (uint32_t)(A % K);
+                h[4 * g + 2] = (uint32_t)A;
+              }
+              HIPOK(b, b->bal_plan.reserve(h.size()));
+              HIPOK(b, hipMemcpyAsync(b->bal_plan.p, h.data(), h.size() * 4,
+                                      hipMemcpyHostToDevice, st));
+              b->bal_key[0] = ntiles;
+              b->bal_key[1] = K;
+              b->bal_key[2] = grid;
+            }
+          }
           HIPOK(b, swk_launch_pair_bal(res, offs, lens, np, b->qpair.p, b->nv16, b->S, b->O, b->E,
                                        b->pair_bytes, b->pad, Wl, scores, b->pS1, b->pS2, ulen,
-                                       ustride, rbal ? 0u : K, b->bal_flag.p, b->bal_state.p,
-                                       ++b->bal_gen, grid, idx, nidx, ident,
-                                       rbal ? b->bal_plan.p : nullptr, st));
+                                       ustride, b->bal_flag.p, b->bal_state.p, ++b->bal_gen, grid,
+                                       idx, nidx, ident, b->bal_plan.p, st));
           ++b->ctr.balanced_calls;
           const size_t L = strlen(b->last_kernel);
           snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " balanced grid=%u", grid);
