@@ -41,11 +41,38 @@
 // register copies; a two-copy chunk spills)
 #define SWK_TRIM 0
 #endif
+#ifndef SWK_PRIO_ROT
+// Rotating wave priorities in the persistent tile kernel: the SIMD issues from the oldest ready
+// wave first, so of the 4 resident workgroups of a CU the first dispatched ran ahead and
+// finished at 37 % of the kernel, and the last one ran alone on its CU for the final 22 %
+// (stamps).  Each workgroup takes priority (time / 2^SWK_PRIO_SHIFT + q) mod 4, q its
+// quarter of the grid (the dispatcher puts block i, i + CUs, ... on one CU), so every resident
+// workgroup holds each priority level for the same share of time.
+#define SWK_PRIO_ROT 1
+#endif
+#ifndef SWK_PRIO_SHIFT
+#define SWK_PRIO_SHIFT 19
+#endif
 #ifndef SWK_STAMPS
 #define SWK_STAMPS 0  // measurement builds: per-wave phase timing of the tile kernel (swk_set_stamps)
 #endif
 
 namespace swk {
+
+#if SWK_PRIO_ROT
+// (SWK_PRIO_ROT) the wave's issue priority for now: (time / 2^SWK_PRIO_SHIFT + q) mod 4, set when
+// it changes (s_setprio takes an immediate)
+__device__ __forceinline__ void prio_rotate(uint32_t q, uint32_t& prio) {
+  const uint32_t pr = ((uint32_t)(__builtin_amdgcn_s_memtime() >> SWK_PRIO_SHIFT) + q) & 3u;
+  if (pr != prio) {
+    prio = pr;
+    if (pr == 0) __builtin_amdgcn_s_setprio(0);
+    else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(3);
+  }
+}
+#endif
 
 #if SWK_STAMPS
 static uint64_t* g_stamps_host = nullptr;  // the buffer launch_score hands the tile kernel
@@ -1162,6 +1189,10 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   int c = vc0, k = 0;
   int nch_n = 1, nfull_n = 0, ncl_n = C;  // the next tile's chunk counts
   uint32_t packed_n = packed;  // STREAM: the next tile's code layout
+#if SWK_PRIO_ROT
+  const uint32_t prq = (uint32_t)((blockIdx.x * 4ull) / gridDim.x);
+  uint32_t prio = 4;  // (none set yet)
+#endif
 #if SWK_STAMPS
   // (measurement builds only) per wave: kernel entry / exit, cycles in active phases (the
   // column work), in fill/drain phases (no chunk of its own) and in the per-phase barrier
@@ -1171,6 +1202,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   for (int ph = 0;; ++ph) {
     if constexpr (STREAM) total = __builtin_amdgcn_readfirstlane(sq[W]);
     if (ph >= total + W - 1) break;
+#if SWK_PRIO_ROT
+    if (W <= 4) prio_rotate(prq, prio);  // (a 16-wave workgroup has its CU alone)
+#endif
     const int g = ph - wave;
     if (g >= 0 && g < total) {
       const uint2 clo = rlo, chi = rhi;
@@ -2398,9 +2432,17 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   // of steps from an even t never wraps, so one address per pair and immediate offsets.
   // SWK_HALF_UNROLL: steps per loop iteration (2 or 4)
   const uint32_t* rp = ring_l;
+#if SWK_PRIO_ROT
+  // (the resident main waves of a SIMD come from blocks a quarter of the grid apart)
+  const uint32_t prq = (uint32_t)((blockIdx.x * 4ull) / gridDim.x);
+  uint32_t prio = 4;
+#endif
   const auto step = [&](const int t, const bool even) __attribute__((always_inline)) {
     // the next 32 columns go in before they are read (AHEAD: two steps before)
     if ((AHEAD ? even : !even) && (t & 31) == (AHEAD ? 30 : 31)) {
+#if SWK_PRIO_ROT
+      prio_rotate(prq, prio);
+#endif
       ring_write(ncode);
       // (t through an opaque copy: no per-step pointer increments for these loads)
       uint32_t tt = (uint32_t)t;
