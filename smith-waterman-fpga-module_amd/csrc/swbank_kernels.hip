@@ -47,11 +47,13 @@
 // finished at 37 % of the kernel, and the last one ran alone on its CU for the final 22 %
 // (stamps).  Each workgroup takes priority (time / 2^SWK_PRIO_SHIFT + q) mod 4, q its
 // quarter of the grid (the dispatcher puts block i, i + CUs, ... on one CU), so every resident
-// workgroup holds each priority level for the same share of time.
+// workgroup holds each priority level for the same share of time.  Period: 2^18 s_memtime
+// ticks (~0.11 ms, ~10 phases of the headline); measured 2^14..2^22.  (The
+// two-pairs protein kernel measured 2 % slower with it: not used there.)
 #define SWK_PRIO_ROT 1
 #endif
 #ifndef SWK_PRIO_SHIFT
-#define SWK_PRIO_SHIFT 19
+#define SWK_PRIO_SHIFT 18
 #endif
 #ifndef SWK_STAMPS
 #define SWK_STAMPS 0  // measurement builds: per-wave phase timing of the tile kernel (swk_set_stamps)
@@ -2432,17 +2434,9 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   // of steps from an even t never wraps, so one address per pair and immediate offsets.
   // SWK_HALF_UNROLL: steps per loop iteration (2 or 4)
   const uint32_t* rp = ring_l;
-#if SWK_PRIO_ROT
-  // (the resident main waves of a SIMD come from blocks a quarter of the grid apart)
-  const uint32_t prq = (uint32_t)((blockIdx.x * 4ull) / gridDim.x);
-  uint32_t prio = 4;
-#endif
   const auto step = [&](const int t, const bool even) __attribute__((always_inline)) {
     // the next 32 columns go in before they are read (AHEAD: two steps before)
     if ((AHEAD ? even : !even) && (t & 31) == (AHEAD ? 30 : 31)) {
-#if SWK_PRIO_ROT
-      prio_rotate(prq, prio);
-#endif
       ring_write(ncode);
       // (t through an opaque copy: no per-step pointer increments for these loads)
       uint32_t tt = (uint32_t)t;
