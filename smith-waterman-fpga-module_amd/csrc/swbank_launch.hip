@@ -234,7 +234,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   if (dsort && !sort_out && !use_wave && !perm && use_f16 && use_pair && !gotoh && nseg == 1 &&
       wait_prev && packed == SWK_PACK_BYTES && min_len < max_len && max_len < 2048 && !opt16 &&
       b->R == 32 && b->segs[0].W <= 4 && n <= 0xFFFFFFFFull && env_int("SWBANK_DSORT", 1) != 0 &&
-      env_int("SWBANK_BAL", 1) != 0 && env_int("SWBANK_BAL_RAGGED", 0) != 0 &&
+      env_int("SWBANK_BAL", 1) != 0 && env_int("SWBANK_BAL_RAGGED", 1) != 0 &&
       !one_len_bin(min_len, max_len)) {
     const unsigned grid = swk_bal_slots(b->segs[0].W, b->pair_bytes);
     const size_t kmin = std::max<uint32_t>(1u, (min_len + 7) / 8), kmax = (max_len + 7) / 8;
