@@ -49,13 +49,10 @@
 // quarter of the grid (the dispatcher puts block i, i + CUs, ... on one CU), so every resident
 // workgroup holds each priority level for the same share of time.  Period: 2^18 s_memtime
 // ticks (~0.11 ms, ~10 phases of the headline); measured 2^14..2^22.  (The
-// two-pairs protein kernel measured 2 % slower with it: not used there.)
+// two-pairs protein kernel: -2 % with it, and within +-0.5 % with its split-tail waves on top
+// and the 3 main waves rotating over 3 levels: not used there.  Priorities from each
+// workgroup's progress against its CU's others, published per phase: 0.2-2 % below.)
 #define SWK_PRIO_ROT 1
-#endif
-#ifndef SWK_PRIO_WAVE
-// (A/B build) the two-pairs protein kernel: split-tail waves at the top priority, the 3 main
-// waves of a SIMD rotating over levels 0-2 (time / 2^SWK_PRIO_SHIFT + q) mod 3
-#define SWK_PRIO_WAVE 0
 #endif
 #ifndef SWK_PRIO_SHIFT
 #define SWK_PRIO_SHIFT 18
@@ -2439,27 +2436,9 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   // of steps from an even t never wraps, so one address per pair and immediate offsets.
   // SWK_HALF_UNROLL: steps per loop iteration (2 or 4)
   const uint32_t* rp = ring_l;
-#if SWK_PRIO_WAVE
-  // (a SIMD's 3 main waves come from main blocks a third of them apart)
-  const uint32_t mbk = (a.main_pairs + 7) / 8;
-  const uint32_t prq = (uint32_t)(((blockIdx.x - a.split_blocks) * 3ull) / max(mbk, 1u));
-  uint32_t prio = 4;
-#endif
   const auto step = [&](const int t, const bool even) __attribute__((always_inline)) {
     // the next 32 columns go in before they are read (AHEAD: two steps before)
     if ((AHEAD ? even : !even) && (t & 31) == (AHEAD ? 30 : 31)) {
-#if SWK_PRIO_WAVE
-      {
-        const uint32_t pr =
-            ((uint32_t)(__builtin_amdgcn_s_memtime() >> SWK_PRIO_SHIFT) + prq) % 3u;
-        if (pr != prio) {
-          prio = pr;
-          if (pr == 0) __builtin_amdgcn_s_setprio(0);
-          else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-          else __builtin_amdgcn_s_setprio(2);
-        }
-      }
-#endif
       ring_write(ncode);
       // (t through an opaque copy: no per-step pointer increments for these loads)
       uint32_t tt = (uint32_t)t;
@@ -2685,9 +2664,6 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
   uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
   const int lane = threadIdx.x & 63;
   if (blockIdx.x < a.split_blocks) {  // block-uniform
-#if SWK_PRIO_WAVE
-    __builtin_amdgcn_s_setprio(3);
-#endif
     if (a.split_P == 4) wave_split_block<2, 4, false, true, GOTOH, true>(a, smem, lane);
     else wave_split_block<4, 2, false, true, GOTOH, true>(a, smem, lane);
     return;
