@@ -57,6 +57,12 @@
 #ifndef SWK_PRIO_SHIFT
 #define SWK_PRIO_SHIFT 18
 #endif
+#ifndef SWK_PRIO_END
+#define SWK_PRIO_END 0
+#endif
+#ifndef SWK_PRIO_END_FRAC
+#define SWK_PRIO_END_FRAC 3
+#endif
 #ifndef SWK_STAMPS
 #define SWK_STAMPS 0  // measurement builds: per-wave phase timing of the tile kernel (swk_set_stamps)
 #endif
@@ -66,8 +72,8 @@ namespace swk {
 #if SWK_PRIO_ROT
 // (SWK_PRIO_ROT) the wave's issue priority for now: (time / 2^SWK_PRIO_SHIFT + q) mod 4, set when
 // it changes (s_setprio takes an immediate)
-__device__ __forceinline__ void prio_rotate(uint32_t q, uint32_t& prio) {
-  const uint32_t pr = ((uint32_t)(__builtin_amdgcn_s_memtime() >> SWK_PRIO_SHIFT) + q) & 3u;
+__device__ __forceinline__ void prio_rotate(uint32_t q, uint32_t& prio, uint32_t shift) {
+  const uint32_t pr = ((uint32_t)(__builtin_amdgcn_s_memtime() >> shift) + q) & 3u;
   if (pr != prio) {
     prio = pr;
     if (pr == 0) __builtin_amdgcn_s_setprio(0);
@@ -1207,7 +1213,12 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     if constexpr (STREAM) total = __builtin_amdgcn_readfirstlane(sq[W]);
     if (ph >= total + W - 1) break;
 #if SWK_PRIO_ROT
-    if (W <= 4) prio_rotate(prq, prio);  // (a 16-wave workgroup has its CU alone)
+    // (a 16-wave workgroup has its CU alone; SWK_PRIO_END: the last 1/2^SWK_PRIO_END_FRAC of
+    // the phases rotate 2^SWK_PRIO_END times faster, so the four finish closer together)
+    if (W <= 4)
+      prio_rotate(prq, prio,
+                  SWK_PRIO_END && ph >= total - (total >> SWK_PRIO_END_FRAC)
+                      ? SWK_PRIO_SHIFT - SWK_PRIO_END : SWK_PRIO_SHIFT);
 #endif
     const int g = ph - wave;
     if (g >= 0 && g < total) {
