@@ -48,7 +48,8 @@
 // (stamps).  Each workgroup takes priority (time / 2^SWK_PRIO_SHIFT + q) mod 4, q its
 // quarter of the grid (the dispatcher puts block i, i + CUs, ... on one CU), so every resident
 // workgroup holds each priority level for the same share of time.  Period: 2^18 s_memtime
-// ticks (~0.11 ms, ~10 phases of the headline); measured 2^14..2^22.  (The
+// ticks (~0.11 ms, ~10 phases of the headline), 2^15 over the last 1/16 of a workgroup's
+// phases (+0.1-1.2 %, so the four finish closer); measured 2^14..2^22.  (The
 // two-pairs protein kernel: -2 % with it, and within +-0.5 % with its split-tail waves on top
 // and the 3 main waves rotating over 3 levels: not used there.  Priorities from each
 // workgroup's progress against its CU's others, published per phase: 0.2-2 % below.)
@@ -58,10 +59,13 @@
 #define SWK_PRIO_SHIFT 18
 #endif
 #ifndef SWK_PRIO_END
-#define SWK_PRIO_END 0
+#define SWK_PRIO_END 3  // the last 1/16 of a workgroup's phases rotate 8 times faster
 #endif
 #ifndef SWK_PRIO_END_FRAC
-#define SWK_PRIO_END_FRAC 3
+#define SWK_PRIO_END_FRAC 4
+#endif
+#ifndef SWK_PRIO_STAGE
+#define SWK_PRIO_STAGE 0  // (A/B) 16-wave workgroups: 1 = later stages first, 2 = earlier first
 #endif
 #ifndef SWK_STAMPS
 #define SWK_STAMPS 0  // measurement builds: per-wave phase timing of the tile kernel (swk_set_stamps)
@@ -1219,6 +1223,16 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       prio_rotate(prq, prio,
                   SWK_PRIO_END && ph >= total - (total >> SWK_PRIO_END_FRAC)
                       ? SWK_PRIO_SHIFT - SWK_PRIO_END : SWK_PRIO_SHIFT);
+#if SWK_PRIO_STAGE
+    if (W > 4 && ph == 0) {
+      const int st = (wave * 4) / W;
+      const int pr = SWK_PRIO_STAGE == 1 ? st : 3 - st;
+      if (pr == 0) __builtin_amdgcn_s_setprio(0);
+      else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+      else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(3);
+    }
+#endif
 #endif
     const int g = ph - wave;
     if (g >= 0 && g < total) {
