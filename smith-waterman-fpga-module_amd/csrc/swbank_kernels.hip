@@ -52,7 +52,8 @@
 // phases (+0.1-1.2 %, so the four finish closer); measured 2^14..2^22.  (The
 // two-pairs protein kernel: -2 % with it, and within +-0.5 % with its split-tail waves on top
 // and the 3 main waves rotating over 3 levels: not used there.  Priorities from each
-// workgroup's progress against its CU's others, published per phase: 0.2-2 % below.)
+// workgroup's progress against its CU's others, published per phase: 0.2-2 % below.  16-wave
+// workgroups with later pipeline stages on top: +0.2 %, not kept.)
 #define SWK_PRIO_ROT 1
 #endif
 #ifndef SWK_PRIO_SHIFT
@@ -64,9 +65,7 @@
 #ifndef SWK_PRIO_END_FRAC
 #define SWK_PRIO_END_FRAC 4
 #endif
-#ifndef SWK_PRIO_STAGE
-#define SWK_PRIO_STAGE 0  // (A/B) 16-wave workgroups: 1 = later stages first, 2 = earlier first
-#endif
+
 #ifndef SWK_STAMPS
 #define SWK_STAMPS 0  // measurement builds: per-wave phase timing of the tile kernel (swk_set_stamps)
 #endif
@@ -1219,20 +1218,11 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
 #if SWK_PRIO_ROT
     // (a 16-wave workgroup has its CU alone; SWK_PRIO_END: the last 1/2^SWK_PRIO_END_FRAC of
     // the phases rotate 2^SWK_PRIO_END times faster, so the four finish closer together)
-    if (W <= 4)
+    if (W <= 8)
       prio_rotate(prq, prio,
                   SWK_PRIO_END && ph >= total - (total >> SWK_PRIO_END_FRAC)
                       ? SWK_PRIO_SHIFT - SWK_PRIO_END : SWK_PRIO_SHIFT);
-#if SWK_PRIO_STAGE
-    if (W > 4 && ph == 0) {
-      const int st = (wave * 4) / W;
-      const int pr = SWK_PRIO_STAGE == 1 ? st : 3 - st;
-      if (pr == 0) __builtin_amdgcn_s_setprio(0);
-      else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-      else if (pr == 2) __builtin_amdgcn_s_setprio(2);
-      else __builtin_amdgcn_s_setprio(3);
-    }
-#endif
+
 #endif
     const int g = ph - wave;
     if (g >= 0 && g < total) {
