@@ -35,12 +35,6 @@
 
 #include "swbank_internal.h"
 
-#ifndef SWK_TRIM
-// A/B build: a tile's last chunk stops at its last column holding a code (saves the ragged
-// batches' padding columns, but the per-column test costs the headline ~25 VALU per chunk in
-// register copies; a two-copy chunk spills)
-#define SWK_TRIM 0
-#endif
 #ifndef SWK_PRIO_ROT
 // Rotating wave priorities in the persistent tile kernel: the SIMD issues from the oldest ready
 // wave first, so of the 4 resident workgroups of a CU the first dispatched ran ahead and
@@ -658,11 +652,10 @@ __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t
   return t;
 }
 
-// Chunk counts of a tile (uniform): nch = ceil(max len / C) (>= 1), nfull = min len / C, ncl =
-// the columns of chunk nch - 1 that hold a code of some lane (1..C).
+// Chunk counts of a tile (uniform): nch = ceil(max len / C) (>= 1), nfull = min len / C.
 template <int C = 8>
 __device__ __forceinline__ void tile_chunks(const Lane2& t, size_t tlo, size_t thi, size_t n,
-                                            int& nch, int& nfull, int& ncl) {
+                                            int& nch, int& nfull) {
   uint32_t Lmax = max(t.llo, t.lhi);
   uint32_t Lmin = min(tlo < n ? t.llo : ~0u, thi < n ? t.lhi : ~0u);
 #pragma unroll
@@ -672,7 +665,6 @@ __device__ __forceinline__ void tile_chunks(const Lane2& t, size_t tlo, size_t t
   }
   const int lx = (int)__builtin_amdgcn_readfirstlane(Lmax);
   nch = max(1, (lx + C - 1) / C);
-  ncl = lx == 0 ? C : lx - C * (nch - 1);
   const uint32_t lm = __builtin_amdgcn_readfirstlane(Lmin);
   nfull = lm == ~0u ? 0 : (int)(lm / C);  // no valid lane (a tile past the end): no full loads
 }
@@ -1026,11 +1018,10 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     cur = lane_targets<!MQ>(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen,
                             a.ustride);
   }
-  int nch, nfull, ncl;
+  int nch, nfull;
   tile_chunks<C>(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
-              nfull, ncl);
+              nfull);
   if constexpr (BAL) {  // BAL: nch = the visit's end chunk (a head's last chunk is whole)
-    if (vend >= 0 && vend < nch) ncl = C;
     nch = vend < 0 ? nch : vend;
   }
   const uint32_t S = a.S;
@@ -1200,7 +1191,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   // chunk within the current tile, tile ordinal in this workgroup (BAL: the visit ordinal; a
   // first visit is a head or a whole tile, never a tail)
   int c = vc0, k = 0;
-  int nch_n = 1, nfull_n = 0, ncl_n = C;  // the next tile's chunk counts
+  int nch_n = 1, nfull_n = 0;  // the next tile's chunk counts
   uint32_t packed_n = packed;  // STREAM: the next tile's code layout
 #if SWK_PRIO_ROT
   const uint32_t prq = (uint32_t)((blockIdx.x * 4ull) / gridDim.x);
@@ -1271,8 +1262,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           cur = lane_targets<!MQ>(a.res, a.offs, a.lens, n, ntile, lane, packed, idx, a.ulen,
                                   a.ustride);
         tile_chunks<C>(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
-                    n, nch_n, nfull_n, ncl_n);
-        if (BAL && nvend >= 0 && nvend < nch_n) ncl_n = C;
+                    n, nch_n, nfull_n);
         if (BAL && nvend < 0) nvend = nch_n;
         load_raw<C, !MQ>(cur, nc0, nc0 < nfull_n, a.pad, STREAM ? packed_n : packed, rlo, rhi);
       }
@@ -1289,16 +1279,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       uint2 rv = rin[0];
       ProfLookup16<PROF && F16 ? R : 2> lkq;  // f16 profile: the next column's words
       (void)lkq;
-      // the tile's last chunk stops after its last column holding a code (a tile runs to its
-      // longest lane; every wave stops at the same column, so the ring stays consistent)
-      const int ncols = SWK_TRIM && c + 1 == nch ? ncl : C;
-      bool trimmed = false;
 #pragma unroll
       for (int jj = 0; jj < C; ++jj) {
-        if (SWK_TRIM && jj > 0 && __builtin_expect(jj >= ncols, 0)) {
-          trimmed = true;
-          continue;
-        }
         const u16x2 upH = as_u16x2(rv.x);
         u16x2 upX = as_u16x2(rv.y);
         if (jj + 1 < C) rv = rin[(jj + 1) * istride];  // one column ahead
@@ -1455,15 +1437,6 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         asm volatile("" : "+v"(best));
         rout[jj * ostride] = make_uint2(as_u32(Hl[R - 1]), as_u32(upX));
       }
-      if constexpr (PAIR && SWK_TRIM) {
-        if (trimmed) {  // the next chunk's column 0, read ahead as at a chunk's end
-          acur = pair_addr(rlo.x, rhi.x, 0);
-          pA0 = ld4(acur + 16);
-          pA1 = ld4(acur + 32);
-          pw = ld1(acur + 12);
-        }
-      }
-      (void)trimmed;
       if (seg_out && wave == W - 1) {  // this segment's bottom row -> the next segment
         uint2* dst = a.edge_out + ((size_t)(MQ ? unit : tile) * a.ecols + (size_t)c * C) * 64 + lane;
 #pragma unroll
@@ -1529,7 +1502,6 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         }
         nch = nch_n;
         nfull = nfull_n;
-        ncl = ncl_n;
         c = 0;
         if constexpr (BAL) {
           c = nc0;
