@@ -750,15 +750,15 @@ sw_status prepare_multi(sw_bank* b) {
     }
   }
   // letter-pair tables (DNA merged f16 without the column-0 rule), one per (segment, query):
-  // 256-row segments (8 waves of 32 rows, 4-column chunks, 2 workgroups per CU whose wave
-  // priorities rotate: a 1-kbp query is 4 segments, 3 bottom-row hand-offs through HBM; +10 %
-  // against 512-row segments, one workgroup per CU) unless SWBANK_MQ_PAIR_ROWS=128
-  // (4 waves, 4 workgroups per CU) or 512 (16 waves)
+  // 128-row segments (4 waves of 32 rows, 4-column chunks, 4 workgroups per CU whose wave
+  // priorities rotate: a 1-kbp query is 8 segments, 7 bottom-row hand-offs through HBM; +11 %
+  // against 512-row segments, one workgroup per CU) unless SWBANK_MQ_PAIR_ROWS=256
+  // (8 waves, 2 workgroups per CU) or 512 (16 waves)
   std::vector<uint32_t> tp;
   b->mq_pair_segs = 0;
   if (b->f16 && !b->prof && !b->gotoh() && !b->col0 && A == SW_DNA_ALPHA &&
       env_int("SWBANK_MQ_PAIR", 1) != 0) {
-    const int want = env_int("SWBANK_MQ_PAIR_ROWS", 256);
+    const int want = env_int("SWBANK_MQ_PAIR_ROWS", 128);
     const uint32_t NR = want == 128 ? 128 : want == 256 ? 256 : 512;
     b->mq_pair_rows = (int)NR;
     pair_strides(NR, b->mq_pS1, b->mq_pS2);
