@@ -16,7 +16,8 @@ Other workloads (``--workload``), same JSON line:
                  longest first on the device.
   reads150x1k    configs[3]: per GPU ``--reads`` synthetic 150-bp reads x a fixed slice of
                  ``--slice`` 1-kbp targets (every read x every target of the slice); each
-                 1-kbp target is the bank query (2 segments of 512 rows), the reads the batch.
+                 1-kbp target is the bank query (a query set in 128-row segments), the reads
+                 the batch.
   protein512x1k  configs[4]: a 512-aa query x ``--ptargets`` 1-kaa targets per GPU,
                  BLOSUM62, gap -11/-1, Gotoh (ssearch36 semantics), uniform 20-letter residues.
 
@@ -47,7 +48,8 @@ HBM_PEAK_GBS = 8000.0
 # The path is bound by VALU issue, not HBM or MFMA.
 # Ceiling (roofline.peak): a SIMD issues one wave64 VALU instruction per 4 cycles (packed
 # 16-bit ops, v_perm_b32 and 32-bit integer ops alike: scripts/ubench/valu_rate.hip measured
-# 0.244-0.27 wave-instr/SIMD/cycle), and one packed 16-bit instruction advances one query row
+# 0.221-0.231 for packed f16 and 0.245-0.248 for 32-bit ops at 4 waves/SIMD, 0.374 for f32:
+# profiles/r04/valu_rate.jsonl), and one packed 16-bit instruction advances one query row
 # for 64 lanes x 2 targets = 128 cells.  The fewest such instructions per row the recurrence
 # needs on gfx950 (DESIGN §6 derivation: every add is its own instruction because no
 # instruction fuses an add into a max; v_pk_maximum3_f16 takes 3 inputs; the add's clamp is
@@ -196,7 +198,7 @@ class Workload:
             self.name = f"reads150x{n}x1k{args.slice}"
             self.desc = (f"{n} synthetic 150-bp reads per GPU x a slice of {args.slice} "
                          f"synthetic 1-kbp targets (BASELINE configs[3]); target = bank query "
-                         f"(2 x 512-row segments), reads = batch")
+                         f"(a query set in 128-row segments), reads = batch")
         elif w == "protein512x1k":
             n, L = args.ptargets, 1000
             self.set_uniform(make_codes(3000 + rank, n, L, 20))

@@ -7,6 +7,8 @@ HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come from 
 coalesced stream on gfx950, so it is doubled (our 8-byte-per-lane code loads are not a
 calibrated width: the doubled figure is an estimate, within ~10% of the algorithmic bytes).
 usage: python scripts/collect_profiles.py ROUND PROF_DIR PMC_DIR WORKLOAD [KERNEL [SUFFIX]]
+  WORKLOAD: bench.py's workload name (its JSON line's traffic lookup), e.g. query100x1021952x128,
+            query100xragged1021952, reads150x131072x1k16, protein512x12500x1k
   KERNEL: substring of the kernel name the counters are averaged over (default score_kernel)
   SUFFIX: file suffix for a second workload (kernel_stats_SUFFIX.csv, pmc_SUFFIX_*.csv,
           pmc_summary_WORKLOAD.json); without it the files are the headline's
