@@ -60,6 +60,8 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t pS2, uint32_t ulen, uint32_t ustride, uint32_t nq,
                                        uint32_t qwords, size_t sstride, hipStream_t st);
 extern "C" unsigned swk_bal_slots(int W, uint32_t PS);
+extern "C" hipError_t swk_bal_plan_uniform(void* plan, uint32_t ntiles, uint32_t K, uint32_t G,
+                                           hipStream_t st);
 extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* offs,
                                           const uint32_t* lens, size_t n, const uint32_t* qtab,
                                           uint32_t nv, uint32_t S, uint32_t O, uint32_t E,
@@ -491,10 +493,9 @@ struct sw_bank {
   // generation the flags are compared with
   DevBuf<uint32_t> bal_state, bal_flag;
   // range starts, 4 words each: a ragged batch's (the device sort writes them per call) or a
-  // uniform batch's (host-computed for bal_key = {tiles, chunks per tile, grid}, kept while the
-  // key holds; bal_key[0] = 0 when the sort overwrote them)
+  // uniform batch's (swk_bal_plan_uniform for bal_key = {tiles, chunks per tile, grid}, kept
+  // while the key holds; bal_key[0] = 0 when the sort overwrote them)
   DevBuf<uint32_t> bal_plan;
-  std::vector<uint32_t> bal_plan_host;
   size_t bal_key[3] = {0, 0, 0};
   uint32_t bal_gen = 0;
   bool peer_ready = false;

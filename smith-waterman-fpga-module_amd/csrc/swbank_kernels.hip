@@ -2834,6 +2834,26 @@ extern "C" void swk_set_stamps(void* p) { swk::g_stamps_host = static_cast<uint6
 // poll time-outs).  plan: grid + 1 entries {tile, chunk, chunk index} (swk_bal_plan_uniform for
 // a uniform batch; a ragged batch visited longest first through the device sort's permutation
 // idx / nidx / ident passes the sort's, swk_sort_lens with the same grid).
+namespace swk {
+__global__ void __launch_bounds__(256) bal_plan_uniform(uint4* plan, uint32_t ntiles, uint32_t K,
+                                                        uint32_t G) {
+  for (uint32_t g = threadIdx.x; g <= G; g += blockDim.x) {
+    const uint64_t A = (uint64_t)ntiles * K * g / G;
+    plan[g] = make_uint4((uint32_t)(A / K), (uint32_t)(A % K), (uint32_t)A, 0u);
+  }
+}
+}  // namespace swk
+
+// The plan of a uniform batch (ntiles tiles of K chunks, G workgroups): entry g = {tile, chunk,
+// chunk index} of chunk floor(g ntiles K / G), g = 0..G (ntiles K < 2^31).
+extern "C" hipError_t swk_bal_plan_uniform(void* plan, uint32_t ntiles, uint32_t K, uint32_t G,
+                                           hipStream_t st) {
+  if (!plan || K == 0 || G == 0 || (uint64_t)ntiles * K >= (1ull << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(swk::bal_plan_uniform, dim3(1), dim3(256), 0, st, static_cast<uint4*>(plan),
+                     ntiles, K, G);
+  return hipGetLastError();
+}
+
 extern "C" unsigned swk_bal_slots(int W, uint32_t PS) {
   auto fn = &swk::score_kernel<32, 4, false, false, false, true, true, false, false, 8, true>;
   static bool attr_set = false;

@@ -345,17 +345,9 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
           if (!rbal) {  // uniform: workgroup g starts at chunk floor(g x tiles x K / grid)
             const size_t K = (max_len + 7) / 8;
             if (b->bal_key[0] != ntiles || b->bal_key[1] != K || b->bal_key[2] != grid) {
-              std::vector<uint32_t>& h = b->bal_plan_host;
-              h.assign((size_t)(grid + 1) * 4, 0u);
-              for (size_t g = 0; g <= grid; ++g) {
-                const size_t A = ntiles * K * g / grid;
-                h[4 * g] = (uint32_t)(A / K);
-                h[4 * g + 1] = (uint32_t)(A % K);
-                h[4 * g + 2] = (uint32_t)A;
-              }
-              HIPOK(b, b->bal_plan.reserve(h.size()));
-              HIPOK(b, hipMemcpyAsync(b->bal_plan.p, h.data(), h.size() * 4,
-                                      hipMemcpyHostToDevice, st));
+              HIPOK(b, b->bal_plan.reserve((size_t)(grid + 1) * 4));
+              HIPOK(b, swk_bal_plan_uniform(b->bal_plan.p, (uint32_t)ntiles, (uint32_t)K, grid,
+                                            st));
               b->bal_key[0] = ntiles;
               b->bal_key[1] = K;
               b->bal_key[2] = grid;
