@@ -179,6 +179,8 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->i32scr.release();
   b->dperm.release();
   b->dsort.release();
+  b->dpoffs.release();
+  b->dplens.release();
   b->bal_state.release();
   b->bal_flag.release();
   b->bal_plan.release();
