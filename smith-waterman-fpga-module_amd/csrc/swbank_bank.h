@@ -58,9 +58,7 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        const uint32_t* nidx, uint32_t idx_base,
                                        const uint32_t* ident, int pair, uint32_t pS1,
                                        uint32_t pS2, uint32_t ulen, uint32_t ustride, uint32_t nq,
-                                       uint32_t qwords, size_t sstride, hipStream_t st,
-                                       const uint64_t* poffs = nullptr,
-                                       const uint32_t* plens = nullptr);
+                                       uint32_t qwords, size_t sstride, hipStream_t st);
 extern "C" unsigned swk_bal_slots(int W, uint32_t PS);
 extern "C" hipError_t swk_bal_plan_uniform(void* plan, uint32_t ntiles, uint32_t K, uint32_t G,
                                            hipStream_t st);
@@ -72,9 +70,7 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           uint32_t ustride, uint32_t* flag, uint32_t* state,
                                           uint32_t gen, unsigned grid, const uint32_t* idx,
                                           const uint32_t* nidx, const uint32_t* ident,
-                                          const void* plan, hipStream_t st,
-                                          const uint64_t* poffs = nullptr,
-                                          const uint32_t* plens = nullptr);
+                                          const void* plan, hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
                                    hipStream_t st);
@@ -85,8 +81,7 @@ extern "C" hipError_t swk_best_finalize(const unsigned long long* key, const uin
 extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max_len,
                                     uint32_t* perm, uint32_t* perm_n, uint32_t* ident,
                                     uint32_t* scratch, hipStream_t st, void* plan = nullptr,
-                                    unsigned G = 0, const uint64_t* offs = nullptr,
-                                    uint64_t* poffs = nullptr, uint32_t* plens = nullptr);
+                                    unsigned G = 0);
 extern "C" size_t swk_sort_scratch_bytes(void);
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
                                     uint32_t* idx, uint32_t* count, hipStream_t st);
@@ -509,8 +504,6 @@ struct sw_bank {
   // on-device longest-first order of a ragged device batch (sw_score_batch_device):
   // dperm = visiting order + count, dsort = histogram / scan scratch
   DevBuf<uint32_t> dperm, dsort;
-  DevBuf<uint64_t> dpoffs;  // the device sort's copies of offsets / lengths in its order
-  DevBuf<uint32_t> dplens;
   bool is_multi() const { return !kids.empty(); }
   bool gotoh() const { return cfg.gap_model == SW_GAP_GOTOH; }
 

@@ -179,8 +179,6 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->i32scr.release();
   b->dperm.release();
   b->dsort.release();
-  b->dpoffs.release();
-  b->dplens.release();
   b->bal_state.release();
   b->bal_flag.release();
   b->bal_plan.release();

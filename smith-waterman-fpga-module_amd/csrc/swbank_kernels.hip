@@ -766,13 +766,8 @@ struct ScoreArgs {
   // poll time-outs.
   uint32_t* tail_prog;
   uint32_t tail_pairs, tail_cols;
-  // device sort with metadata (poffs != nullptr): offs / lens already in the sort's order
-  // (poffs[k] = offs[idx[k]], plens[k] = lens[idx[k]]), so tiles load them directly and idx
-  // only maps scores back (unless *ident: then the sort wrote nothing and offs / lens hold)
-  const uint64_t* poffs;
-  const uint32_t* plens;
 };
-static_assert(sizeof(ScoreArgs) == 360, "ScoreArgs layout (kernel argument block) changed");
+static_assert(sizeof(ScoreArgs) == 344, "ScoreArgs layout (kernel argument block) changed");
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) void* glob_void_ptr;
@@ -885,16 +880,6 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   size_t n = a.n;
   const uint32_t* idx = a.idx;
   if (idx && a.ident && __builtin_amdgcn_readfirstlane(*a.ident)) idx = nullptr;
-  // the target metadata the tiles load, and the index they load it through (lidx): the
-  // sort's permuted copies need none
-  const uint64_t* toffs = a.offs;
-  const uint32_t* tlens = a.lens;
-  const uint32_t* lidx = idx;
-  if (idx && a.poffs) {
-    toffs = a.poffs;
-    tlens = a.plens;
-    lidx = nullptr;
-  }
   if (idx) {
     const uint32_t cnt = __builtin_amdgcn_readfirstlane(*a.nidx);
     n = cnt > a.idx_base ? min(a.n, (size_t)(cnt - a.idx_base)) : 0;
@@ -946,8 +931,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     total = (int)blockIdx.x < ntiles ? (1 << 30) : 0;
   } else {
     for (int u = blockIdx.x; u < nunits; u += G)  // (the unit's tile: see the MQ order below)
-      total += tile_nch<C>(a.res, tlens, n, !MQ ? u : PAIR ? u / (int)a.nq : u % ntiles, lane,
-                        packed, lidx, a.ulen, a.ustride);
+      total += tile_nch<C>(a.res, a.lens, n, !MQ ? u : PAIR ? u / (int)a.nq : u % ntiles, lane,
+                        packed, idx, a.ulen, a.ustride);
   }
   // STREAM: the chunk of this wave's current tile (tiles only grow), its first tile, target
   // count, code offset and layout
@@ -1030,7 +1015,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     wperm = cperm;
     wst0 = st0;
   } else {
-    cur = lane_targets<!MQ>(a.res, toffs, tlens, n, tile, lane, packed, lidx, a.ulen,
+    cur = lane_targets<!MQ>(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen,
                             a.ustride);
   }
   int nch, nfull;
@@ -1274,7 +1259,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       } else if (nunit < nunits) {  // first chunk of the next tile
         if constexpr (STREAM) cur = stream_tile(ntile, packed_n);
         else
-          cur = lane_targets<!MQ>(a.res, toffs, tlens, n, ntile, lane, packed, lidx, a.ulen,
+          cur = lane_targets<!MQ>(a.res, a.offs, a.lens, n, ntile, lane, packed, idx, a.ulen,
                                   a.ustride);
         tile_chunks<C>(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
                     n, nch_n, nfull_n);
@@ -2774,10 +2759,8 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        const uint32_t* ident, int pair, uint32_t pS1,
                                        uint32_t pS2, uint32_t ulen, uint32_t ustride,
                                        uint32_t nq, uint32_t qwords, size_t sstride,
-                                       hipStream_t st, const uint64_t* poffs,
-                                       const uint32_t* plens) {
+                                       hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if ((poffs != nullptr) != (plens != nullptr) || (poffs && !idx)) return hipErrorInvalidValue;
   swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                    O,    E,    PS,   pad, scores, static_cast<const uint2*>(edge_in),
                    static_cast<uint2*>(edge_out), ecols, (uint32_t)accum, (uint32_t)packed,
@@ -2789,8 +2772,6 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
   a.nq = nq;
   a.qwords = qwords;
   a.sstride = sstride;
-  a.poffs = poffs;
-  a.plens = plens;
   const uint32_t prof_bytes = (pad + 1) * PS;
   if (nq > 1 && pair) {  // several queries, pair tables (PS = one table's bytes)
     // more than 4 waves (a 512-row table): 4-column chunks, so the ring fits beside the table;
@@ -2897,10 +2878,8 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           uint32_t ustride, uint32_t* flag, uint32_t* state,
                                           uint32_t gen, unsigned grid, const uint32_t* idx,
                                           const uint32_t* nidx, const uint32_t* ident,
-                                          const void* plan, hipStream_t st,
-                                          const uint64_t* poffs, const uint32_t* plens) {
+                                          const void* plan, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if ((poffs != nullptr) != (plens != nullptr) || (poffs && !idx)) return hipErrorInvalidValue;
   if (W > 4 || !flag || !state || !plan || (idx && !nidx)) return hipErrorInvalidValue;
   swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                    O,    E,    PS,   pad, scores, nullptr, nullptr, 0u, 0u, (uint32_t)SWK_PACK_BYTES,
@@ -2914,8 +2893,6 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
   a.bal_state = state;
   a.bal_gen = gen;
   a.bal_plan = static_cast<const uint4*>(plan);
-  a.poffs = poffs;
-  a.plens = plens;
   return swk::launch_score<32, 4, false, false, false, true, true, false, false, 8, true>(
       a, W, 0, st, grid);
 }
@@ -3455,21 +3432,18 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_hist_scan(const uint32_t* len
 __global__ void __launch_bounds__(SORT_BLOCK) sort_scatter(const uint32_t* lens, size_t n,
                                                            uint32_t max_len, uint32_t shift,
                                                            uint32_t nb, uint32_t* offs,
-                                                           uint32_t* perm, const uint32_t* ident,
-                                                           const uint64_t* toffs, uint64_t* poffs,
-                                                           uint32_t* plens) {
+                                                           uint32_t* perm, const uint32_t* ident) {
   if (__builtin_amdgcn_readfirstlane(*ident)) return;  // one length bin: order unchanged
   __shared__ uint32_t h[SORT_BINS];
   __shared__ int last;
   for (uint32_t i = threadIdx.x; i < nb; i += SORT_BLOCK) h[i] = 0;
   __syncthreads();
   const size_t base = (size_t)blockIdx.x * SORT_BLOCK * SORT_ITEMS;
-  uint32_t bin[SORT_ITEMS], slot[SORT_ITEMS], len[SORT_ITEMS];
+  uint32_t bin[SORT_ITEMS], slot[SORT_ITEMS];
 #pragma unroll
   for (int it = 0; it < SORT_ITEMS; ++it) {
     const size_t k = base + (size_t)it * SORT_BLOCK + threadIdx.x;
-    len[it] = k < n ? lens[k] : 0u;
-    bin[it] = k < n ? sort_bin(len[it], max_len, shift) : 0u;
+    bin[it] = k < n ? sort_bin(lens[k], max_len, shift) : 0u;
     slot[it] = wave_bin_add(h, bin[it], k < n);
   }
   __syncthreads();
@@ -3480,13 +3454,7 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_scatter(const uint32_t* lens,
   for (int it = 0; it < SORT_ITEMS; ++it) {
     const size_t k = base + (size_t)it * SORT_BLOCK + threadIdx.x;
     const uint32_t pos = h[bin[it]] + slot[it];
-    if (k < n && pos < n) {
-      perm[pos] = (uint32_t)k;
-      if (poffs) {  // the metadata in sorted order (the tiles then load it without perm)
-        poffs[pos] = toffs[k];
-        plens[pos] = len[it];
-      }
-    }
+    if (k < n && pos < n) perm[pos] = (uint32_t)k;
   }
   // the last block zeroes the offsets and the counters for the next call (every block's
   // offset atomics returned before its counter add; the zeros reach the next call's kernels
@@ -3503,24 +3471,21 @@ __global__ void __launch_bounds__(SORT_BLOCK) sort_scatter(const uint32_t* lens,
 
 // perm[0, n) <- target numbers longest first, *perm_n <- n, *ident <- 1 when the lengths
 // share one bin (perm then left unwritten: visit in input order); scratch:
-// swk_sort_scratch_bytes(), zero on entry and on return.  offs / poffs / plens (optional):
-// poffs[k] <- offs[perm[k]], plens[k] <- lens[perm[k]] (unwritten when *ident).
+// swk_sort_scratch_bytes(), zero on entry and on return.
 extern "C" hipError_t swk_sort_lens(const uint32_t* lens, size_t n, uint32_t max_len,
                                     uint32_t* perm, uint32_t* perm_n, uint32_t* ident,
-                                    uint32_t* scratch, hipStream_t st, void* plan, unsigned G,
-                                    const uint64_t* offs, uint64_t* poffs, uint32_t* plens) {
+                                    uint32_t* scratch, hipStream_t st, void* plan, unsigned G) {
   if (n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
   uint32_t shift = 0;
   while ((max_len >> shift) >= (uint32_t)swk::SORT_BINS) ++shift;
   const uint32_t nb = (max_len >> shift) + 1;
   if (plan && (shift != 0 || G == 0)) return hipErrorInvalidValue;
-  if ((poffs != nullptr) != (plens != nullptr) || (poffs && !offs)) return hipErrorInvalidValue;
   const unsigned blocks =
       (unsigned)((n + swk::SORT_BLOCK * swk::SORT_ITEMS - 1) / (swk::SORT_BLOCK * swk::SORT_ITEMS));
   hipLaunchKernelGGL(swk::sort_hist_scan, dim3(blocks), dim3(swk::SORT_BLOCK), 0, st, lens, n,
                      max_len, shift, nb, scratch, perm_n, ident, static_cast<uint4*>(plan), G);
   hipLaunchKernelGGL(swk::sort_scatter, dim3(blocks), dim3(swk::SORT_BLOCK), 0, st, lens, n,
-                     max_len, shift, nb, scratch, perm, ident, offs, poffs, plens);
+                     max_len, shift, nb, scratch, perm, ident);
   return hipGetLastError();
 }
 

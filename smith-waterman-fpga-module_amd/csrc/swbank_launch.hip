@@ -226,8 +226,6 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   // A device batch (dsort) visits its targets longest first, sorted on the device, so every
   // tile holds similar lengths (a tile runs to its longest lane); SWBANK_DSORT=0 disables.
   const uint32_t* ident = nullptr;  // device sort: 1 when the lengths share one bin
-  uint64_t* moffs = nullptr;  // device sort: offsets / lengths in the sort's order
-  uint32_t* mlens = nullptr;
   // Balanced chunk ranges over a ragged device batch: the sort's last block also
   // writes where each workgroup's range starts in the longest-first tile sequence, so the choice
   // is made before the sort.  Every range must hold two of the longest tiles' chunks (the head
@@ -265,16 +263,8 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       HIPOK(b, b->bal_plan.reserve((size_t)(rbal_grid + 1) * 4));
       b->bal_key[0] = 0;  // the uniform plan is overwritten
     }
-    // a device batch of byte codes also gets its offsets and lengths in the sort's order, so
-    // the tiles load them directly (one dependent load level less per tile)
-    if (!sort_out && packed == SWK_PACK_BYTES && d_offs && env_int("SWBANK_DSORT_META", 1) != 0) {
-      HIPOK(b, b->dpoffs.reserve(n));
-      HIPOK(b, b->dplens.reserve(n));
-      moffs = b->dpoffs.p;
-      mlens = b->dplens.p;
-    }
     HIPOK(b, swk_sort_lens(d_lens, n, max_len, order, order + n, order + n + 1, scr, st,
-                           rbal_grid ? b->bal_plan.p : nullptr, rbal_grid, d_offs, moffs, mlens));
+                           rbal_grid ? b->bal_plan.p : nullptr, rbal_grid));
     ++b->ctr.device_sorts;
     if (!sort_out) {  // (the host feeder's chunks sort too: not named per chunk)
       const size_t L = strlen(b->last_kernel);
@@ -318,15 +308,9 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       int32_t* scores = d_scores;
       const uint32_t* idx = nullptr;
       const uint32_t* nidx = nullptr;
-      const uint64_t* poffs = nullptr;  // the sort's ordered metadata (pass 0, with perm)
-      const uint32_t* plens = nullptr;
       if (pass == 0 && perm) {  // whole arrays, visited through the permutation
         idx = perm + p0;
         nidx = perm_n;
-        if (moffs) {
-          poffs = moffs + p0;
-          plens = mlens + p0;
-        }
       } else if (pass == 0 && rec) {
         res = d_res + p0 * SWB_RECORD;
         scores = d_scores + p0;
@@ -372,7 +356,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
           HIPOK(b, swk_launch_pair_bal(res, offs, lens, np, b->qpair.p, b->nv16, b->S, b->O, b->E,
                                        b->pair_bytes, b->pad, Wl, scores, b->pS1, b->pS2, ulen,
                                        ustride, b->bal_flag.p, b->bal_state.p, ++b->bal_gen, grid,
-                                       idx, nidx, ident, b->bal_plan.p, st, poffs, plens));
+                                       idx, nidx, ident, b->bal_plan.p, st));
           ++b->ctr.balanced_calls;
           const size_t L = strlen(b->last_kernel);
           snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " balanced grid=%u", grid);
@@ -395,7 +379,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                                   b->pad, Wl, scores, ein, eout, ecols, s > 0 ? 1 : 0,
                                   (int)packed, idx, nidx, (uint32_t)p0,
                                   pass == 0 ? ident : nullptr, pair ? 1 : 0, b->pS1, b->pS2,
-                                  ulen, ustride, 1u, 0u, 0, st, poffs, plens));
+                                  ulen, ustride, 1u, 0u, 0, st));
       }
     }
   }
