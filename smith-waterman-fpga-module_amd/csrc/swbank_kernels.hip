@@ -35,6 +35,9 @@
 
 #include "swbank_internal.h"
 
+#ifndef SWK_TAIL_TOP
+#define SWK_TAIL_TOP 1
+#endif
 #ifndef SWK_PRIO_ROT
 // Rotating wave priorities in the persistent tile kernel: the SIMD issues from the oldest ready
 // wave first, so of the 4 resident workgroups of a CU the first dispatched ran ahead and
@@ -2660,6 +2663,9 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
     if (blockIdx.x >= a.split_blocks + mb) {
       const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
       const unsigned u = (blockIdx.x - a.split_blocks - mb) * 4 + wave;
+      // the tail waves are the youngest on their SIMDs: without the top priority the SIMD's
+      // oldest-first issue starves their segment chain behind the main waves
+      if (SWK_TAIL_TOP) __builtin_amdgcn_s_setprio(3);
       if (u < a.tail_pairs * a.split_P)
         wave_tail_seg<GOTOH>(a, prof + (size_t)wave * a.split_words * 4, lane, u);
       return;
