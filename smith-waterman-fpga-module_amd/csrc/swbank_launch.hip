@@ -165,10 +165,10 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       if (sforce >= 0) T = std::min(pairs, (size_t)sforce);
       else if (pairs >= units && pairs % units <= units / 2) T = pairs % units;
       const int pforce = env_int("SWBANK_WAVE_SPLIT_P", 0);
-      // two pairs per wave (f16), SWBANK_WAVE_SPLIT_P=8 only: the tail as 8 segments of 64 rows,
-      // one wave each on its own SIMD, handed on through global memory (measured 12 % slower
-      // than P = 4 on configs[4])
-      const bool seg8 = half && b->sK[2] == 1 && T && pforce == 8;
+      // two pairs per wave (f16): a tail of at most SIMDs / 8 pairs runs as 8 segments of 64
+      // rows, one wave each on its own SIMD at the top issue priority, handed on through global
+      // memory; SWBANK_WAVE_SPLIT_P=4 forces the in-block split
+      const bool seg8 = half && b->sK[2] == 1 && T && (pforce == 8 || (!pforce && 8 * T <= simds));
       const int i = pforce == 2 ? 0 : pforce == 4 ? 1 : (4 * T <= simds ? 1 : 0);
       if (seg8) {
         HIPOK(b, b->sring.reserve(std::max<size_t>(1, T * 7 * (size_t)ecols)));

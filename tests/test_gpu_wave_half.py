@@ -82,19 +82,19 @@ def test_half_with_split_tail(monkeypatch, split, P):
     assert np.array_equal(got, want) and np.array_equal(one, want), kern
 
 
-@pytest.mark.parametrize("tail", ["default", "seg8"])
+@pytest.mark.parametrize("tail", ["default", "split4"])
 @pytest.mark.parametrize("model", [S.GAP_GOTOH, S.GAP_MERGED])
 @pytest.mark.parametrize("n,qlen", [(12500, 512), (2300, 480), (4127, 300)])
 def test_half_segmented_tail_policy(monkeypatch, poisoned_buffers, model, n, qlen, tail):
     """The policy's own tail (configs[4]'s shape: 6,250 pairs = 3 two-pair waves per SIMD + 106
-    pairs, as P = 4 row segments in one block by default, or as 8 x 64-row segments on separate
-    SIMDs with SWBANK_WAVE_SPLIT_P=8), ragged and empty targets among the tail pairs,
+    pairs, as 8 x 64-row segments on separate SIMDs by default, or as P = 4 row segments in one
+    block with SWBANK_WAVE_SPLIT_P=4), ragged and empty targets among the tail pairs,
     near-copies of the query past 2048 in the tail (the last segment re-scores its pair in u16),
     both gap models, poisoned device buffers; device API (no host chunking)."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("SWBANK_KERNEL", "wave")
-    if tail == "seg8":
-        monkeypatch.setenv("SWBANK_WAVE_SPLIT_P", "8")
+    if tail == "split4":
+        monkeypatch.setenv("SWBANK_WAVE_SPLIT_P", "4")
     rng = np.random.default_rng(n + qlen + model)
     q = rng.integers(0, 20, qlen, dtype=np.uint8)
     seqs = _targets(rng, n, 900, 1000, 20)
@@ -121,7 +121,7 @@ def test_half_segmented_tail_policy(monkeypatch, poisoned_buffers, model, n, qle
     got = d_sc.cpu().numpy()
     assert "pairs/wave=2" in kern, kern
     if n == 12500:
-        assert ("tail=106/8" if tail == "seg8" else "split=106/4") in kern, kern
+        assert ("split=106/4" if tail == "split4" else "tail=106/8") in kern, kern
     want = O.score_batch(q, res, offs, lens, O.BLOSUM62, -11, -1,
                          O.GAP_GOTOH if model == S.GAP_GOTOH else O.GAP_MERGED)
     bad = np.nonzero(got != want)[0]
