@@ -35,9 +35,6 @@
 
 #include "swbank_internal.h"
 
-#ifndef SWK_PRIO_MAIN
-#define SWK_PRIO_MAIN 0
-#endif
 #ifndef SWK_TAIL_TOP
 #define SWK_TAIL_TOP 1
 #endif
@@ -2429,27 +2426,9 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   // of steps from an even t never wraps, so one address per pair and immediate offsets.
   // SWK_HALF_UNROLL: steps per loop iteration (2 or 4)
   const uint32_t* rp = ring_l;
-#if SWK_PRIO_MAIN
-  // (the 3 main waves of a SIMD come from main blocks a third of them apart)
-  const uint32_t mbk = (a.main_pairs + 7) / 8;
-  const uint32_t prq = (uint32_t)(((blockIdx.x - a.split_blocks) * 3ull) / max(mbk, 1u));
-  uint32_t prio = 4;
-#endif
   const auto step = [&](const int t, const bool even) __attribute__((always_inline)) {
     // the next 32 columns go in before they are read (AHEAD: two steps before)
     if ((AHEAD ? even : !even) && (t & 31) == (AHEAD ? 30 : 31)) {
-#if SWK_PRIO_MAIN
-      {  // (A/B) the 3 main waves of a SIMD rotate over levels 0-2 (the tail waves hold 3)
-        const uint32_t pr =
-            ((uint32_t)(__builtin_amdgcn_s_memtime() >> SWK_PRIO_SHIFT) + prq) % 3u;
-        if (pr != prio) {
-          prio = pr;
-          if (pr == 0) __builtin_amdgcn_s_setprio(0);
-          else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-          else __builtin_amdgcn_s_setprio(2);
-        }
-      }
-#endif
       ring_write(ncode);
       // (t through an opaque copy: no per-step pointer increments for these loads)
       uint32_t tt = (uint32_t)t;
