@@ -52,7 +52,7 @@ def test_bench_two_ranks_gathered_parity(workload):
 @pytest.mark.parametrize("workload", ["ragged", "data500", "reads150x1k", "protein512x1k"])
 def test_bench_workloads_one_gpu(workload):
     """Every bench workload the driver does not run itself, at reduced size: configs[3] (the
-    query-set path, 4 x 1-kbp queries) and configs[4] (protein, the wave kernel with its split
+    query-set path, 4 x 1-kbp queries) and configs[4] (protein, the wave kernel with its segmented
     tail: 4,300 targets = 2,150 pairs, 102 past two pairs per SIMD)."""
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
            "--reps", "64", "--reads", "8192", "--slice", "4", "--ptargets", "4300",
@@ -68,4 +68,4 @@ def test_bench_workloads_one_gpu(workload):
     if workload == "reads150x1k":
         assert "queries=4" in d["kernel"], d["kernel"]
     if workload == "protein512x1k":
-        assert d["kernel"].startswith("wave") and "split=" in d["kernel"], d["kernel"]
+        assert d["kernel"].startswith("wave") and "tail=102/8" in d["kernel"], d["kernel"]
