@@ -53,9 +53,12 @@ extern "C" {
 /* ABI 2: ids on the batch calls and the batch best hit (ScoreBank_v2.v:39-43), multi-device
  * banks (sw_config.n_devices / devices[]), scores past the 16-bit lanes (int32 re-score).
  * ABI 3: sw_score_batch_device_range (caller length range) and sw_bank_counters.
- * ABI 4: sw_bank_counters takes the caller's struct size; multi-device banks take device
- *        batches and query sets. */
-#define SWBANK_ABI_VERSION 4
+ * ABI 4: sw_bank_counters took the caller's struct size; multi-device banks take device
+ *        batches and query sets.
+ * ABI 5: SW_ERR_TIMEOUT and sw_bank_sync (device-side hand-off waits that run out fail the call,
+ *        ≙ the CAPI host failing on the AFU's error bits, main_test.c:64-100); sw_bank_counters
+ *        is the two-argument ABI-3 form again, sw_bank_counters_ex takes the struct size. */
+#define SWBANK_ABI_VERSION 5
 
 typedef int32_t sw_status;
 enum {
@@ -67,7 +70,10 @@ enum {
   SW_ERR_STATE = -5,       /* penalties or query not loaded yet                          */
   SW_ERR_NOMEM = -6,       /* host or device allocation failed                           */
   SW_ERR_IO = -7,          /* file I/O or parse error (FASTA helpers)                    */
-  SW_ERR_UNSUPPORTED = -8  /* configuration not implemented (e.g. query too long)       */
+  SW_ERR_UNSUPPORTED = -8, /* configuration not implemented (e.g. query too long)       */
+  SW_ERR_TIMEOUT = -9      /* a device-side hand-off wait ran out: the scores of the call
+                              (device calls: of the device calls since the last
+                              synchronising call) are invalid; see sw_bank_sync            */
 };
 
 enum { SW_ALPHABET_DNA = 0, SW_ALPHABET_PROTEIN = 1 };
@@ -229,9 +235,6 @@ sw_status sw_bank_timing(sw_bank *bank, uint64_t *launches, double *pack_ms, dou
  * of chunked calls sent as mixed 2-bit / 4-bit codes (ragged DNA), and the pool parts of those
  * chunks packed as one run (targets back to back in the caller's residues), device calls
  * with balanced chunk ranges. */
-/* out_size = sizeof(sw_counters) as the caller compiled it: the library writes that many bytes
- * (its counters first, zeros past them), so a struct that grows in a later ABI never overflows
- * an older caller's buffer. */
 typedef struct sw_counters {
   uint64_t stream_calls;
   uint64_t stream_reruns;
@@ -245,8 +248,28 @@ typedef struct sw_counters {
    * and hand-off waits that ran out (0 unless a workgroup never started) */
   uint64_t balanced_calls;
   uint64_t balanced_timeouts;
+  /* ABI 5: protein-tail hand-off waits that ran out, and host-buffer calls re-run without
+   * hand-offs because one did (counted when a synchronising call observed them) */
+  uint64_t tail_timeouts;
+  uint64_t handoff_reruns;
 } sw_counters;
-sw_status sw_bank_counters(const sw_bank *bank, sw_counters *out, size_t out_size);
+/* The first 8 counters (the ABI-3 struct, 64 bytes): safe for a caller of any ABI. */
+sw_status sw_bank_counters(const sw_bank *bank, sw_counters *out);
+/* out_size = sizeof(sw_counters) as the caller compiled it: 64 (ABI 3), 80 (ABI 4) or 96
+ * (ABI 5); any other size is SW_ERR_ARG.  No HIP call: the counts are host-side. */
+sw_status sw_bank_counters_ex(const sw_bank *bank, sw_counters *out, size_t out_size);
+
+/* Device-side failure reporting (≙ the CAPI host decoding the AFU's error bits and failing the
+ * call, capi_sample_aligner/software-C,C++/src/main_test.c:64-100).  Two launch shapes hand
+ * work between workgroups of one launch (balanced chunk ranges of device batches, the segmented
+ * protein tail); each wait is bounded, and one that runs out marks the launch as failed instead
+ * of hanging.  A host-buffer call that sees the mark re-runs itself without hand-offs
+ * (handoff_reruns) and returns SW_ERR_TIMEOUT only if that fails too.  A device call is
+ * asynchronous, so its mark is latched on the bank and returned (once, as SW_ERR_TIMEOUT) by
+ * the next call that synchronises with it -- sw_bank_sync, sw_batch_best, sw_bank_timing -- or
+ * by the next device scoring call on the bank, which then scores nothing.
+ * sw_bank_sync waits for the bank's last scoring call (any stream) and returns that status. */
+sw_status sw_bank_sync(sw_bank *bank);
 
 /* Which kernel the last score call ran, e.g. "tile f16 R=32 W=4 segs=1 grid=998" or
  * "wave u16 K=4" (empty before the first call).  No reference counterpart: the RTL has one

@@ -70,7 +70,8 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           uint32_t ustride, uint32_t* flag, uint32_t* state,
                                           uint32_t gen, unsigned grid, const uint32_t* idx,
                                           const uint32_t* nidx, const uint32_t* ident,
-                                          const void* plan, hipStream_t st);
+                                          const void* plan, uint32_t* fault, uint32_t poll_limit,
+                                          uint32_t stall, hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
                                    hipStream_t st);
@@ -517,6 +518,15 @@ struct sw_bank {
   // feeder / fallback counters (sw_bank_counters)
   sw_counters ctr{};
 
+  // Fault words of the cross-workgroup hand-off waits (balanced ranges, the segmented protein
+  // tail; ScoreArgs.fault): coherent host memory, [0] for device calls, [1] for host-buffer
+  // calls, written only by a wait that ran out (SWK_FAULT_* bits) and read after the launch
+  // completed: a host-buffer call re-runs itself without hand-offs (no_handoff), a device call's
+  // fault is latched until the next synchronising call returns it (SW_ERR_TIMEOUT).
+  PinBuf faultw{hipHostMallocCoherent};
+  bool host_call = false;   // launches belong to a host-buffer call (fault word [1])
+  bool no_handoff = false;  // launch() runs neither balanced ranges nor the segmented tail
+
   // profiling
   bool timing = false;
   struct Ev { hipEvent_t a, b, c; };
@@ -592,6 +602,13 @@ inline uint32_t record_len(const uint8_t* rec) {
 
 // ---- swbank_bank.hip
 void copy_kernel_name(sw_bank* b, const char* gather);
+// The fault word launch() hands the kernels (allocated and zeroed on first use; nullptr when the
+// allocation failed), and the check of it: SW_ERR_TIMEOUT (counted, the word cleared) when a
+// hand-off wait of the given kind of call (0 device, 1 host) ran out since the last check.  The
+// caller has synchronised with the launches it means to cover.  A multi-device bank checks every
+// child.
+uint32_t* fault_word(sw_bank* b);
+sw_status take_fault(sw_bank* b, int which);
 sw_status prepare(sw_bank* b);
 sw_status prepare_multi(sw_bank* b);
 sw_status prepare_i32(sw_bank* b);

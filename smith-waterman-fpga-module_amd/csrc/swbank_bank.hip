@@ -160,6 +160,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   uint64_t nl;
   double pm, sm;
   (void)sw_bank_timing(b, &nl, &pm, &sm);
+  b->faultw.release();
   b->qtab.release();
   b->qtab16.release();
   b->mqtab.release();
@@ -241,33 +242,92 @@ extern "C" const char* sw_last_error(const sw_bank* b) { return b ? b->err : "nu
 
 extern "C" const char* sw_last_kernel(const sw_bank* b) { return b ? b->last_kernel : ""; }
 
-extern "C" sw_status sw_bank_counters(const sw_bank* b, sw_counters* out, size_t out_size) {
+uint32_t* fault_word(sw_bank* b) {
+  if (!b->faultw.p) {
+    if (b->faultw.reserve(64) != hipSuccess) return nullptr;
+    std::memset(b->faultw.p, 0, b->faultw.cap);
+  }
+  return reinterpret_cast<uint32_t*>(b->faultw.p);
+}
+
+sw_status take_fault(sw_bank* b, int which) {
+  if (b->is_multi()) {
+    sw_status st = SW_OK;
+    for (sw_bank* k : b->kids) {  // every child's word is cleared, the first fault reported
+      const sw_status ks = take_fault(k, which);
+      if (ks != SW_OK && st == SW_OK) st = fail(b, ks, "device %d: %s", k->device, k->err);
+    }
+    return st;
+  }
+  if (!b->faultw.p) return SW_OK;
+  volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(b->faultw.p) + which;
+  const uint32_t f = *w;
+  if (f == 0) return SW_OK;
+  *w = 0;
+  if (f & SWK_FAULT_BAL) ++b->ctr.balanced_timeouts;
+  if (f & SWK_FAULT_TAIL) ++b->ctr.tail_timeouts;
+  return fail(b, SW_ERR_TIMEOUT,
+              "a cross-workgroup hand-off wait ran out (%s%s) in a %s call: its scores are invalid",
+              f & SWK_FAULT_BAL ? "balanced ranges " : "", f & SWK_FAULT_TAIL ? "protein tail" : "",
+              which ? "host-buffer" : "device");
+}
+
+extern "C" sw_status sw_bank_sync(sw_bank* b) {
+  if (!b) return SW_ERR_ARG;
+  if (b->is_multi()) {
+    for (sw_bank* k : b->kids) {
+      const sw_status st = sw_bank_sync(k);
+      if (st != SW_OK) {
+        (void)take_fault(b, 0);  // (clear the other devices' words too)
+        return fail(b, st, "device %d: %s", k->device, k->err);
+      }
+    }
+    return SW_OK;
+  }
+  int cur = -1;
+  HIPOK(b, hipGetDevice(&cur));
+  hipError_t e = hipSetDevice(b->device);
+  // ev_used follows every launch of a scoring call on the stream it ran on
+  if (e == hipSuccess && b->ev_used) e = hipEventSynchronize(b->ev_used);
+  if (e == hipSuccess) e = hipStreamSynchronize(b->stream);
+  (void)hipSetDevice(cur);
+  HIPOK(b, e);
+  return take_fault(b, 0);
+}
+
+static void sum_counters(sw_counters& c, const sw_bank* b) {
+  c.stream_calls += b->ctr.stream_calls;
+  c.stream_reruns += b->ctr.stream_reruns;
+  c.stream_declined += b->ctr.stream_declined;
+  c.chunked_calls += b->ctr.chunked_calls;
+  c.device_sorts += b->ctr.device_sorts;
+  c.gather_timeouts += b->ctr.gather_timeouts;
+  c.mixed_chunks += b->ctr.mixed_chunks;
+  c.mixed_runs += b->ctr.mixed_runs;
+  c.balanced_calls += b->ctr.balanced_calls;
+  c.balanced_timeouts += b->ctr.balanced_timeouts;
+  c.tail_timeouts += b->ctr.tail_timeouts;
+  c.handoff_reruns += b->ctr.handoff_reruns;
+}
+
+// Host-side counts only (no HIP call): a hand-off time-out is counted when a synchronising call
+// takes it from the fault word.
+extern "C" sw_status sw_bank_counters_ex(const sw_bank* b, sw_counters* out, size_t out_size) {
   if (!b || !out) return SW_ERR_ARG;
-  sw_counters c = b->ctr;
-  for (const sw_bank* k : b->kids) {
-    c.stream_calls += k->ctr.stream_calls;
-    c.stream_reruns += k->ctr.stream_reruns;
-    c.stream_declined += k->ctr.stream_declined;
-    c.chunked_calls += k->ctr.chunked_calls;
-    c.device_sorts += k->ctr.device_sorts;
-    c.gather_timeouts += k->ctr.gather_timeouts;
-    c.mixed_chunks += k->ctr.mixed_chunks;
-    c.mixed_runs += k->ctr.mixed_runs;
-    c.balanced_calls += k->ctr.balanced_calls;
-  }
-  // balanced-range hand-off waits that ran out, counted on the device (a snapshot)
-  for (const sw_bank* k : b->kids.empty() ? std::vector<const sw_bank*>{b}
-                                           : std::vector<const sw_bank*>(b->kids.begin(),
-                                                                         b->kids.end())) {
-    uint32_t t = 0;  // bal_flag[0] (workgroup 0's flag slot, never waited on)
-    if (k->bal_flag.cap && hipSetDevice(k->device) == hipSuccess &&
-        hipMemcpy(&t, k->bal_flag.p, 4, hipMemcpyDeviceToHost) == hipSuccess)
-      c.balanced_timeouts += t;
-  }
-  // a caller built against an older (shorter) struct gets its prefix, a newer one zeroes past ours
-  std::memset(out, 0, out_size);
-  std::memcpy(out, &c, std::min(out_size, sizeof(c)));
+  // the struct sizes of ABI 3 (8 counters), ABI 4 (10) and ABI 5 (12)
+  if (out_size != 64 && out_size != 80 && out_size != sizeof(sw_counters))
+    return SW_ERR_ARG;
+  sw_counters c{};
+  sum_counters(c, b);
+  for (const sw_bank* k : b->kids) sum_counters(c, k);
+  std::memcpy(out, &c, out_size);
   return SW_OK;
+}
+
+// ABI 5: the two-argument form of ABI 3 again, writing the ABI-3 prefix (8 counters), so a
+// caller of either earlier ABI never gets more bytes than its struct holds.
+extern "C" sw_status sw_bank_counters(const sw_bank* b, sw_counters* out) {
+  return sw_bank_counters_ex(b, out, 64);
 }
 
 void copy_kernel_name(sw_bank* b, const char* gather) {
@@ -883,6 +943,8 @@ extern "C" sw_status sw_bank_timing(sw_bank* b, uint64_t* launches, double* pack
   if (launches) *launches = n;
   if (pack_ms) *pack_ms = p;
   if (score_ms) *score_ms = s;
+  // the launches timed are complete: a device call's latched hand-off fault surfaces here
+  if (st == SW_OK && n > 0) st = take_fault(b, 0);
   return st;
 }
 

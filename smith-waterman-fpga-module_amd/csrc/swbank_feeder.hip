@@ -423,10 +423,40 @@ bool mixed_pack(sw_bank* b, const uint8_t* residues, size_t nres, const uint64_t
   return true;
 }
 
+// A host-buffer call `run` (its launches complete when it returns) with the hand-off fault
+// check: a wait that ran out in one of its launches (fault word [1]) re-runs the call once
+// without hand-offs (neither balanced ranges nor the segmented protein tail: every dependency
+// inside a workgroup), which returns SW_ERR_TIMEOUT only if it faults too.
+template <class F>
+static sw_status with_fault_check(sw_bank* b, F&& run) {
+  struct Scope {
+    sw_bank* b;
+    ~Scope() { b->host_call = b->no_handoff = false; }
+  } scope{b};
+  b->host_call = true;
+  sw_status st = run();
+  const sw_status fs = take_fault(b, 1);
+  if (st != SW_OK || fs == SW_OK) return st;
+  ++b->ctr.handoff_reruns;
+  b->no_handoff = true;
+  st = run();
+  const sw_status fs2 = take_fault(b, 1);
+  return st != SW_OK ? st : fs2;
+}
+
+static sw_status batch_feed_once(sw_bank* b, const uint8_t* residues, size_t nres,
+                                 const uint64_t* offsets, const uint32_t* lens, size_t n,
+                                 int32_t* out);
+
 // The host-buffer batch through the feeder (n >= 1, buffers checked by the caller).
-sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres,
-                            const uint64_t* offsets, const uint32_t* lens, size_t n,
-                            int32_t* out) {
+sw_status batch_feed(sw_bank* b, const uint8_t* residues, size_t nres, const uint64_t* offsets,
+                     const uint32_t* lens, size_t n, int32_t* out) {
+  return with_fault_check(b, [&] { return batch_feed_once(b, residues, nres, offsets, lens, n, out); });
+}
+
+static sw_status batch_feed_once(sw_bank* b, const uint8_t* residues, size_t nres,
+                                 const uint64_t* offsets, const uint32_t* lens, size_t n,
+                                 int32_t* out) {
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
   if ((st = feeder_init(b)) != SW_OK) return st;
@@ -829,6 +859,7 @@ extern "C" sw_status sw_score_records_device(sw_bank* b, const void* d_records, 
   if (!b) return SW_ERR_ARG;
   b->best_kind = 0;
   b->best_root = false;
+  if (const sw_status fs = take_fault(b, 0); fs != SW_OK) return fs;  // latched, see swbank.h
   if (n == 0) return SW_OK;
   if (!d_records || !d_scores) return fail(b, SW_ERR_ARG, "null device buffer");
   if (b->alpha != SW_DNA_ALPHA) return fail(b, SW_ERR_UNSUPPORTED, "records carry DNA only");
@@ -844,9 +875,15 @@ extern "C" sw_status sw_score_records_device(sw_bank* b, const void* d_records, 
                 SWK_PACK_RECORDS);
 }
 
+static sw_status records_feed_once(sw_bank* b, const uint8_t* recs, size_t n, int32_t* out);
+
 // Host records through the feeder (n >= 1, buffers checked by the caller); lengths are
 // checked while gathering.
 sw_status records_feed(sw_bank* b, const uint8_t* recs, size_t n, int32_t* out) {
+  return with_fault_check(b, [&] { return records_feed_once(b, recs, n, out); });
+}
+
+static sw_status records_feed_once(sw_bank* b, const uint8_t* recs, size_t n, int32_t* out) {
   sw_status st = prepare(b);
   if (st != SW_OK) return st;
   if ((st = feeder_init(b)) != SW_OK) return st;

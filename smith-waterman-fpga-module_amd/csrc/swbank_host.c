@@ -24,6 +24,7 @@ const char *sw_status_string(sw_status s) {
     case SW_ERR_NOMEM: return "out of memory";
     case SW_ERR_IO: return "I/O or parse error";
     case SW_ERR_UNSUPPORTED: return "unsupported configuration";
+    case SW_ERR_TIMEOUT: return "device-side hand-off wait timed out (scores invalid)";
     default: return "unknown status";
   }
 }

@@ -42,11 +42,18 @@ typedef struct SwkWaveSplit {
   unsigned words, fb_words, PS, fb_PS;
   void* ring;
   /* P = 8 (two-pairs kernel only): the segmented tail, one 64-row segment per wave in blocks
-   * after the main ones; ring = pairs x 7 x cols columns of 8 B, prog = pairs x 8 x 3 + 1
-   * words zeroed before the launch (progress, bests, poll time-outs) */
+   * after the main ones; ring = pairs x 7 x cols columns of 8 B, prog = pairs x 8 x 3 words
+   * zeroed before the launch (progress, bests); a hand-off wait that runs out after poll_limit
+   * polls marks *fault (SWK_FAULT_TAIL, coherent host memory); stall: a test hook (ScoreArgs) */
   unsigned cols;
   unsigned* prog;
+  unsigned* fault;
+  unsigned poll_limit, stall;
 } SwkWaveSplit;
+
+/* Bits of a launch's fault word (cross-workgroup hand-off waits that ran out). */
+#define SWK_FAULT_BAL 1u
+#define SWK_FAULT_TAIL 2u
 
 /* One chunk of a streamed host batch (uploaded before the launch): its first tile and the
  * offset of its codes in the device batch buffer.  Its code layout travels in a flag word per

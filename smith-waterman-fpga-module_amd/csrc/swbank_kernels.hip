@@ -765,12 +765,25 @@ struct ScoreArgs {
   // each, in 4-wave blocks after the main blocks; segment s hands its bottom row to s + 1
   // through split_ring (a whole row of columns per boundary) and tail_prog (64-column blocks
   // done, zeroed by the host before the launch) instead of a barrier, so a pair's segments sit
-  // on different CUs.  tail_prog: [pair][segment] progress | [pair][segment] best (uint2) |
-  // poll time-outs.
+  // on different CUs.  tail_prog: [pair][segment] progress | [pair][segment] best (uint2).
   uint32_t* tail_prog;
   uint32_t tail_pairs, tail_cols;
+  // cross-workgroup hand-off waits (balanced ranges, the segmented tail): a wait that runs out
+  // after poll_limit polls stores its bit (SWK_FAULT_*) into *fault, a word in coherent host
+  // memory the host reads at its next synchronisation and turns into SW_ERR_TIMEOUT or a re-run
+  // (the scores of the launch are not trusted).  stall (a test hook, 0 = off): the producer the
+  // g-th waiter depends on skips its hand-off (balanced ranges: workgroup g - 1's flag; the tail:
+  // segment 0 of tail pair g - 1), so the time-out path runs.
+  uint32_t* fault;
+  uint32_t poll_limit, stall;
 };
-static_assert(sizeof(ScoreArgs) == 344, "ScoreArgs layout (kernel argument block) changed");
+static_assert(sizeof(ScoreArgs) == 360, "ScoreArgs layout (kernel argument block) changed");
+
+// a hand-off wait ran out: mark the launch's fault word (a vector store to host memory; only the
+// host reads it, after the launch completed)
+__device__ __forceinline__ void report_fault(uint32_t* fault, uint32_t bit) {
+  if (fault) __hip_atomic_store(fault, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) void* glob_void_ptr;
@@ -1131,8 +1144,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   // + l] (coalesced), written and read with sc1 (write-through / L2) accesses and a flag
   // (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores, vmcnt(0), sc1 flag; sc1 poll,
   // sc1 loads).  The consumer's tail is its last visit and the producer's head its first, so
-  // the flag is normally long set; the poll is bounded (about 4 s) and counts a time-out in
-  // bal_flag[0] rather than hanging.
+  // the flag is normally long set; the poll is bounded (poll_limit, about 4 s) and a time-out
+  // marks the launch's fault word (the host fails the call) rather than hanging.
   // (the state addresses go through an opaque copy: loop-invariant, LLVM would otherwise hoist
   // all 2R + 2 of them out of the phase loop, 2 VGPRs each, and spill)
   int bal_pend = 0;  // BAL: phases until the head's flag goes out (0: none pending)
@@ -1152,7 +1165,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   };
   const auto bal_flag_out = [&]() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0)
+    if (lane == 0 && blockIdx.x + 1 != a.stall)  // (stall: a test hook)
       __hip_atomic_store(a.bal_flag + ((size_t)blockIdx.x + 1) * W + wave, a.bal_gen,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
@@ -1164,14 +1177,14 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     const uint64_t sb0 = __builtin_amdgcn_s_memtime();
 #endif
     const uint32_t* fl = a.bal_flag + (size_t)blockIdx.x * W + wave;
-    int it = 0;
-    for (; it < (1 << 23); ++it) {
+    uint32_t it = 0;
+    for (; it < a.poll_limit; ++it) {
       if (__builtin_amdgcn_readfirstlane(
               __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == a.bal_gen)
         break;
       __builtin_amdgcn_s_sleep(8);
     }
-    if (it == (1 << 23) && lane == 0) atomicAdd(a.bal_flag, 1u);  // (workgroup 0 never waits)
+    if (it == a.poll_limit && lane == 0) report_fault(a.fault, SWK_FAULT_BAL);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t* sp = a.bal_state + ((size_t)blockIdx.x * W + wave) * (2 * R + 2) * 64 + lane;
     asm volatile("" : "+v"(sp));
@@ -2538,16 +2551,17 @@ __device__ __forceinline__ void wave_tail_seg(const ScoreArgs& a, uint8_t* wlds,
   };
   uint32_t* prog = a.tail_prog + (size_t)ti * P;
   uint2* bests = reinterpret_cast<uint2*>(a.tail_prog + (size_t)T * P) + (size_t)ti * P;
-  uint32_t* timeouts = a.tail_prog + (size_t)T * P * 3;
   const auto wait_for = [&](const uint32_t* w, uint32_t v) {
-    for (int it = 0; it < (1 << 24); ++it) {
+    for (uint32_t it = 0; it < a.poll_limit; ++it) {
       if (__builtin_amdgcn_readfirstlane(
               __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= v)
         return;
       __builtin_amdgcn_s_sleep(4);
     }
-    if (lane == 0) atomicAdd(timeouts, 1u);
+    if (lane == 0) report_fault(a.fault, SWK_FAULT_TAIL);
   };
+  // (test hook) segment 0 of tail pair stall - 1 publishes nothing
+  const bool mute = a.stall != 0 && s == 0 && ti + 1 == a.stall;
   const uint2* rin = s > 0 ? a.split_ring + ((size_t)ti * (P - 1) + (s - 1)) * a.tail_cols
                            : nullptr;
   uint2* rout = s + 1 < P ? a.split_ring + ((size_t)ti * (P - 1) + s) * a.tail_cols : nullptr;
@@ -2601,7 +2615,7 @@ __device__ __forceinline__ void wave_tail_seg(const ScoreArgs& a, uint8_t* wlds,
     }
     if (rout) {  // this block's ring columns are out
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0)
+      if (lane == 0 && !mute)
         __hip_atomic_store(prog + s, (uint32_t)(blk + 1), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -2619,7 +2633,7 @@ __device__ __forceinline__ void wave_tail_seg(const ScoreArgs& a, uint8_t* wlds,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0)
+    if (lane == 0 && !mute)
       __hip_atomic_store(prog + s, (uint32_t)nblk + 1u, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     return;
@@ -2836,8 +2850,8 @@ extern "C" void swk_set_stamps(void* p) { swk::g_stamps_host = static_cast<uint6
 // Balanced chunk ranges (ScoreArgs.bal_*) for the DNA merged f16 pair-table kernel (the
 // headline shape): codes one byte each (or ustride / ulen), one query segment of W <= 4 waves.
 // swk_bal_slots gives the grid (every resident slot); the host sizes bal_state ((grid + 1) x W
-// x (2R + 2) x 64 words) and bal_flag ((grid + 1) x W words, zeroed once; bal_flag[0] counts
-// poll time-outs).  plan: grid + 1 entries {tile, chunk, chunk index} (swk_bal_plan_uniform for
+// x (2R + 2) x 64 words) and bal_flag ((grid + 1) x W words, zeroed once); a hand-off wait
+// that runs out after poll_limit polls marks *fault (SWK_FAULT_BAL).  plan: grid + 1 entries {tile, chunk, chunk index} (swk_bal_plan_uniform for
 // a uniform batch; a ragged batch visited longest first through the device sort's permutation
 // idx / nidx / ident passes the sort's, swk_sort_lens with the same grid).
 namespace swk {
@@ -2884,9 +2898,11 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           uint32_t ustride, uint32_t* flag, uint32_t* state,
                                           uint32_t gen, unsigned grid, const uint32_t* idx,
                                           const uint32_t* nidx, const uint32_t* ident,
-                                          const void* plan, hipStream_t st) {
+                                          const void* plan, uint32_t* fault, uint32_t poll_limit,
+                                          uint32_t stall, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (W > 4 || !flag || !state || !plan || (idx && !nidx)) return hipErrorInvalidValue;
+  if (W > 4 || !flag || !state || !plan || !fault || poll_limit == 0 || (idx && !nidx))
+    return hipErrorInvalidValue;
   swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                    O,    E,    PS,   pad, scores, nullptr, nullptr, 0u, 0u, (uint32_t)SWK_PACK_BYTES,
                    idx, nidx, 0u, ident, pS1, pS2,
@@ -2899,6 +2915,9 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
   a.bal_state = state;
   a.bal_gen = gen;
   a.bal_plan = static_cast<const uint4*>(plan);
+  a.fault = fault;
+  a.poll_limit = poll_limit;
+  a.stall = stall;
   return swk::launch_score<32, 4, false, false, false, true, true, false, false, 8, true>(
       a, W, 0, st, grid);
 }
@@ -3057,9 +3076,13 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
   if (split && split->pairs > 0 && split->P == 8) {
     // the segmented tail of the two-pairs kernel (ScoreArgs.tail_*)
     if (!half || K != 8 || edge_in || edge_out || accum || split->pairs > pairs ||
-        pairs > 0xFFFFFFFFull || !split->prog || split->cols == 0)
+        pairs > 0xFFFFFFFFull || !split->prog || split->cols == 0 || !split->fault ||
+        split->poll_limit == 0)
       return hipErrorInvalidValue;
     a.split_P = 8;
+    a.fault = split->fault;
+    a.poll_limit = split->poll_limit;
+    a.stall = split->stall;
     a.tail_pairs = split->pairs;
     a.tail_cols = split->cols;
     a.tail_prog = split->prog;

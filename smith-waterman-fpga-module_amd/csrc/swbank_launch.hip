@@ -65,6 +65,13 @@ bool wave_preferred(const sw_bank* b, size_t n, uint32_t max_len, bool use_f16) 
   return use_wave;
 }
 
+// Polls of a cross-workgroup hand-off wait before it gives up (ScoreArgs.poll_limit): the
+// kernel's default (about 4 s), or SWBANK_POLL_LIMIT (a test hook: short waits with SWBANK_STALL).
+static uint32_t poll_limit(uint32_t dflt) {
+  const int v = env_int("SWBANK_POLL_LIMIT", 0);
+  return v > 0 ? (uint32_t)v : dflt;
+}
+
 // packed (SWK_PACK_*): RECORDS: d_res holds n 64-byte CAPI records (2-bit codes), d_offs and
 // d_lens are unused; STREAM: 2-bit codes, d_offs in bytes (the host feeder's DNA chunks).
 // perm/perm_n (optional, tile kernel): pass 0 visits the targets in the order perm[0..n)
@@ -168,11 +175,15 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       // two pairs per wave (f16): a tail of at most SIMDs / 8 pairs runs as 8 segments of 64
       // rows, one wave each on its own SIMD at the top issue priority, handed on through global
       // memory; SWBANK_WAVE_SPLIT_P=4 forces the in-block split
-      const bool seg8 = half && b->sK[2] == 1 && T && (pforce == 8 || (!pforce && 8 * T <= simds));
+      // (no_handoff: a host call's re-run after a hand-off wait ran out, take_fault)
+      const bool seg8 = half && b->sK[2] == 1 && T && !b->no_handoff &&
+                        (pforce == 8 || (!pforce && 8 * T <= simds));
       const int i = pforce == 2 ? 0 : pforce == 4 ? 1 : (4 * T <= simds ? 1 : 0);
+      uint32_t* fw = seg8 ? fault_word(b) : nullptr;
+      if (seg8 && !fw) return fail(b, SW_ERR_NOMEM, "fault word allocation failed");
       if (seg8) {
         HIPOK(b, b->sring.reserve(std::max<size_t>(1, T * 7 * (size_t)ecols)));
-        const size_t pw = T * 8 * 3 + 1;  // progress, bests (uint2), poll time-outs
+        const size_t pw = T * 8 * 3;  // progress, bests (uint2)
         HIPOK(b, b->tprog.reserve(pw));
         HIPOK(b, hipMemsetAsync(b->tprog.p, 0, pw * 4, st));
         sp.pairs = (unsigned)T;
@@ -183,6 +194,9 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
         sp.ring = b->sring.p;
         sp.cols = ecols;
         sp.prog = b->tprog.p;
+        sp.fault = fw + (b->host_call ? 1 : 0);
+        sp.poll_limit = poll_limit(1u << 24);
+        sp.stall = (unsigned)std::max(0, env_int("SWBANK_STALL", 0));
         const size_t L = strlen(b->last_kernel);
         snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " tail=%zu/8", T);
       } else if (T && b->sK[i]) {
@@ -231,7 +245,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   // is made before the sort.  Every range must hold two of the longest tiles' chunks (the head
   // and the tail of a range are different tiles): checked with the caller's length bounds.
   unsigned rbal_grid = 0;
-  if (dsort && !sort_out && !use_wave && !perm && use_f16 && use_pair && !gotoh && nseg == 1 &&
+  if (dsort && !sort_out && !b->no_handoff && !use_wave && !perm && use_f16 && use_pair && !gotoh && nseg == 1 &&
       wait_prev && packed == SWK_PACK_BYTES && min_len < max_len && max_len < 2048 && !opt16 &&
       b->R == 32 && b->segs[0].W <= 4 && n <= 0xFFFFFFFFull && env_int("SWBANK_DSORT", 1) != 0 &&
       env_int("SWBANK_BAL", 1) != 0 && env_int("SWBANK_BAL_RAGGED", 1) != 0 &&
@@ -329,12 +343,14 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       // (998 of 1,024 on the headline batch, -2.4 %).  A ragged device batch (rbal_grid) runs
       // through the sort's permutation with the sort's plan.  SWBANK_BAL=0 disables.
       const bool rbal = pass == 0 && rbal_grid && perm && idx == perm && span == n;
-      if (rbal || (pass == 0 && f16 && use_pair && !gotoh && nseg == 1 && !idx && wait_prev &&
+      if (rbal || (pass == 0 && !b->no_handoff && f16 && use_pair && !gotoh && nseg == 1 && !idx && wait_prev &&
                    packed == SWK_PACK_BYTES && min_len == max_len && max_len > 0 && span == n &&
                    ntiles * ((max_len + 7) / 8) < (1ull << 31) && !opt16 && b->R == 32 &&
                    b->segs[0].W <= 4 && env_int("SWBANK_BAL", 1) != 0)) {
         const int Wl = b->segs[0].W;
         const unsigned grid = rbal ? rbal_grid : swk_bal_slots(Wl, b->pair_bytes);
+        uint32_t* fw = fault_word(b);
+        if (!fw) return fail(b, SW_ERR_NOMEM, "fault word allocation failed");
         if (grid && (rbal || ntiles >= 2 * (size_t)grid)) {
           const size_t sw = (size_t)(grid + 1) * Wl * (2 * 32 + 2) * 64;
           HIPOK(b, b->bal_state.reserve(sw));
@@ -356,7 +372,9 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
           HIPOK(b, swk_launch_pair_bal(res, offs, lens, np, b->qpair.p, b->nv16, b->S, b->O, b->E,
                                        b->pair_bytes, b->pad, Wl, scores, b->pS1, b->pS2, ulen,
                                        ustride, b->bal_flag.p, b->bal_state.p, ++b->bal_gen, grid,
-                                       idx, nidx, ident, b->bal_plan.p, st));
+                                       idx, nidx, ident, b->bal_plan.p,
+                                       fw + (b->host_call ? 1 : 0), poll_limit(1u << 23),
+                                       (uint32_t)std::max(0, env_int("SWBANK_STALL", 0)), st));
           ++b->ctr.balanced_calls;
           const size_t L = strlen(b->last_kernel);
           snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " balanced grid=%u", grid);
@@ -568,6 +586,8 @@ extern "C" sw_status sw_score_batch_device_range(sw_bank* b, const uint8_t* d_re
   if (min_len > max_len) return fail(b, SW_ERR_ARG, "min_len %u > max_len %u", min_len, max_len);
   b->best_kind = 0;
   b->best_root = false;
+  // a hand-off fault latched by an earlier device call is returned before anything is scored
+  if (const sw_status fs = take_fault(b, 0); fs != SW_OK) return fs;
   if (n == 0) return SW_OK;
   if (!d_res || !d_offs || !d_lens || !d_scores) return fail(b, SW_ERR_ARG, "null device buffer");
   if (b->is_multi()) {
@@ -597,6 +617,10 @@ extern "C" sw_status sw_batch_best(sw_bank* b, uint64_t* best_id, int32_t* best_
     uint64_t h[3];
     HIPOK(b, hipSetDevice(b->device));
     HIPOK(b, hipEventSynchronize(b->best_ev));
+    if (const sw_status fs = take_fault(b, 0); fs != SW_OK) {  // the call's scores are invalid
+      b->best_kind = 0;
+      return fs;
+    }
     HIPOK(b, hipMemcpy(h, b->best_dev.p, sizeof(h), hipMemcpyDeviceToHost));
     b->best_id = h[0];
     b->best_score = (int32_t)(int64_t)h[1];

@@ -28,6 +28,7 @@ CLI_PATH = os.path.join(_PKG, "bin", "swbank")
 OK = 0
 ERR_ARG, ERR_NO_DEVICE, ERR_HIP, ERR_RANGE, ERR_STATE, ERR_NOMEM, ERR_IO, ERR_UNSUPPORTED = \
     -1, -2, -3, -4, -5, -6, -7, -8
+ERR_TIMEOUT = -9  # a device-side hand-off wait ran out (ABI 5): the call's scores are invalid
 ALPHABET_DNA, ALPHABET_PROTEIN = 0, 1
 GAP_MERGED, GAP_GOTOH = 0, 1
 DNA_ALPHA, PROTEIN_ALPHA = 5, 24
@@ -42,11 +43,12 @@ EXPORTS = (
     "sw_last_kernel", "sw_load_query_record", "sw_score_records", "sw_score_records_device",
     "sw_best_hit_device", "sw_batch_best", "sw_bank_devices", "sw_load_queries",
     "sw_query_count", "sw_score_batch_device_range", "sw_bank_counters",
+    "sw_bank_counters_ex", "sw_bank_sync",
 )
-ABI_VERSION = 4
+ABI_VERSION = 5
 COUNTERS = ("stream_calls", "stream_reruns", "stream_declined", "chunked_calls", "device_sorts",
             "gather_timeouts", "mixed_chunks", "mixed_runs", "balanced_calls",
-            "balanced_timeouts")
+            "balanced_timeouts", "tail_timeouts", "handoff_reruns")
 MAX_DEVICES = 16
 RECORD_BYTES, RECORD_MAX_BASES = 64, 232
 
@@ -103,7 +105,9 @@ def lib() -> ctypes.CDLL:
         "sw_score_batch": (i32, [P, P, sz, P, P, P, sz, P]),
         "sw_score_batch_device": (i32, [P, P, P, P, P, sz, u32, P, P]),
         "sw_score_batch_device_range": (i32, [P, P, P, P, P, sz, u32, u32, P, P]),
-        "sw_bank_counters": (i32, [P, P, sz]),
+        "sw_bank_counters": (i32, [P, P]),
+        "sw_bank_counters_ex": (i32, [P, P, sz]),
+        "sw_bank_sync": (i32, [P]),
         "sw_batch_best": (i32, [P, P, P, P]),
         "sw_bank_devices": (i32, [P, P, i32]),
         "sw_best_hit": (i32, [P, P, P, sz, P, P]),
@@ -376,8 +380,13 @@ class ScoreBank:
     def counters(self) -> dict:
         """sw_bank_counters: feeder / fallback counts since the bank was created."""
         c = (ctypes.c_uint64 * len(COUNTERS))()
-        self._check(lib().sw_bank_counters(self._h, ctypes.byref(c), ctypes.sizeof(c)))
+        self._check(lib().sw_bank_counters_ex(self._h, ctypes.byref(c), ctypes.sizeof(c)))
         return dict(zip(COUNTERS, (int(x) for x in c)))
+
+    def sync(self):
+        """sw_bank_sync: wait for the bank's last scoring call; raises SwbankError(ERR_TIMEOUT)
+        when a device call since the last synchronising call had a hand-off wait run out."""
+        self._check(lib().sw_bank_sync(self._h))
 
     # CAPI record path (sequence_t arrays, 2-bit codes)
     def load_query_record(self, record: np.ndarray):
