@@ -30,6 +30,17 @@ Lookups: LUT (DNA) `v_perm_b32 s, nv, lut[row], sel` with the row's LUT word in 
 profile (any alphabet, 2-byte f16 entries) `v_perm_b32 s, hi[w], lo[w], selk` with the two
 target letters' profile words in VGPRs and a per-parity selector in an SGPR.
 
+Mode "F" (profile, 4-byte words {s, 1.0} per letter and row): no lookup instruction at all.
+The next row's diagonal add is one packed FMA that takes target A's entry from the low half of
+A's word and target B's from the low half of B's word, the 1.0 in the other word's high half
+being the multiplier:
+    v_pk_fma_f16 D, a, b, h op_sel:[0,1,0] op_sel_hi:[1,0,1]
+    D.lo = a.lo * b.hi + h.lo = sA + h.lo      D.hi = a.hi * b.lo + h.hi = sB + h.hi
+(exact: every operand is an f16 multiple of 2^-11 in [-1, 1], one rounding; the clamp modifier
+is max(0, x) as for the add; scripts/ubench/fma_opsel.hip checks both and the issue rate, which
+equals v_pk_add_f16's).  So a profile row costs 7.5 VALU (Gotoh) / 5.5 (merged) per 2 cells like
+the DNA letter-pair table, without a table per letter pair.
+
 No two dependent packed (VOP3P) ops are adjacent (gfx950 needs a wait state between them;
 v_perm_b32 -> VOP3P needs none), so a block needs no s_nop inside; LLVM adds one wait state
 per asm block.  D alternates between Da/Db by row parity.  The last block of a column ends
@@ -51,6 +62,19 @@ def perm(mode, i):
     return f"v_perm_b32 %[S1], %[hi{w}], %[lo{w}], {k}"
 
 
+FMA_SEL = "op_sel:[0,1,0] op_sel_hi:[1,0,1]"
+
+
+def next_d(mode, i, dnext, clamp):
+    """the diagonal add of block row i + 1 (into dnext) for mode F / pair / L,P (S1)"""
+    c = " clamp" if clamp else ""
+    if mode == "F":
+        return [f"v_pk_fma_f16 {dnext}, %[fa{i}], %[fb{i}], %[h{i}] {FMA_SEL}{c}"]
+    if mode == "pair":
+        return [f"v_pk_add_f16 {dnext}, %[h{i}], %[p{i}]{c}"]
+    return [perm(mode, i), f"v_pk_add_f16 {dnext}, %[h{i}], %[S1]{c}"]
+
+
 def merged_block(mode, zdown, last, nrows=8):
     """Merged gap matrix with the clamp modifier: values are f16 multiples of 2^-11, so the
     [0, 1] clamp of v_pk_add_f16 is max(0, x) on everything the exact path reaches, and the
@@ -66,11 +90,10 @@ def merged_block(mode, zdown, last, nrows=8):
         final = last and i == nrows - 1
         if final:
             nxt = ["s_nop 0"]
-        elif mode == "pair":
-            nxt = [f"v_pk_add_f16 {dnext}, %[h{i}], %[p{i}] clamp"]
         else:
-            out.append(perm(mode, i))
-            nxt = [f"v_pk_add_f16 {dnext}, %[h{i}], %[S1] clamp"]
+            nd = next_d(mode, i, dnext, True)
+            out += nd[:-1]  # (the perm of the L / P lookups)
+            nxt = nd[-1:]
         if i == 0:
             out += nxt
             out.append(f"v_pk_add_f16 %[DN], {dcur}, %[no]")
@@ -96,11 +119,8 @@ def gotoh_block(mode, last, nrows=8):
         final = last and i == nrows - 1
         if final:
             out.append("s_nop 0")
-        elif mode == "pair":
-            out.append(f"v_pk_add_f16 {dnext}, %[h{i}], %[p{i}]")
         else:
-            out.append(perm(mode, i))
-            out.append(f"v_pk_add_f16 {dnext}, %[h{i}], %[S1]")
+            out += next_d(mode, i, dnext, False)
         out.append(f"v_pk_maximum3_f16 %[h{i}], {dcur}, %[t{i}], %[F]")
         out.append(f"v_pk_add_f16 %[EN], %[t{i}], %[ne]")
         out.append(f"v_pk_add_f16 %[HN], %[h{i}], %[noe]")
@@ -160,6 +180,10 @@ def main():
     parts.append("#define SWK_F16PAIRG_F \\\n" + fmt(pair_gotoh_block(True, False)))
     parts.append("#define SWK_F16PAIRG_M \\\n" + fmt(pair_gotoh_block(False, False)))
     parts.append("#define SWK_F16PAIRG_L \\\n" + fmt(pair_gotoh_block(False, True)))
+    # mode F (profile words {s, 1.0}: one packed FMA per row, no lookup), 8-row blocks
+    for last in (0, 1):
+        parts.append(f"#define SWK_F16M_F_Z0_L{last} \\\n" + fmt(merged_block("F", 0, last)))
+        parts.append(f"#define SWK_F16G_F_L{last} \\\n" + fmt(gotoh_block("F", last)))
     # 4- and 2-row single blocks (the wave kernel's K = 4, and K = 2 of its split tail: a
     # whole column in one block)
     for nr in (4, 2):

@@ -1665,6 +1665,10 @@ struct ProfLookupK16 {  // f16 profile, 2-byte entries: word k = rows 2k, 2k+1 o
   }
 };
 template <int K>
+struct ProfLookupF {  // f16 profile words {s, 1.0}, one per row: a[r] target A's, b[r] B's
+  uint32_t a[K], b[K];  // (the column asm adds them with one op_sel FMA, gen_f16_rows.py "F")
+};
+template <int K>
 struct LaneLutLookup {  // per-lane row LUTs (the lane's own query rows) in VGPRs
   const uint32_t (&lut)[K];
   uint32_t nv, selw;
@@ -1732,6 +1736,15 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
 #ifndef SWK_HALF_AHEAD
 #define SWK_HALF_AHEAD 1  // two-pairs wave kernel: profile words one step ahead
 #endif
+#ifndef SWK_HALF_FMA
+// two-pairs wave kernel: LDS profile words {s, 1.0} (4 B per letter and row) added with one
+// op_sel FMA per row (gen_f16_rows.py mode F) instead of 2-byte entries interleaved by a v_perm
+#define SWK_HALF_FMA 1
+#endif
+// the two-pairs kernel's LDS: the profile (letter stride SWK_HALF_LS bytes, 512 rows) and
+// each wave's code ring (profile offsets of both halves' targets, SWK_HALF_RING bytes a wave)
+#define SWK_HALF_LS (SWK_HALF_FMA ? 2048u : 1024u)
+#define SWK_HALF_RING (SWK_HALF_FMA ? 512u : 1024u)
 #define SWK_W_HT(B)                                                                           \
   [h0] "+v"(Hl[B]), [h1] "+v"(Hl[SWK_CLAMP(B + 1, K)]), [h2] "+v"(Hl[SWK_CLAMP(B + 2, K)]),    \
       [h3] "+v"(Hl[SWK_CLAMP(B + 3, K)]), [h4] "+v"(Hl[SWK_CLAMP(B + 4, K)]),                  \
@@ -1778,15 +1791,46 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
   [noe] "s"(noe), [ne] "s"(ne), [no] "s"(no), [up] "v"(up), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), \
       SWK_W_LH(B)
 #define SWK_W_IN_PG(B) [noe] "s"(noe), [ne] "s"(ne), [selA] "s"(0x05040100u), [selB] "s"(0x07060302u), SWK_W_LH(B)
+// mode F (ProfLookupF): block row i's next-row words a / b [B + i + 1]
+#define SWK_W_FAB(B)                                                                          \
+  [fa0] "v"(lk.a[SWK_CLAMP(B + 1, K)]), [fa1] "v"(lk.a[SWK_CLAMP(B + 2, K)]),                  \
+      [fa2] "v"(lk.a[SWK_CLAMP(B + 3, K)]), [fa3] "v"(lk.a[SWK_CLAMP(B + 4, K)]),              \
+      [fa4] "v"(lk.a[SWK_CLAMP(B + 5, K)]), [fa5] "v"(lk.a[SWK_CLAMP(B + 6, K)]),              \
+      [fa6] "v"(lk.a[SWK_CLAMP(B + 7, K)]), [fa7] "v"(lk.a[SWK_CLAMP(B + 8, K)]),              \
+      [fb0] "v"(lk.b[SWK_CLAMP(B + 1, K)]), [fb1] "v"(lk.b[SWK_CLAMP(B + 2, K)]),              \
+      [fb2] "v"(lk.b[SWK_CLAMP(B + 3, K)]), [fb3] "v"(lk.b[SWK_CLAMP(B + 4, K)]),              \
+      [fb4] "v"(lk.b[SWK_CLAMP(B + 5, K)]), [fb5] "v"(lk.b[SWK_CLAMP(B + 6, K)]),              \
+      [fb6] "v"(lk.b[SWK_CLAMP(B + 7, K)]), [fb7] "v"(lk.b[SWK_CLAMP(B + 8, K)])
+#define SWK_W_IN_FM(B) [noe] "s"(noe), [ne] "s"(ne), [no] "s"(no), [up] "v"(up), SWK_W_FAB(B)
+#define SWK_W_IN_FG(B) [noe] "s"(noe), [ne] "s"(ne), SWK_W_FAB(B)
 
 template <int K, bool GOTOH, class LK>
 __device__ __forceinline__ void column_f16_lane_asm(const LK& lk, u16x2& diag_, u16x2& upX_,
                                                     u16x2 (&Hl)[K], u16x2 (&Xl)[K],
                                                     u16x2& best_, uint32_t noe, uint32_t ne,
                                                     uint32_t no) {
+  constexpr bool FMA = std::is_same<LK, ProfLookupF<K>>::value;
   constexpr bool PROF = !std::is_same<LK, LaneLutLookup<K>>::value;
   uint32_t Da, Db, S1, X, DN, IN;
   u16x2 best = best_, up = upX_;
+  if constexpr (FMA) {
+    static_assert(K % 8 == 0, "mode F: 8-row blocks");
+    asm volatile("v_pk_fma_f16 %[Da], %[a0], %[b0], %[dg] op_sel:[0,1,0] op_sel_hi:[1,0,1] clamp"
+                 : [Da] "=&v"(Da)
+                 : [a0] "v"(lk.a[0]), [b0] "v"(lk.b[0]), [dg] "v"(diag_));
+#pragma unroll
+    for (int b = 0; b < K; b += 8) {
+      const bool last = b + 8 >= K;
+      if constexpr (GOTOH) {
+        if (last) asm volatile(SWK_F16G_F_L1 : SWK_W_OUT_G(b) : SWK_W_IN_FG(b));
+        else      asm volatile(SWK_F16G_F_L0 : SWK_W_OUT_G(b) : SWK_W_IN_FG(b));
+      } else {
+        if (last) asm volatile(SWK_F16M_F_Z0_L1 : SWK_W_OUT_M(b) : SWK_W_IN_FM(b));
+        else      asm volatile(SWK_F16M_F_Z0_L0 : SWK_W_OUT_M(b) : SWK_W_IN_FM(b));
+        up = Xl[SWK_CLAMP(b + 7, K)];
+      }
+    }
+  } else {
   if constexpr (PROF)
     asm volatile(
         "v_perm_b32 %[Da], %[h0], %[l0], %[sA]\n\t"
@@ -1831,6 +1875,7 @@ __device__ __forceinline__ void column_f16_lane_asm(const LK& lk, u16x2& diag_, 
       if constexpr (!GOTOH) up = Xl[SWK_CLAMP(b + 7, K)];
     }
   }
+  }  // (mode F)
   (void)Db; (void)S1; (void)X; (void)DN; (void)IN;
   upX_ = up;
   best_ = best;
@@ -2392,40 +2437,55 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
     }
     return min(x, pad) | (min(y, pad) << 8);
   };
-  // ring entries are 32-bit profile offsets (letter x PSb): a byte entry read in one step and
-  // used in the next would be masked again in every basic block it crosses
-  uint32_t* ring = reinterpret_cast<uint32_t*>(cring) + 128 * h;
-  const uint32_t* ring_l = ring + 32 - hl;  // step T + j reads ring_l[j] (A), ring_l[64 + j] (B)
+  // ring entries are profile offsets (letter x LS), 32-bit (or 16-bit loads that zero-extend):
+  // a byte entry read in one step and used in the next would be masked again in every basic
+  // block it crosses
+  typedef typename std::conditional<SWK_HALF_FMA != 0, uint16_t, uint32_t>::type RingT;
+  constexpr uint32_t LS = SWK_HALF_LS;
+  (void)PSb;
+  RingT* ring = reinterpret_cast<RingT*>(cring) + 128 * h;
+  const RingT* ring_l = ring + 32 - hl;  // step T + j reads ring_l[j] (A), ring_l[64 + j] (B)
   uint32_t ringprev = pad | pad << 8;
   const auto ring_write = [&](const uint32_t nc) __attribute__((always_inline)) {
-    ring[hl] = __umul24(ringprev & 0xFFu, PSb);
-    ring[32 + hl] = __umul24(nc & 0xFFu, PSb);
-    ring[64 + hl] = __umul24(ringprev >> 8, PSb);
-    ring[96 + hl] = __umul24(nc >> 8, PSb);
+    ring[hl] = (RingT)((ringprev & 0xFFu) * LS);
+    ring[32 + hl] = (RingT)((nc & 0xFFu) * LS);
+    ring[64 + hl] = (RingT)((ringprev >> 8) * LS);
+    ring[96 + hl] = (RingT)((nc >> 8) * LS);
     ringprev = nc;
   };
   ring_write(load_codes((uint32_t)hl));
   uint32_t ncode = load_codes(32u + hl);  // the next block's codes, one block ahead
-  // score_wave_half's LDS copy of the profile keeps each letter's rows 8-15 of every lane 512
-  // bytes after its rows 0-7: a ds_read_b128 of 16 lanes then covers all 64 banks
+  // score_wave_half's LDS copy of the profile keeps each letter's rows of every lane in 16-byte
+  // pieces 512 bytes apart (piece q of lane l at 512 q + 16 l): a ds_read_b128 of 16 lanes then
+  // covers all 64 banks.  2-byte entries: 2 pieces (rows 0-7, 8-15); FMA words: 4 pieces.
+  typedef typename std::conditional<SWK_HALF_FMA != 0, ProfLookupF<K>, ProfLookupK16<K>>::type LK;
   const uint8_t* plds = prof + hl * 16;
-  const auto load_prof = [&](ProfLookupK16<K>& lk, uint32_t oa, uint32_t ob)
-      __attribute__((always_inline)) {
+  const auto load_prof = [&](auto& lk, uint32_t oa, uint32_t ob) __attribute__((always_inline)) {
     const uint8_t* la = plds + oa;
     const uint8_t* lb = plds + ob;
+    if constexpr (SWK_HALF_FMA) {
 #pragma unroll
-    for (int q = 0; q < K / 8; ++q) {
-      const uint4 x = *reinterpret_cast<const uint4*>(la + 512 * q);
-      const uint4 y = *reinterpret_cast<const uint4*>(lb + 512 * q);
-      lk.lo[4 * q] = x.x; lk.lo[4 * q + 1] = x.y; lk.lo[4 * q + 2] = x.z; lk.lo[4 * q + 3] = x.w;
-      lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z; lk.hi[4 * q + 3] = y.w;
+      for (int q = 0; q < K / 4; ++q) {
+        const uint4 x = *reinterpret_cast<const uint4*>(la + 512 * q);
+        const uint4 y = *reinterpret_cast<const uint4*>(lb + 512 * q);
+        lk.a[4 * q] = x.x; lk.a[4 * q + 1] = x.y; lk.a[4 * q + 2] = x.z; lk.a[4 * q + 3] = x.w;
+        lk.b[4 * q] = y.x; lk.b[4 * q + 1] = y.y; lk.b[4 * q + 2] = y.z; lk.b[4 * q + 3] = y.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < K / 8; ++q) {
+        const uint4 x = *reinterpret_cast<const uint4*>(la + 512 * q);
+        const uint4 y = *reinterpret_cast<const uint4*>(lb + 512 * q);
+        lk.lo[4 * q] = x.x; lk.lo[4 * q + 1] = x.y; lk.lo[4 * q + 2] = x.z; lk.lo[4 * q + 3] = x.w;
+        lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z; lk.hi[4 * q + 3] = y.w;
+      }
     }
   };
   // AHEAD: a step's profile words are loaded during the step before (its ring entries two
   // steps before), so no step waits on its own LDS reads: with 3-4 waves per SIMD the other
   // waves hide less of that latency than the one-pair kernel's 6
   constexpr bool AHEAD = SWK_HALF_AHEAD != 0;
-  ProfLookupK16<K> lkn;
+  LK lkn;
   uint32_t nra, nrb;
   if constexpr (AHEAD) {
     load_prof(lkn, ring_l[0], ring_l[64]);
@@ -2438,7 +2498,7 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   // AHEAD: step t reads the ring entries of step t + 2 at rp = ring_l + ((t + 2) & 31); a pair
   // of steps from an even t never wraps, so one address per pair and immediate offsets.
   // SWK_HALF_UNROLL: steps per loop iteration (2 or 4)
-  const uint32_t* rp = ring_l;
+  const RingT* rp = ring_l;
   const auto step = [&](const int t, const bool even) __attribute__((always_inline)) {
     // the next 32 columns go in before they are read (AHEAD: two steps before)
     if ((AHEAD ? even : !even) && (t & 31) == (AHEAD ? 30 : 31)) {
@@ -2448,11 +2508,11 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
       asm volatile("" : "+s"(tt));
       ncode = load_codes(tt + (AHEAD ? 34u : 33u) + hl);
     }
-    ProfLookupK16<K> lk;
+    LK lk;
     if constexpr (AHEAD) {
       lk = lkn;
       load_prof(lkn, nra, nrb);
-      const uint32_t* np = rp + (t & 1);
+      const RingT* np = rp + (t & 1);
       nra = np[0];
       nrb = np[64];
       __builtin_amdgcn_sched_barrier(0);
@@ -2466,7 +2526,7 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (!AHEAD) {
       load_prof(lk, nra, nrb);
-      const uint32_t* np = ring_l + ((t + 1) & 31);  // the next step's profile offsets
+      const RingT* np = ring_l + ((t + 1) & 31);  // the next step's profile offsets
       nra = np[0];
       nrb = np[64];
     }
@@ -2685,8 +2745,21 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
       return;
     }
   }
-  {  // the K = 8 profile (64 16-byte row groups per letter, PS = 1024) with group 2l + q at
-     // 32 q + l: lane l of a half reads its rows 16 l .. 16 l + 15 as 16 + 16 bytes, 512 apart
+  if constexpr (SWK_HALF_FMA) {
+    // the K = 8 profile (2-byte entries, PS = 1024 bytes per letter) as words {s, 1.0}, 2048
+    // bytes per letter: row r = 16 l + 4 q + j (lane l of a half, piece q, word j) at word
+    // 128 q + 4 l + j, so lane l reads its 16 rows as 4 x 16 bytes, 512 apart
+    const uint32_t rows = (a.pad + 1) * 512;
+    const uint16_t* src = reinterpret_cast<const uint16_t*>(a.qtab);
+    for (uint32_t i = threadIdx.x; i < rows; i += blockDim.x) {
+      const uint32_t r = i & 511u;
+      reinterpret_cast<uint32_t*>(prof)[(i & ~511u) | ((r >> 2) & 3u) << 7 | (r >> 4) << 2 |
+                                        (r & 3u)] = src[i] | 0x3C000000u;
+    }
+    __syncthreads();
+  } else {  // the K = 8 profile (64 16-byte row groups per letter, PS = 1024) with group 2l + q
+            // at 32 q + l: lane l of a half reads its rows 16 l .. 16 l + 15 as 16 + 16 bytes,
+            // 512 apart
     const uint32_t words = (a.pad + 1) * a.PS / 16;
     const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
     for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
@@ -2697,7 +2770,7 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
   const size_t p0 = 2 * ((size_t)(blockIdx.x - a.split_blocks) * (blockDim.x >> 6) + wave);
   const size_t n = a.n;
   if (p0 >= a.main_pairs || 2 * p0 >= n) return;  // whole wave
-  uint8_t* cring = prof + (a.pad + 1) * a.PS + 1024 * wave;
+  uint8_t* cring = prof + (a.pad + 1) * SWK_HALF_LS + SWK_HALF_RING * wave;
   uint2 b = wave_two_pairs<GOTOH>(a, prof, cring, lane, p0);
   if (a.fb_qtab) {  // optimistic f16: re-score a flagged pair in u16 (whole wave, K = 8)
     const uint32_t m0 = __builtin_amdgcn_readlane(max(b.x, b.y), 0);
@@ -2728,7 +2801,9 @@ static hipError_t launch_wave_half(const ScoreArgs& a, uint32_t prof_bytes, hipS
   // hold every segment's profile
   const size_t blocks = a.split_blocks + ((size_t)a.main_pairs + 7) / 8 +
                         ((size_t)a.tail_pairs * a.split_P + 3) / 4;
-  size_t lds = (size_t)prof_bytes + 1024 * 4;  // + each wave's code rings (2 x 128 u32)
+  // the profile (prof_bytes at PS = 1024: 2 bytes per letter and row; SWK_HALF_FMA: 4) + each
+  // wave's code rings
+  size_t lds = (size_t)prof_bytes / 1024 * SWK_HALF_LS + SWK_HALF_RING * 4;
   if (a.split_blocks) lds = std::max<size_t>(lds, (size_t)a.split_words * 4 * a.split_P);
   if (a.tail_pairs) lds = std::max<size_t>(lds, (size_t)a.split_words * 4 * 4);  // a slice a wave
   auto fn = &score_wave_half<GOTOH>;
