@@ -60,6 +60,7 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t pS2, uint32_t ulen, uint32_t ustride, uint32_t nq,
                                        uint32_t qwords, size_t sstride, hipStream_t st);
 extern "C" unsigned swk_bal_slots(int W, uint32_t PS);
+extern "C" unsigned swk_wave_half_grid(int gotoh, uint32_t prof_bytes);
 extern "C" hipError_t swk_bal_plan_uniform(void* plan, uint32_t ntiles, uint32_t K, uint32_t G,
                                            hipStream_t st);
 extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* offs,
@@ -493,6 +494,9 @@ struct sw_bank {
   // balanced chunk ranges (swk_launch_pair_bal): the hand-off states and flags, the launch
   // generation the flags are compared with
   DevBuf<uint32_t> bal_state, bal_flag;
+  // balanced ranges of the two-pairs wave kernel: lane states, flags, their generation
+  DevBuf<uint32_t> wbal_state, wbal_flag;
+  uint32_t wbal_gen = 0;
   // range starts, 4 words each: a ragged batch's (the device sort writes them per call) or a
   // uniform batch's (swk_bal_plan_uniform for bal_key = {tiles, chunks per tile, grid}, kept
   // while the key holds; bal_key[0] = 0 when the sort overwrote them)

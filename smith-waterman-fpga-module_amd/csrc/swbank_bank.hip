@@ -182,6 +182,8 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->dsort.release();
   b->bal_state.release();
   b->bal_flag.release();
+  b->wbal_state.release();
+  b->wbal_flag.release();
   b->bal_plan.release();
   b->wtab.release();
   b->wtab16.release();

@@ -49,11 +49,19 @@ typedef struct SwkWaveSplit {
   unsigned* prog;
   unsigned* fault;
   unsigned poll_limit, stall;
+  /* balanced ranges of the two-pairs kernel (pairs = 0, P = 0; wbal_blocks > 0): a grid of
+   * wbal_grid blocks of 4 waves (the resident capacity), wbal_blocks 32-step blocks per unit,
+   * the hand-off flags ((4 wbal_grid + 1) words, zeroed once, compared with wbal_gen) and lane
+   * states ((4 wbal_grid + 1) x 36 x 64 words); fault / poll_limit / stall as above */
+  unsigned wbal_blocks, wbal_grid, wbal_gen;
+  unsigned* wbal_flag;
+  unsigned* wbal_state;
 } SwkWaveSplit;
 
 /* Bits of a launch's fault word (cross-workgroup hand-off waits that ran out). */
 #define SWK_FAULT_BAL 1u
 #define SWK_FAULT_TAIL 2u
+#define SWK_FAULT_WBAL 4u
 
 /* One chunk of a streamed host batch (uploaded before the launch): its first tile and the
  * offset of its codes in the device batch buffer.  Its code layout travels in a flag word per

@@ -776,8 +776,14 @@ struct ScoreArgs {
   // segment 0 of tail pair g - 1), so the time-out path runs.
   uint32_t* fault;
   uint32_t poll_limit, stall;
+  // two-pairs wave kernel, balanced ranges (wbal_blocks > 0: the grid is the resident capacity,
+  // G waves): the units (two pairs each, wbal_blocks 32-step blocks per unit) form one block
+  // sequence, wave g takes blocks [g UB / G, (g + 1) UB / G); a unit cut by a range boundary is
+  // scored in two visits, the head by wave g - 1 first, the tail by wave g last, the lane state
+  // handed over through bal_state (WBAL_WORDS x 64 words a wave) and bal_flag[g] = bal_gen
+  uint32_t wbal_blocks, wbal_grid;
 };
-static_assert(sizeof(ScoreArgs) == 360, "ScoreArgs layout (kernel argument block) changed");
+static_assert(sizeof(ScoreArgs) == 368, "ScoreArgs layout (kernel argument block) changed");
 
 // a hand-off wait ran out: mark the launch's fault word (a vector store to host memory; only the
 // host reads it, after the launch completed)
@@ -2378,10 +2384,22 @@ static hipError_t launch_wave(const ScoreArgs& a, uint32_t prof_bytes, hipStream
 //   bottom row through wave_shr): one v_cndmask per moved value.
 // Each half keeps its own 128-byte code ring (targets A, B: [previous 32 | next 32] columns).
 // Returns the half's two bests (every lane of the half).
+// Balanced ranges (score_wave_half, ScoreArgs.wbal_blocks): a visit may run steps [t0, t1) of
+// the unit only (t0, t1 multiples of 32): it starts from the lane state a predecessor's head
+// visit stored at sin and, when it stops before the unit's end, stores its own at sout (the
+// return value is then meaningless).  The state is complete: the lanes' rows {H, E/T}, the
+// running best, the diagonal above, the bottom row that moves down at the next step; the code
+// ring and the profile words of the first steps are rebuilt from the codes.
+constexpr int WBAL_WORDS = 2 * 16 + 4;  // state words per lane (K = 16)
 template <bool GOTOH>
 __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_t* prof,
-                                                uint8_t* cring, int lane, size_t p0) {
+                                                uint8_t* cring, int lane, size_t p0,
+                                                int t0 = 0, int t1 = 0x7FFFFFFF,
+                                                const uint32_t* sin = nullptr,
+                                                uint32_t* sout = nullptr) {
   constexpr int K = 16;
+  t0 = __builtin_amdgcn_readfirstlane(t0);  // (wave-uniform step bounds)
+  t1 = __builtin_amdgcn_readfirstlane(t1);
   const int h = lane >> 5, hl = lane & 31;
   const size_t pair = p0 + (size_t)h;
   const size_t n = a.n;
@@ -2421,6 +2439,20 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   }
   u16x2 best = {0, 0}, prevUpH = H0;
   uint32_t botH = as_u32(H0), botX = as_u32(X0);
+  if (sin) {  // a tail visit: the predecessor's lane state (sc1 loads, word i at i x 64 + lane)
+    const uint32_t* sp = sin + lane;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      Hl[k] = as_u16x2(__hip_atomic_load(sp + k * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      Xl[k] = as_u16x2(
+          __hip_atomic_load(sp + (K + k) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    best = as_u16x2(__hip_atomic_load(sp + 2 * K * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    prevUpH = as_u16x2(
+        __hip_atomic_load(sp + (2 * K + 1) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    botH = __hip_atomic_load(sp + (2 * K + 2) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    botX = __hip_atomic_load(sp + (2 * K + 3) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   const bool top = hl == 0;  // row -1 of this half's pair
   // the codes of column c of this half's targets (pad past the end) as {A, B << 8}
   const auto load_codes = [&](const uint32_t c) __attribute__((always_inline)) -> uint32_t {
@@ -2453,8 +2485,12 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
     ring[96 + hl] = (RingT)((nc >> 8) * LS);
     ringprev = nc;
   };
-  ring_write(load_codes((uint32_t)hl));
-  uint32_t ncode = load_codes(32u + hl);  // the next block's codes, one block ahead
+  // the ring holds the 32-column blocks k - 1 and k while steps 32 k .. 32 k + 31 run (k = t0 /
+  // 32 at the start of a visit); ncode the next block's codes, one block ahead
+  const uint32_t c0 = (uint32_t)t0;
+  if (c0) ringprev = load_codes(c0 - 32u + hl);
+  ring_write(load_codes(c0 + hl));
+  uint32_t ncode = load_codes(c0 + 32u + hl);
   // score_wave_half's LDS copy of the profile keeps each letter's rows of every lane in 16-byte
   // pieces 512 bytes apart (piece q of lane l at 512 q + 16 l): a ds_read_b128 of 16 lanes then
   // covers all 64 banks.  2-byte entries: 2 pieces (rows 0-7, 8-15); FMA words: 4 pieces.
@@ -2535,14 +2571,29 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
     botH = as_u32(Hl[K - 1]);
     botX = as_u32(upX);
   };
-  const int nsteps = Lmax + 31;
-  for (int t = 0; t < nsteps; t += SWK_HALF_UNROLL) {
+  const int nsteps = min(Lmax + 31, t1);
+  for (int t = t0; t < nsteps; t += SWK_HALF_UNROLL) {
 #pragma unroll
     for (int u = 0; u < SWK_HALF_UNROLL; u += 2) {
       rp = ring_l + ((t + u + 2) & 31);
       step(t + u, true);
       step(t + u + 1, false);
     }
+  }
+  if (sout) {  // a head visit: the lane state for the successor's tail visit (sc1 stores)
+    uint32_t* sp = sout + lane;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      __hip_atomic_store(sp + k * 64, as_u32(Hl[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sp + (K + k) * 64, as_u32(Xl[k]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __hip_atomic_store(sp + 2 * K * 64, as_u32(best), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(sp + (2 * K + 1) * 64, as_u32(prevUpH), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(sp + (2 * K + 2) * 64, botH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(sp + (2 * K + 3) * 64, botX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint2(0u, 0u);
   }
   uint32_t bx = (uint32_t)f16_unscore(best.x), by = (uint32_t)f16_unscore(best.y);
 #pragma unroll
@@ -2723,6 +2774,10 @@ __device__ __forceinline__ void wave_tail_seg(const ScoreArgs& a, uint8_t* wlds,
 // above the optimistic f16 threshold is re-scored in u16 by the whole wave with the one-pair
 // K = 8 code and table (rare).
 template <bool GOTOH>
+__device__ __forceinline__ void wave_half_finish(const ScoreArgs& a, uint2 b, int lane,
+                                                 size_t p0);
+
+template <bool GOTOH>
 __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
@@ -2767,11 +2822,71 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
     __syncthreads();
   }
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const size_t p0 = 2 * ((size_t)(blockIdx.x - a.split_blocks) * (blockDim.x >> 6) + wave);
-  const size_t n = a.n;
-  if (p0 >= a.main_pairs || 2 * p0 >= n) return;  // whole wave
   uint8_t* cring = prof + (a.pad + 1) * SWK_HALF_LS + SWK_HALF_RING * wave;
-  uint2 b = wave_two_pairs<GOTOH>(a, prof, cring, lane, p0);
+  // Balanced ranges (ScoreArgs.wbal_blocks): wave g of the G resident waves scores
+  // blocks [A_g, A_g+1) of the unit-major sequence of 32-step blocks, A_g = g U B / G (U units
+  // of two pairs, B blocks each), so every wave slot gets the same number of steps whatever
+  // U / G is -- the ScoreBank's answer to an uneven batch end is the first free module
+  // (ScoreBank_v2.v:142-148,164-165); here no slot idles while another runs one unit more.  The
+  // cut unit at the range end is scored first (the head, lane state out), the cut unit at the
+  // range start last (the tail, after the predecessor's flag).  U >= G (host): a range holds at
+  // least one unit, so a unit is cut at most once and every wait points to an earlier wave.
+  // Without: one unit per wave.  One call site of wave_two_pairs for every visit (an inlined
+  // copy per visit kind spills).
+  const uint32_t G = gridDim.x * 4,
+                 g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (uint32_t)wave);
+  uint32_t u0 = 0, u1 = 0, whole0 = 0;
+  int b0 = 0, b1 = 0, nvis = 1;
+  if (a.wbal_blocks) {
+    const uint64_t U = ((uint64_t)a.main_pairs + 1) / 2, B = a.wbal_blocks, UB = U * B;
+    const uint64_t A0 = UB * g / G, A1 = UB * (g + 1) / G;
+    u0 = (uint32_t)(A0 / B);
+    u1 = (uint32_t)(A1 / B);
+    b0 = __builtin_amdgcn_readfirstlane((int)(A0 % B));
+    b1 = __builtin_amdgcn_readfirstlane((int)(A1 % B));
+    whole0 = b0 ? u0 + 1 : u0;  // whole units [whole0, u1)
+    nvis = (b1 ? 1 : 0) + (int)(u1 - whole0) + (b0 ? 1 : 0);
+  } else {
+    whole0 = (blockIdx.x - a.split_blocks) * 4 + (uint32_t)wave;
+    if (2 * (size_t)whole0 >= a.main_pairs || 4 * (size_t)whole0 >= a.n) return;  // whole wave
+  }
+  const size_t sw = (size_t)WBAL_WORDS * 64;
+  for (int v = 0; v < nvis; ++v) {
+    const bool head = b1 && v == 0, tail = b0 && v == nvis - 1;
+    const uint32_t unit = __builtin_amdgcn_readfirstlane(
+        head ? u1 : tail ? u0 : whole0 + (uint32_t)(v - (b1 ? 1 : 0)));
+    if (tail) {  // wave g - 1's head is done (a bounded poll, as DESIGN §3.8)
+      uint32_t it = 0;
+      for (; it < a.poll_limit; ++it) {
+        if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                a.bal_flag + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == a.bal_gen)
+          break;
+        __builtin_amdgcn_s_sleep(8);
+      }
+      if (it == a.poll_limit && lane == 0) report_fault(a.fault, SWK_FAULT_WBAL);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const uint2 b = wave_two_pairs<GOTOH>(
+        a, prof, cring, lane, 2 * (size_t)unit, tail ? 32 * b0 : 0, head ? 32 * b1 : 0x7FFFFFFF,
+        tail ? a.bal_state + (size_t)g * sw : nullptr,
+        head ? a.bal_state + (size_t)(g + 1) * sw : nullptr);
+    if (head) {  // the lane state is out: wave g + 1 may take the unit on
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0 && g + 1 != a.stall)  // (stall: a test hook)
+        __hip_atomic_store(a.bal_flag + g + 1, a.bal_gen, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      wave_half_finish<GOTOH>(a, b, lane, 2 * (size_t)unit);
+    }
+  }
+}
+
+// The end of a two-pairs unit: a pair above the optimistic f16 threshold is re-scored in u16 by
+// the whole wave (K = 8, rare), then each half's lane 0 writes its pair's two scores.
+template <bool GOTOH>
+__device__ __forceinline__ void wave_half_finish(const ScoreArgs& a, uint2 b, int lane,
+                                                 size_t p0) {
+  const size_t n = a.n;
   if (a.fb_qtab) {  // optimistic f16: re-score a flagged pair in u16 (whole wave, K = 8)
     const uint32_t m0 = __builtin_amdgcn_readlane(max(b.x, b.y), 0);
     const uint32_t m1 = __builtin_amdgcn_readlane(max(b.x, b.y), 32);
@@ -2795,15 +2910,21 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
   }
 }
 
+
+// the main blocks' LDS: the profile (prof_bytes at PS = 1024: 2 bytes per letter and row;
+// SWK_HALF_FMA: 4) + each wave's code rings
+static size_t wave_half_lds(uint32_t prof_bytes) {
+  return (size_t)prof_bytes / 1024 * SWK_HALF_LS + SWK_HALF_RING * 4;
+}
+
 template <bool GOTOH>
 static hipError_t launch_wave_half(const ScoreArgs& a, uint32_t prof_bytes, hipStream_t st) {
   // 4 waves per block = 8 pairs, sharing one LDS copy of the profile; the split tail's blocks
   // hold every segment's profile
-  const size_t blocks = a.split_blocks + ((size_t)a.main_pairs + 7) / 8 +
-                        ((size_t)a.tail_pairs * a.split_P + 3) / 4;
-  // the profile (prof_bytes at PS = 1024: 2 bytes per letter and row; SWK_HALF_FMA: 4) + each
-  // wave's code rings
-  size_t lds = (size_t)prof_bytes / 1024 * SWK_HALF_LS + SWK_HALF_RING * 4;
+  const size_t blocks = a.wbal_blocks ? (size_t)a.wbal_grid
+                                      : a.split_blocks + ((size_t)a.main_pairs + 7) / 8 +
+                                            ((size_t)a.tail_pairs * a.split_P + 3) / 4;
+  size_t lds = wave_half_lds(prof_bytes);
   if (a.split_blocks) lds = std::max<size_t>(lds, (size_t)a.split_words * 4 * a.split_P);
   if (a.tail_pairs) lds = std::max<size_t>(lds, (size_t)a.split_words * 4 * 4);  // a slice a wave
   auto fn = &score_wave_half<GOTOH>;
@@ -2947,6 +3068,20 @@ extern "C" hipError_t swk_bal_plan_uniform(void* plan, uint32_t ntiles, uint32_t
   hipLaunchKernelGGL(swk::bal_plan_uniform, dim3(1), dim3(256), 0, st, static_cast<uint4*>(plan),
                      ntiles, K, G);
   return hipGetLastError();
+}
+
+// Resident 4-wave blocks of the two-pairs kernel (the balanced grid) for a profile of
+// prof_bytes at PS = 1024 (0 when the occupancy query fails).
+extern "C" unsigned swk_wave_half_grid(int gotoh, uint32_t prof_bytes) {
+  const void* fn = gotoh ? reinterpret_cast<const void*>(&swk::score_wave_half<true>)
+                         : reinterpret_cast<const void*>(&swk::score_wave_half<false>);
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+      hipSuccess)
+    return 0;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  const int occ = swk::cached_occupancy(fn, 256, swk::wave_half_lds(prof_bytes), dev, &cus);
+  return occ > 0 && cus > 0 ? (unsigned)(occ * cus) : 0u;
 }
 
 extern "C" unsigned swk_bal_slots(int W, uint32_t PS) {
@@ -3148,7 +3283,21 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
   a.ustride = ustride;
   const size_t pairs = (n + 1) / 2;
   a.main_pairs = (uint32_t)pairs;
-  if (split && split->pairs > 0 && split->P == 8) {
+  if (split && split->wbal_blocks > 0) {
+    // balanced ranges of the two-pairs kernel (ScoreArgs.wbal_*): no split or tail
+    if (!half || K != 8 || edge_in || edge_out || accum || split->pairs || !split->wbal_grid ||
+        !split->wbal_flag || !split->wbal_state || !split->fault || split->poll_limit == 0 ||
+        (pairs + 1) / 2 < 4ull * split->wbal_grid || pairs > 0xFFFFFFFFull)
+      return hipErrorInvalidValue;
+    a.wbal_blocks = split->wbal_blocks;
+    a.wbal_grid = split->wbal_grid;
+    a.bal_flag = split->wbal_flag;
+    a.bal_state = split->wbal_state;
+    a.bal_gen = split->wbal_gen;
+    a.fault = split->fault;
+    a.poll_limit = split->poll_limit;
+    a.stall = split->stall;
+  } else if (split && split->pairs > 0 && split->P == 8) {
     // the segmented tail of the two-pairs kernel (ScoreArgs.tail_*)
     if (!half || K != 8 || edge_in || edge_out || accum || split->pairs > pairs ||
         pairs > 0xFFFFFFFFull || !split->prog || split->cols == 0 || !split->fault ||

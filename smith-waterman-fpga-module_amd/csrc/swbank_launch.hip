@@ -165,7 +165,37 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
     SwkWaveSplit sp{};
     const size_t pairs = (n + 1) / 2;
     const int sforce = env_int("SWBANK_WAVE_SPLIT", -1);
-    if (b->sK[0] && b->wsegs == 1 && n == wspan && pairs <= 0xFFFFFFFFull) {
+    // Balanced ranges (two pairs per wave, equal target lengths): every resident
+    // wave slot scores the same number of 32-step blocks of the unit sequence, a unit cut by a
+    // range boundary handed between two waves, instead of a tail of pairs % slots pairs.  Needs
+    // at least one unit (two pairs) per slot and a remainder; SWBANK_WAVE_BAL=0 disables.
+    bool wbal = false;
+    if (half && b->wsegs == 1 && n == wspan && !b->no_handoff && (ustride || min_len == max_len) &&
+        sforce < 0 && pairs <= 0xFFFFFFFFull && env_int("SWBANK_WAVE_BAL", 1) != 0) {
+      const unsigned grid = swk_wave_half_grid(gotoh ? 1 : 0, (b->pad + 1) * b->wPS16);
+      const size_t U = (pairs + 1) / 2, G = 4 * (size_t)grid;
+      uint32_t* fw = grid ? fault_word(b) : nullptr;
+      if (grid && fw && U >= G && U % G) {
+        const size_t sw = (G + 1) * 36 * 64;  // (WBAL_WORDS per lane)
+        HIPOK(b, b->wbal_state.reserve(sw));
+        if (b->wbal_flag.cap < G + 1) {  // zeroed once: flags carry wbal_gen
+          HIPOK(b, b->wbal_flag.reserve(G + 1));
+          HIPOK(b, hipMemsetAsync(b->wbal_flag.p, 0, b->wbal_flag.cap * 4, st));
+        }
+        sp.wbal_blocks = (max_len + 31 + 31) / 32;
+        sp.wbal_grid = grid;
+        sp.wbal_gen = ++b->wbal_gen;
+        sp.wbal_flag = b->wbal_flag.p;
+        sp.wbal_state = b->wbal_state.p;
+        sp.fault = fw + (b->host_call ? 1 : 0);
+        sp.poll_limit = poll_limit(1u << 23);
+        sp.stall = (unsigned)std::max(0, env_int("SWBANK_STALL", 0));
+        wbal = true;
+        const size_t L = strlen(b->last_kernel);
+        snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " balanced grid=%u", grid);
+      }
+    }
+    if (!wbal && b->sK[0] && b->wsegs == 1 && n == wspan && pairs <= 0xFFFFFFFFull) {
       const size_t simds = 4 * (size_t)std::max(b->cus, 1);
       const size_t units = half ? 2 * simds : simds;  // pairs per layer of one wave per SIMD
       size_t T = 0;
