@@ -57,7 +57,8 @@ extern "C" {
  *        batches and query sets.
  * ABI 5: SW_ERR_TIMEOUT and sw_bank_sync (device-side hand-off waits that run out fail the call,
  *        ≙ the CAPI host failing on the AFU's error bits, main_test.c:64-100); sw_bank_counters
- *        is the two-argument ABI-3 form again, sw_bank_counters_ex takes the struct size. */
+ *        is the two-argument ABI-3 form again, sw_bank_counters_ex takes the struct size;
+ *        multi-device device calls copy each device's share into its own HBM. */
 #define SWBANK_ABI_VERSION 5
 
 typedef int32_t sw_status;
@@ -159,11 +160,12 @@ sw_status sw_score_batch(sw_bank *bank, const uint8_t *residues, size_t residues
  * lengths differ, then longest first (an on-device length sort).  d_scores receives int32
  * scores in input order.  With d_ids (device, may be NULL) the call also records the batch's
  * best hit on the device (sw_batch_best); without, it records nothing.  Nothing is copied to
- * or from the host.  On a multi-device bank (ABI 4) the buffers and the stream belong to the
- * root device (devices[0]): device d scores the contiguous range [n*d/D, n*(d+1)/D) reading the
- * root's buffers through peer access and writes its scores into d_scores, its work ordered
- * after the caller's stream and the caller's stream after it (SW_ERR_UNSUPPORTED when a device
- * cannot access the root's memory).
+ * or from the host.  On a multi-device bank (ABI 5) the buffers and the stream belong to the
+ * root device (devices[0]): the batch is ordered longest first on the root (when its lengths
+ * differ) and dealt round robin over the devices (length-balanced); each device copies its
+ * share into its own HBM (max_len + 12 bytes per target over xGMI), scores it there and copies
+ * its int32 scores back, and the root writes them to d_scores in input order; the devices'
+ * work is ordered after the caller's stream and the caller's stream after it (n < 2^32).
  * Device memory is not validated: the caller keeps every target inside d_residues
  * (d_offsets[k] + d_lens[k] <= its size) and every d_lens[k] <= max_len. */
 sw_status sw_score_batch_device(sw_bank *bank, const uint8_t *d_residues,
@@ -205,7 +207,8 @@ sw_status sw_load_query_record(sw_bank *bank, const void *record);
  * best hit (sw_batch_best) carries the record's ID.  Multi-device banks deal the records. */
 sw_status sw_score_records(sw_bank *bank, const void *records, size_t n, int32_t *scores_out);
 /* Device-resident records (n x 64 B) -> device scores, asynchronous on `stream` (a
- * multi-device bank: contiguous ranges per device, as sw_score_batch_device). */
+ * multi-device bank: device d copies the contiguous range [n*d/D, n*(d+1)/D) of records into
+ * its own HBM and writes its scores into d_scores). */
 sw_status sw_score_records_device(sw_bank *bank, const void *d_records, size_t n,
                                   int32_t *d_scores, void *stream);
 

@@ -487,9 +487,11 @@ struct sw_bank {
   unsigned pool_threads = 0; // feeder threads (0: host_threads(); children share the host)
   DevBuf<int32_t> grecv;
   PinBuf hrecv;
-  // device batches on a multi-device bank (multi_device): every child's kernels read the
-  // caller's buffers on the root device through peer access, enabled once (peer_ready);
-  // ev_join: a child's work on its stream is done (the caller's stream waits on it);
+  // device batches on a multi-device bank (multi_device): the caller's batch on the root is
+  // dealt into a staging buffer (res / offs / lens of the parent, on the root), each child
+  // copies its region into its own buffers (peer access enabled once, peer_ready) and its
+  // scores back (grecv); ev_join: the staging is ready (parent) / a child's work on its stream
+  // is done (child; the caller's stream waits on it); ev_used (parent): the call's scatter;
   // best_root: the last device call's best hit is tracked by kids[0]
   // balanced chunk ranges (swk_launch_pair_bal): the hand-off states and flags, the launch
   // generation the flags are compared with

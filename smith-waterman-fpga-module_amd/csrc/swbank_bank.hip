@@ -145,13 +145,20 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
     const Rccl& r = rccl();
     for (void* c : b->comms) (void)r.commDestroy(static_cast<ncclComm_t>(c));
     (void)hipSetDevice(b->device);
+    if (b->ev_used) (void)hipEventSynchronize(b->ev_used);  // the last device call's scatter
     if (b->ev_join) (void)hipEventDestroy(b->ev_join);
+    if (b->ev_used) (void)hipEventDestroy(b->ev_used);
     for (sw_bank* k : b->kids) sw_bank_destroy(k);
     b->dpool.reset();
     b->pool.reset();
     (void)hipSetDevice(b->device);
     b->grecv.release();
     b->hrecv.release();
+    b->res.release();  // the device-call deal's staging (multi_device)
+    b->offs.release();
+    b->lens.release();
+    b->dperm.release();
+    b->dsort.release();
     delete b;
     return;
   }
@@ -283,6 +290,14 @@ extern "C" sw_status sw_bank_sync(sw_bank* b) {
         (void)take_fault(b, 0);  // (clear the other devices' words too)
         return fail(b, st, "device %d: %s", k->device, k->err);
       }
+    }
+    if (b->ev_used) {  // the device-call deal's scatter on the root (multi_device)
+      int cur = -1;
+      HIPOK(b, hipGetDevice(&cur));
+      hipError_t e = hipSetDevice(b->device);
+      if (e == hipSuccess) e = hipEventSynchronize(b->ev_used);
+      (void)hipSetDevice(cur);
+      HIPOK(b, e);
     }
     return SW_OK;
   }

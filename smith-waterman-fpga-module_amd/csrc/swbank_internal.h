@@ -74,6 +74,21 @@ typedef struct SwkStreamChunk {
 } SwkStreamChunk;
 #define SWK_STREAM_ABORT 0xFFFFFFFFu
 
+/* The deal of a device batch over the devices of a multi-device bank (swk_deal_gather /
+ * swk_deal_scatter): position p of the visiting order (a permutation, or the identity) goes to
+ * device p % D as its target p / D, copied into that device's region of a staging buffer at a
+ * fixed stride of `stride` bytes (offsets rebased, lengths kept); its scores come back from
+ * scores[d] (nq rows, cnt[d] apart). */
+#define SWK_DEAL_MAX 16
+typedef struct SwkDeal {
+  unsigned D, stride;
+  unsigned char* codes[SWK_DEAL_MAX];
+  unsigned long long* offs[SWK_DEAL_MAX];
+  unsigned* lens[SWK_DEAL_MAX];
+  const int* scores[SWK_DEAL_MAX];
+  unsigned long long cnt[SWK_DEAL_MAX];
+} SwkDeal;
+
 #ifdef __cplusplus
 /* (declared here so the definition in swbank_kernels.hip and the call in swbank_device.hip are
  * checked against one signature) */
@@ -84,6 +99,15 @@ extern "C" hipError_t swk_launch_stream(int R, int gotoh, int f16, int pair, con
                                         uint32_t S, uint32_t O, uint32_t E, uint32_t PS,
                                         uint32_t pad, int W, int32_t* scores, uint32_t pS1,
                                         uint32_t pS2, hipStream_t st);
+/* perm / ident: the device sort's order (ident[0] != 0: the identity), or perm = nullptr */
+extern "C" hipError_t swk_deal_gather(const uint8_t* res, const uint64_t* offs,
+                                      const uint32_t* lens, const uint32_t* perm,
+                                      const uint32_t* ident, size_t n, const SwkDeal* deal,
+                                      hipStream_t st);
+/* out[q * sstride + t] = scores[d][q * cnt[d] + i] for every position p = i D + d of target t */
+extern "C" hipError_t swk_deal_scatter(const uint32_t* perm, const uint32_t* ident, size_t n,
+                                       unsigned nq, size_t sstride, const SwkDeal* deal,
+                                       int32_t* out, hipStream_t st);
 #endif
 
 #endif

@@ -3248,6 +3248,71 @@ extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, s
   return e;
 }
 
+// ---- the deal of a multi-device bank's device batch (swbank_multi.hip) -------------------
+namespace swk {
+__device__ __forceinline__ size_t deal_target(const uint32_t* perm, bool id, size_t p) {
+  return id ? p : (size_t)perm[p];
+}
+// one wave per position (grid-stride): the target's bytes, lane-strided, to its device's slot
+__global__ void __launch_bounds__(256) deal_gather(const uint8_t* res, const uint64_t* offs,
+                                                   const uint32_t* lens, const uint32_t* perm,
+                                                   const uint32_t* ident, size_t n,
+                                                   const SwkDeal dl) {
+  const int lane = threadIdx.x & 63;
+  const size_t w0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const size_t nw = ((size_t)gridDim.x * blockDim.x) >> 6;
+  const bool id = !perm || (ident && *ident != 0);
+  for (size_t p = w0; p < n; p += nw) {
+    const size_t t = deal_target(perm, id, p);
+    const unsigned d = (unsigned)(p % dl.D);
+    const size_t i = p / dl.D;
+    const uint32_t L = lens[t];
+    const uint8_t* src = res + offs[t];
+    uint8_t* dst = dl.codes[d] + i * dl.stride;
+    for (uint32_t j = lane; j < L; j += 64) dst[j] = src[j];
+    if (lane == 0) {
+      dl.offs[d][i] = (unsigned long long)i * dl.stride;
+      dl.lens[d][i] = L;
+    }
+  }
+}
+__global__ void __launch_bounds__(256) deal_scatter(const uint32_t* perm, const uint32_t* ident,
+                                                    size_t n, unsigned nq, size_t sstride,
+                                                    const SwkDeal dl, int32_t* out) {
+  const bool id = !perm || (ident && *ident != 0);
+  const size_t total = n * nq;
+  for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
+       x += (size_t)gridDim.x * blockDim.x) {
+    const size_t q = x / n, p = x % n;
+    const unsigned d = (unsigned)(p % dl.D);
+    out[q * sstride + deal_target(perm, id, p)] = dl.scores[d][q * dl.cnt[d] + p / dl.D];
+  }
+}
+}  // namespace swk
+
+extern "C" hipError_t swk_deal_gather(const uint8_t* res, const uint64_t* offs,
+                                      const uint32_t* lens, const uint32_t* perm,
+                                      const uint32_t* ident, size_t n, const SwkDeal* deal,
+                                      hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (!deal || deal->D == 0 || deal->D > SWK_DEAL_MAX || deal->stride == 0) return hipErrorInvalidValue;
+  const size_t blocks = std::min<size_t>((n + 3) / 4, 8192);
+  hipLaunchKernelGGL(swk::deal_gather, dim3((unsigned)blocks), dim3(256), 0, st, res, offs, lens,
+                     perm, ident, n, *deal);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t swk_deal_scatter(const uint32_t* perm, const uint32_t* ident, size_t n,
+                                       unsigned nq, size_t sstride, const SwkDeal* deal,
+                                       int32_t* out, hipStream_t st) {
+  if (n == 0 || nq == 0) return hipSuccess;
+  if (!deal || deal->D == 0 || deal->D > SWK_DEAL_MAX) return hipErrorInvalidValue;
+  const size_t blocks = std::min<size_t>((n * nq + 255) / 256, 8192);
+  hipLaunchKernelGGL(swk::deal_scatter, dim3((unsigned)blocks), dim3(256), 0, st, perm, ident, n,
+                     nq, sstride, *deal, out);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t swk_flag_high(const int32_t* scores, size_t n, int32_t thresh,
                                     uint32_t* idx, uint32_t* count, hipStream_t st) {
   hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), st);

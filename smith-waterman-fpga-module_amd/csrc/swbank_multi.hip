@@ -263,27 +263,40 @@ sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_t* scor
 }
 
 // Device buffers on a multi-device bank (the caller's buffers live on the root device,
-// devices[0]; ≙ the ScoreBank's MODULES all reading the one target stream, ScoreBank_v2.v:76-148):
-// device d scores the contiguous range [n d / D, n (d + 1) / D) straight from the root's buffers
-// (peer access over xGMI) and writes its scores into the root's d_scores, so nothing is staged
-// or gathered.  Asynchronous: every device's work waits for the caller's stream (an event) and
-// the caller's stream waits for every device's (one event each).  A query set is scored by every
-// device against its range (rows n apart in d_scores, as on one device).  With d_ids the batch
-// best hit is tracked on the root after all ranges (sw_batch_best).
+// devices[0]; ≙ the ScoreBank's MODULES, each latching its own copy of its target before
+// scoring it, ScoreBank_v2.v:117-137, SM_Feeder3.v:104-182).  Every device scores its share
+// from its OWN HBM: xGMI carries one bulk copy in and the scores out, never the kernel's reads.
+//  1. the visiting order: a ragged batch is sorted longest first on the root (swk_sort_lens),
+//     and position p goes to device p % D -- the length-balanced deal of the host path
+//     (multi_batch); a batch of one length keeps its order;
+//  2. one gather kernel on the root copies each device's targets into its region of a staging
+//     buffer at a fixed stride of max_len bytes (offsets rebased, lengths kept);
+//  3. device d copies its region into its own buffers (hipMemcpyPeerAsync on its stream: codes
+//     cnt_d x max_len bytes + 12 bytes per target), scores them there (launch / launch_set) and
+//     copies its nq x cnt_d int32 scores back into the root's receive buffer;
+//  4. one scatter kernel on the root writes them to d_scores in input order.
+// CAPI records (fixed 64 bytes, contiguous ranges) skip 1, 2 and 4: each device copies its
+// range of records and writes its scores straight into the caller's d_scores.
+// Asynchronous: the devices' work waits for the caller's stream (an event after the gather),
+// the caller's stream waits for every device (an event each) before the scatter; the next call
+// reuses the staging buffers only after this call's scatter (ev_done).  A device listed twice,
+// or the root itself, copies within its own memory.  With d_ids the batch best hit is tracked on
+// the root after the scatter (sw_batch_best).
 sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                        const uint32_t* d_lens, const uint64_t* d_ids, size_t n, uint32_t min_len,
                        uint32_t max_len, int32_t* d_scores, hipStream_t hs, bool records) {
   const size_t D = b->kids.size();
   sw_bank* root = b->kids[0];
   const bool set = b->qset.size() > 1;
-  if (!b->peer_ready) {
+  const size_t nq = set ? b->qset.size() : 1;
+  if (D > SWK_DEAL_MAX) return fail(b, SW_ERR_UNSUPPORTED, "more than %d devices", SWK_DEAL_MAX);
+  if (n > 0xFFFFFFFFull) return fail(b, SW_ERR_RANGE, "multi-device device batches hold < 2^32 targets");
+  if (!b->peer_ready) {  // direct xGMI copies (without: staged through the host by the runtime)
     for (sw_bank* k : b->kids) {
       if (k->device == root->device) continue;
       int can = 0;
       HIPOK(b, hipDeviceCanAccessPeer(&can, k->device, root->device));
-      if (!can)
-        return fail(b, SW_ERR_UNSUPPORTED, "device %d cannot access device %d's memory (peer)",
-                    k->device, root->device);
+      if (!can) continue;
       HIPOK(b, hipSetDevice(k->device));
       const hipError_t e = hipDeviceEnablePeerAccess(root->device, 0);
       if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
@@ -296,51 +309,130 @@ sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   HIPOK(b, hipSetDevice(root->device));
   if (!hs) hs = root->stream;
   if (!b->ev_join) HIPOK(b, hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
-  HIPOK(b, hipEventRecord(b->ev_join, hs));  // the caller's inputs are ready
+  if (!b->ev_used) HIPOK(b, hipEventCreateWithFlags(&b->ev_used, hipEventDisableTiming));
+  else HIPOK(b, hipStreamWaitEvent(hs, b->ev_used, 0));  // the previous call's scatter is done
+  // shares: round robin over the visiting order (records: contiguous ranges)
+  std::vector<size_t> cnt(D), lo(D, 0);
+  for (size_t d = 0; d < D; ++d) {
+    if (records) {
+      lo[d] = n * d / D;
+      cnt[d] = n * (d + 1) / D - lo[d];
+    } else {
+      cnt[d] = n > d ? (n - d + D - 1) / D : 0;
+    }
+  }
+  const size_t stride = records ? SWB_RECORD : std::max<uint32_t>(max_len, 1u);
+  SwkDeal dl{};
+  dl.D = (unsigned)D;
+  dl.stride = (unsigned)stride;
+  const uint32_t *perm = nullptr, *ident = nullptr;
+  if (!records) {
+    // 1. longest first (the sort's scratch zeroes itself; zeroed once here)
+    if (n > 1 && min_len < max_len && env_int("SWBANK_DSORT", 1) != 0) {
+      HIPOK(b, b->dperm.reserve(n + 2));
+      const size_t sw = swk_sort_scratch_bytes() / 4;
+      if (b->dsort.cap < sw) {
+        HIPOK(b, b->dsort.reserve(sw));
+        HIPOK(b, hipMemsetAsync(b->dsort.p, 0, sw * 4, hs));
+      }
+      HIPOK(b, swk_sort_lens(d_lens, n, max_len, b->dperm.p, b->dperm.p + n, b->dperm.p + n + 1,
+                             b->dsort.p, hs));
+      ++b->ctr.device_sorts;
+      perm = b->dperm.p;
+      ident = b->dperm.p + n + 1;
+    }
+    // 2. the staging regions on the root, then the gather
+    HIPOK(b, b->res.reserve(n * stride + 16));
+    HIPOK(b, b->offs.reserve(n));
+    HIPOK(b, b->lens.reserve(n));
+    HIPOK(b, b->grecv.reserve(n * nq));
+    size_t at = 0;
+    for (size_t d = 0; d < D; ++d) {
+      dl.codes[d] = b->res.p + at * stride;
+      dl.offs[d] = reinterpret_cast<unsigned long long*>(b->offs.p + at);
+      dl.lens[d] = b->lens.p + at;
+      dl.scores[d] = b->grecv.p + at * nq;
+      dl.cnt[d] = cnt[d];
+      at += cnt[d];
+    }
+    HIPOK(b, swk_deal_gather(d_res, d_offs, d_lens, perm, ident, n, &dl, hs));
+  }
+  HIPOK(b, hipEventRecord(b->ev_join, hs));  // the inputs (and the staging) are ready
+  // 3. every device: its share in, scored in its own HBM, scores out
   sw_status st = SW_OK;
-  size_t launched = 0;
+  std::vector<bool> launched(D, false);
   for (size_t d = 0; d < D && st == SW_OK; ++d) {
     sw_bank* k = b->kids[d];
-    const size_t lo = n * d / D, cnt = n * (d + 1) / D - lo;
-    if (!cnt) continue;
+    const size_t c = cnt[d];
+    if (!c) continue;
     if ((st = prepare(k)) != SW_OK) break;
-    if (hipSetDevice(k->device) != hipSuccess) {
-      st = fail(k, SW_ERR_HIP, "hipSetDevice(%d)", k->device);
+    const auto hip = [&](hipError_t e, const char* what) {
+      if (e != hipSuccess && st == SW_OK)
+        st = fail(k, SW_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+      return st == SW_OK;
+    };
+    if (!hip(hipSetDevice(k->device), "hipSetDevice")) break;
+    if (!k->ev_join && !hip(hipEventCreateWithFlags(&k->ev_join, hipEventDisableTiming), "event"))
       break;
-    }
-    if (!k->ev_join && hipEventCreateWithFlags(&k->ev_join, hipEventDisableTiming) != hipSuccess) {
-      st = fail(k, SW_ERR_HIP, "event");
+    const hipStream_t ks = k->stream;
+    if (!hip(hipStreamWaitEvent(ks, b->ev_join, 0), "stream wait")) break;
+    // the bank's own buffers: its previous launch is done with them (launch waits for ev_used,
+    // the copies below must too)
+    if (!hip(hipStreamWaitEvent(ks, k->ev_used, 0), "stream wait")) break;
+    if (!hip(k->res.reserve(c * stride + 16), "device buffer") ||
+        !hip(k->offs.reserve(c), "device buffer") || !hip(k->lens.reserve(c), "device buffer") ||
+        !hip(k->scores.reserve(c * nq), "device buffer"))
       break;
+    launched[d] = true;
+    if (records) {
+      if (!hip(hipMemcpyPeerAsync(k->res.p, k->device, d_res + lo[d] * SWB_RECORD, root->device,
+                                  c * SWB_RECORD, ks), "records in"))
+        break;
+      st = launch(k, k->res.p, nullptr, nullptr, c, SWB_RECORD_MAX, k->scores.p, ks,
+                  SWK_PACK_RECORDS);
+      if (st == SW_OK)
+        (void)hip(hipMemcpyPeerAsync(d_scores + lo[d], root->device, k->scores.p, k->device,
+                                     c * 4, ks), "scores out");
+    } else {
+      if (!hip(hipMemcpyPeerAsync(k->res.p, k->device, dl.codes[d], root->device, c * stride, ks),
+               "codes in") ||
+          !hip(hipMemcpyPeerAsync(k->offs.p, k->device, dl.offs[d], root->device, c * 8, ks),
+               "offsets in") ||
+          !hip(hipMemcpyPeerAsync(k->lens.p, k->device, dl.lens[d], root->device, c * 4, ks),
+               "lengths in"))
+        break;
+      st = set ? launch_set(k, k->res.p, k->offs.p, k->lens.p, c, min_len, max_len, k->scores.p,
+                            ks, c)
+               : launch(k, k->res.p, k->offs.p, k->lens.p, c, max_len, k->scores.p, ks,
+                        SWK_PACK_BYTES, nullptr, nullptr, true, true, nullptr, nullptr, 0, 0,
+                        min_len);
+      if (st == SW_OK)
+        (void)hip(hipMemcpyPeerAsync(const_cast<int*>(dl.scores[d]), root->device, k->scores.p,
+                                     k->device, c * nq * 4, ks), "scores out");
     }
-    // device 0 runs on the caller's stream itself; the others on their own, behind it
-    hipStream_t ks = d == 0 ? hs : k->stream;
-    if (d > 0 && hipStreamWaitEvent(ks, b->ev_join, 0) != hipSuccess) {
-      st = fail(k, SW_ERR_HIP, "stream wait");
-      break;
-    }
-    if (records)
-      st = launch(k, d_res + lo * SWB_RECORD, nullptr, nullptr, cnt, SWB_RECORD_MAX,
-                  d_scores + lo, ks, SWK_PACK_RECORDS);
-    else if (set)
-      st = launch_set(k, d_res, d_offs + lo, d_lens + lo, cnt, min_len, max_len, d_scores + lo,
-                      ks, n);
-    else
-      st = launch(k, d_res, d_offs + lo, d_lens + lo, cnt, max_len, d_scores + lo, ks,
-                  SWK_PACK_BYTES, nullptr, nullptr, true, true, nullptr, nullptr, 0, 0, min_len);
-    // (recorded even after a failed launch: the caller's stream must not run ahead of what
-    // was enqueued)
-    if (d > 0 && hipEventRecord(k->ev_join, ks) == hipSuccess) launched |= (size_t)1 << d;
   }
-  (void)hipSetDevice(root->device);
-  for (size_t d = 1; d < D; ++d)
-    if (launched >> d & 1) HIPOK(b, hipStreamWaitEvent(hs, b->kids[d]->ev_join, 0));
+  // (recorded even after a failure: the caller's stream must not run ahead of what was enqueued)
+  for (size_t d = 0; d < D; ++d) {
+    if (!launched[d]) continue;
+    sw_bank* k = b->kids[d];
+    (void)hipSetDevice(k->device);
+    if (hipEventRecord(k->ev_join, k->stream) == hipSuccess) {
+      (void)hipSetDevice(root->device);
+      HIPOK(b, hipStreamWaitEvent(hs, k->ev_join, 0));
+    }
+  }
+  HIPOK(b, hipSetDevice(root->device));
   if (st != SW_OK) {
+    (void)hipEventRecord(b->ev_used, hs);
     for (sw_bank* k : b->kids)
       if (k->err[0]) return fail(b, st, "device %d: %s", k->device, k->err);
     return st;
   }
-  snprintf(b->last_kernel, sizeof(b->last_kernel), "multi[%zu] device ranges: %s", D,
-           root->last_kernel);
+  // 4. scores to input order (query-major rows n apart for a set)
+  if (!records) HIPOK(b, swk_deal_scatter(perm, ident, n, (unsigned)nq, n, &dl, d_scores, hs));
+  HIPOK(b, hipEventRecord(b->ev_used, hs));
+  snprintf(b->last_kernel, sizeof(b->last_kernel), "multi[%zu] device deal%s: %s", D,
+           perm ? " longest-first" : "", root->last_kernel);
   if (d_ids && !records) {
     if ((st = track_best_device(root, d_scores, d_ids, n, hs)) != SW_OK)
       return fail(b, st, "device %d: %s", root->device, root->err);

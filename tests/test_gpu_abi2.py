@@ -297,11 +297,13 @@ def test_multi_device_bank_equals_single(devices, gather, monkeypatch):
 
 @pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0], [0]])
 def test_multi_device_bank_device_api(devices, poisoned_buffers):
-    """ABI 4: a multi-device bank takes device buffers (on the root device): every device scores
-    a contiguous range straight from the caller's buffers and writes into the caller's score
-    buffer, asynchronous on the caller's stream.  Bit-exact against a single bank for a ragged
-    batch (each device sorts its own range), with the best hit, for a query set (every query
-    broadcast to every device, ScoreBank_v2.v:101-102), and for device records."""
+    """ABI 4/5: a multi-device bank takes device buffers (on the root device): the batch is
+    sorted longest first on the root and dealt round robin (length-balanced, as the host path),
+    each device copies its share into its own HBM, scores it there and copies its scores back,
+    asynchronous on the caller's stream (ScoreBank_v2.v:117-137: each module latches its own
+    target copy).  Bit-exact against a single bank for a ragged batch with the best hit, a
+    uniform batch on another stream right after (the staging reuse is ordered), a query set
+    (every query broadcast to every device, ScoreBank_v2.v:101-102), and device records."""
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda", 0)
     q, seqs = _ragged_batch(40 + len(devices), 6000)
@@ -324,6 +326,12 @@ def test_multi_device_bank_device_api(devices, poisoned_buffers):
         bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,
                                 one.data_ptr(), st.cuda_stream, d_ids=d_ids.data_ptr())
         best = bank.best()
+        kern = bank.last_kernel()
+        st2 = torch.cuda.Stream()  # a uniform batch (4000 targets cut to 60) right after
+        uni = torch.full((4000,), -1, dtype=torch.int32, device=dev)
+        bank.score_batch_device(d_res.data_ptr(), d_o60.data_ptr(), d_u60.data_ptr(), 4000, 60,
+                                uni.data_ptr(), st2.cuda_stream, min_len=60)
+        st2.synchronize()
         rec = torch.full((n,), -1, dtype=torch.int32, device=dev)
         bank.score_records_device(d_rec.data_ptr(), n, rec.data_ptr(), st.cuda_stream)
         bank.load_queries(qs)
@@ -332,16 +340,24 @@ def test_multi_device_bank_device_api(devices, poisoned_buffers):
         bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,
                                 sets.data_ptr(), st.cuda_stream, min_len=int(lens.min()))
         st.synchronize()
-        return one.cpu().numpy(), best, rec.cpu().numpy(), sets.cpu().numpy()
+        bank.sync()
+        return (one.cpu().numpy(), best, rec.cpu().numpy(), sets.cpu().numpy(),
+                uni.cpu().numpy(), kern)
 
+    offs60 = np.ascontiguousarray(offs[np.nonzero(lens >= 60)[0][:4000]])
+    lens60 = np.full(4000, 60, np.uint32)
+    d_o60 = torch.from_numpy(offs60.view(np.int64)).to(dev)
+    d_u60 = torch.from_numpy(lens60.view(np.int32)).to(dev)
     with S.ScoreBank() as single:
         want = run(single)
     with S.ScoreBank(devices=devices) as multi:
         got = run(multi)
-        assert multi.last_kernel().startswith(f"multi[{len(devices)}] device ranges"), \
-            multi.last_kernel()
+        if len(devices) > 1:
+            assert got[5].startswith(f"multi[{len(devices)}] device deal longest-first"), got[5]
     assert (got[0] == want[0]).all() and got[1] == want[1]
     assert (got[2] == want[2]).all() and (got[3] == want[3]).all()
+    assert (got[4] == want[4]).all()
+    assert (want[4] == O.score_batch(q, res, offs60, lens60, O.dna_matrix(), -12, -4)).all()
     assert (want[0] == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
     res2, offs2, lens2 = O.pack_residues(short)
     assert (want[2] == O.score_batch(q, res2, offs2, lens2, O.dna_matrix(), -12, -4)).all()
