@@ -59,7 +59,7 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        const uint32_t* ident, int pair, uint32_t pS1,
                                        uint32_t pS2, uint32_t ulen, uint32_t ustride, uint32_t nq,
                                        uint32_t qwords, size_t sstride, hipStream_t st);
-extern "C" unsigned swk_bal_slots(int W, uint32_t PS);
+extern "C" unsigned swk_bal_slots(int W, uint32_t PS, int trim);
 extern "C" unsigned swk_wave_half_grid(int gotoh, uint32_t prof_bytes);
 extern "C" hipError_t swk_bal_plan_uniform(void* plan, uint32_t ntiles, uint32_t K, uint32_t G,
                                            hipStream_t st);
@@ -72,7 +72,7 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           uint32_t gen, unsigned grid, const uint32_t* idx,
                                           const uint32_t* nidx, const uint32_t* ident,
                                           const void* plan, uint32_t* fault, uint32_t poll_limit,
-                                          uint32_t stall, hipStream_t st);
+                                          uint32_t stall, int trim, hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
                                    hipStream_t st);

@@ -655,10 +655,11 @@ __device__ __forceinline__ Lane2 lane_targets(const uint8_t* res, const uint64_t
   return t;
 }
 
-// Chunk counts of a tile (uniform): nch = ceil(max len / C) (>= 1), nfull = min len / C.
+// Chunk counts of a tile (uniform): nch = ceil(max len / C) (>= 1), nfull = min len / C, ncl =
+// the columns of chunk nch - 1 that hold a code of some lane (1..C).
 template <int C = 8>
 __device__ __forceinline__ void tile_chunks(const Lane2& t, size_t tlo, size_t thi, size_t n,
-                                            int& nch, int& nfull) {
+                                            int& nch, int& nfull, int& ncl) {
   uint32_t Lmax = max(t.llo, t.lhi);
   uint32_t Lmin = min(tlo < n ? t.llo : ~0u, thi < n ? t.lhi : ~0u);
 #pragma unroll
@@ -668,6 +669,7 @@ __device__ __forceinline__ void tile_chunks(const Lane2& t, size_t tlo, size_t t
   }
   const int lx = (int)__builtin_amdgcn_readfirstlane(Lmax);
   nch = max(1, (lx + C - 1) / C);
+  ncl = lx == 0 ? C : lx - C * (nch - 1);
   const uint32_t lm = __builtin_amdgcn_readfirstlane(Lmin);
   nfull = lm == ~0u ? 0 : (int)(lm / C);  // no valid lane (a tile past the end): no full loads
 }
@@ -877,10 +879,14 @@ __device__ __forceinline__ uint32_t stream_mode(const uint32_t* hflag, uint32_t*
 
 // C: columns per chunk (one barrier per chunk); 4 for the 16-wave query-set pair kernel, whose
 // hand-off ring would not fit LDS beside a 512-row pair table at 8.
+// TRIM: a tile's last chunk stops after its last column holding a code of some lane (ragged
+// batches: a tile's lengths are one sort bin, rarely a multiple of C; the per-column test costs
+// a uniform batch ~25 VALU per chunk in register copies, so only the ragged launches take it).
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
-          bool MQ = false, bool STREAM = false, int C = 8, bool BAL = false>
+          bool MQ = false, bool STREAM = false, int C = 8, bool BAL = false, bool TRIM = false>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
   static_assert(!BAL || (!MQ && !STREAM && !COL0), "balanced ranges: one query, resident batch");
+  static_assert(!TRIM || (BAL && PAIR), "trimmed last chunks: the balanced pair kernel");
   static_assert(!MQ || !PROF, "several queries: row-LUT or pair-table variants");
   static_assert(!STREAM || (!MQ && !PROF), "streamed batches: single-query LUT / pair variants");
   static_assert(C == 8 || (C == 4 && PAIR && !STREAM), "4-column chunks: pair tables only");
@@ -1040,10 +1046,12 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
     cur = lane_targets<!MQ>(a.res, a.offs, a.lens, n, tile, lane, packed, idx, a.ulen,
                             a.ustride);
   }
-  int nch, nfull;
+  int nch, nfull, ncl;
   tile_chunks<C>(cur, (size_t)tile * SWB_TILE + lane, (size_t)tile * SWB_TILE + lane + 64, n, nch,
-              nfull);
+              nfull, ncl);
+  (void)ncl;
   if constexpr (BAL) {  // BAL: nch = the visit's end chunk (a head's last chunk is whole)
+    if (vend >= 0 && vend < nch) ncl = C;
     nch = vend < 0 ? nch : vend;
   }
   const uint32_t S = a.S;
@@ -1213,7 +1221,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   // chunk within the current tile, tile ordinal in this workgroup (BAL: the visit ordinal; a
   // first visit is a head or a whole tile, never a tail)
   int c = vc0, k = 0;
-  int nch_n = 1, nfull_n = 0;  // the next tile's chunk counts
+  int nch_n = 1, nfull_n = 0, ncl_n = C;  // the next tile's chunk counts
   uint32_t packed_n = packed;  // STREAM: the next tile's code layout
 #if SWK_PRIO_ROT
   const uint32_t prq = (uint32_t)((blockIdx.x * 4ull) / gridDim.x);
@@ -1284,7 +1292,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
           cur = lane_targets<!MQ>(a.res, a.offs, a.lens, n, ntile, lane, packed, idx, a.ulen,
                                   a.ustride);
         tile_chunks<C>(cur, (size_t)ntile * SWB_TILE + lane, (size_t)ntile * SWB_TILE + lane + 64,
-                    n, nch_n, nfull_n);
+                    n, nch_n, nfull_n, ncl_n);
+        if (BAL && nvend >= 0 && nvend < nch_n) ncl_n = C;
         if (BAL && nvend < 0) nvend = nch_n;
         load_raw<C, !MQ>(cur, nc0, nc0 < nfull_n, a.pad, STREAM ? packed_n : packed, rlo, rhi);
       }
@@ -1301,8 +1310,17 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       uint2 rv = rin[0];
       ProfLookup16<PROF && F16 ? R : 2> lkq;  // f16 profile: the next column's words
       (void)lkq;
+      // TRIM: the tile's last chunk stops after its last column holding a code (a tile runs to
+      // its longest lane; every wave stops at the same column, so the ring stays consistent)
+      const int ncols = TRIM && c + 1 == nch ? ncl : C;
+      bool trimmed = false;
+      (void)ncols;
 #pragma unroll
       for (int jj = 0; jj < C; ++jj) {
+        if (TRIM && jj > 0 && __builtin_expect(jj >= ncols, 0)) {
+          trimmed = true;
+          continue;
+        }
         const u16x2 upH = as_u16x2(rv.x);
         u16x2 upX = as_u16x2(rv.y);
         if (jj + 1 < C) rv = rin[(jj + 1) * istride];  // one column ahead
@@ -1459,6 +1477,15 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         asm volatile("" : "+v"(best));
         rout[jj * ostride] = make_uint2(as_u32(Hl[R - 1]), as_u32(upX));
       }
+      if constexpr (PAIR && TRIM) {
+        if (trimmed) {  // the next chunk's column 0, read ahead as at a chunk's end
+          acur = pair_addr(rlo.x, rhi.x, 0);
+          pA0 = ld4(acur + 16);
+          pA1 = ld4(acur + 32);
+          pw = ld1(acur + 12);
+        }
+      }
+      (void)trimmed;
       if (seg_out && wave == W - 1) {  // this segment's bottom row -> the next segment
         uint2* dst = a.edge_out + ((size_t)(MQ ? unit : tile) * a.ecols + (size_t)c * C) * 64 + lane;
 #pragma unroll
@@ -1524,6 +1551,7 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
         }
         nch = nch_n;
         nfull = nfull_n;
+        ncl = ncl_n;
         c = 0;
         if constexpr (BAL) {
           c = nc0;
@@ -1611,7 +1639,7 @@ static unsigned persistent_grid(const void* fn, size_t ntiles, int threads, size
 }
 
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
-          bool MQ = false, bool STREAM = false, int C = 8, bool BAL = false>
+          bool MQ = false, bool STREAM = false, int C = 8, bool BAL = false, bool TRIM = false>
 static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, hipStream_t st,
                                unsigned bal_grid = 0) {
   const size_t ntiles = (a.n + SWB_TILE - 1) / SWB_TILE * (MQ ? a.nq : 1);  // units
@@ -1619,7 +1647,7 @@ static hipError_t launch_score(const ScoreArgs& a, int W, uint32_t prof_bytes, h
                      (size_t)(64 + (a.edge_out ? C * 64 : 64) + (a.edge_in ? 2 * C * 64 : 0) +
                               (W > 1 ? W - 1 : 0) * 2 * C * 64) * 8 +
                      (PROF ? prof_bytes : 0) + (PAIR ? a.PS : 0) + (STREAM ? 256 : 0);
-  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR, MQ, STREAM, C, BAL>;
+  auto fn = &score_kernel<R, RB, COL0, PROF, GOTOH, F16, PAIR, MQ, STREAM, C, BAL, TRIM>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -3084,19 +3112,20 @@ extern "C" unsigned swk_wave_half_grid(int gotoh, uint32_t prof_bytes) {
   return occ > 0 && cus > 0 ? (unsigned)(occ * cus) : 0u;
 }
 
-extern "C" unsigned swk_bal_slots(int W, uint32_t PS) {
-  auto fn = &swk::score_kernel<32, 4, false, false, false, true, true, false, false, 8, true>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-      return 0;
-    attr_set = true;
-  }
+extern "C" unsigned swk_bal_slots(int W, uint32_t PS, int trim) {
+  const void* fn =
+      trim ? reinterpret_cast<const void*>(
+                 &swk::score_kernel<32, 4, false, false, false, true, true, false, false, 8, true,
+                                    true>)
+           : reinterpret_cast<const void*>(
+                 &swk::score_kernel<32, 4, false, false, false, true, true, false, false, 8, true>);
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+      hipSuccess)
+    return 0;
   const size_t lds = (size_t)W * SWB_TILE * 4 + (size_t)(64 + 64 + (W - 1) * 2 * 8 * 64) * 8 + PS;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
-  const int occ = swk::cached_occupancy(reinterpret_cast<const void*>(fn), 64 * W, lds, dev, &cus);
+  const int occ = swk::cached_occupancy(fn, 64 * W, lds, dev, &cus);
   return occ > 0 && cus > 0 ? (unsigned)(occ * cus) : 0u;
 }
 
@@ -3109,7 +3138,7 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           uint32_t gen, unsigned grid, const uint32_t* idx,
                                           const uint32_t* nidx, const uint32_t* ident,
                                           const void* plan, uint32_t* fault, uint32_t poll_limit,
-                                          uint32_t stall, hipStream_t st) {
+                                          uint32_t stall, int trim, hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (W > 4 || !flag || !state || !plan || !fault || poll_limit == 0 || (idx && !nidx))
     return hipErrorInvalidValue;
@@ -3128,6 +3157,9 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
   a.fault = fault;
   a.poll_limit = poll_limit;
   a.stall = stall;
+  if (trim)  // (a ragged batch: its tiles' last chunks stop at their last column)
+    return swk::launch_score<32, 4, false, false, false, true, true, false, false, 8, true, true>(
+        a, W, 0, st, grid);
   return swk::launch_score<32, 4, false, false, false, true, true, false, false, 8, true>(
       a, W, 0, st, grid);
 }

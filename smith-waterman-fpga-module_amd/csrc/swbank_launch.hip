@@ -72,6 +72,10 @@ static uint32_t poll_limit(uint32_t dflt) {
   return v > 0 ? (uint32_t)v : dflt;
 }
 
+// Ragged balanced launches stop each tile's last chunk at its last column (the TRIM variant of
+// the pair kernel); SWBANK_TRIM=0 keeps whole chunks (A/B).
+static int ragged_trim() { return env_int("SWBANK_TRIM", 1) != 0 ? 1 : 0; }
+
 // packed (SWK_PACK_*): RECORDS: d_res holds n 64-byte CAPI records (2-bit codes), d_offs and
 // d_lens are unused; STREAM: 2-bit codes, d_offs in bytes (the host feeder's DNA chunks).
 // perm/perm_n (optional, tile kernel): pass 0 visits the targets in the order perm[0..n)
@@ -280,7 +284,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       b->R == 32 && b->segs[0].W <= 4 && n <= 0xFFFFFFFFull && env_int("SWBANK_DSORT", 1) != 0 &&
       env_int("SWBANK_BAL", 1) != 0 && env_int("SWBANK_BAL_RAGGED", 1) != 0 &&
       !one_len_bin(min_len, max_len)) {
-    const unsigned grid = swk_bal_slots(b->segs[0].W, b->pair_bytes);
+    const unsigned grid = swk_bal_slots(b->segs[0].W, b->pair_bytes, ragged_trim());
     const size_t kmin = std::max<uint32_t>(1u, (min_len + 7) / 8), kmax = (max_len + 7) / 8;
     if (grid && ntiles * kmin >= 2 * (size_t)grid * kmax && ntiles * kmax < (1ull << 31))
       rbal_grid = grid;
@@ -378,7 +382,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                    ntiles * ((max_len + 7) / 8) < (1ull << 31) && !opt16 && b->R == 32 &&
                    b->segs[0].W <= 4 && env_int("SWBANK_BAL", 1) != 0)) {
         const int Wl = b->segs[0].W;
-        const unsigned grid = rbal ? rbal_grid : swk_bal_slots(Wl, b->pair_bytes);
+        const unsigned grid = rbal ? rbal_grid : swk_bal_slots(Wl, b->pair_bytes, 0);
         uint32_t* fw = fault_word(b);
         if (!fw) return fail(b, SW_ERR_NOMEM, "fault word allocation failed");
         if (grid && (rbal || ntiles >= 2 * (size_t)grid)) {
@@ -404,7 +408,8 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                                        ustride, b->bal_flag.p, b->bal_state.p, ++b->bal_gen, grid,
                                        idx, nidx, ident, b->bal_plan.p,
                                        fw + (b->host_call ? 1 : 0), poll_limit(1u << 23),
-                                       (uint32_t)std::max(0, env_int("SWBANK_STALL", 0)), st));
+                                       (uint32_t)std::max(0, env_int("SWBANK_STALL", 0)),
+                                       rbal && ragged_trim(), st));
           ++b->ctr.balanced_calls;
           const size_t L = strlen(b->last_kernel);
           snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " balanced grid=%u", grid);
