@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build libswbank with extra compile flags into lib/libswbank_NAME.so (A/B of kernel variants on
 # one box with SWBANK_LIB=...):   scripts/build_variant.sh NAME "-DSWK_PROF_AHEAD=0 ..."
+# (every in-tree .so travels with each gpurun push: delete the variant when its A/B is done)
 set -eu
 set -o pipefail
 NAME=$1; FLAGS=${2:-}
