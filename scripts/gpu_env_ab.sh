@@ -1,5 +1,5 @@
 #!/bin/bash
-A=0" W=workload [ROUNDS=2]|A=0" W=workload [ROUNDS=2]
+# Alternating bench lines of environment settings: ENVS="A=1|A=0" W=workload [ROUNDS=2]
 # [TESTS="pytest targets" run first] [BENCH_ARGS=...].  Outputs gpurun_out/ab_<TAG>_*.json.
 set -u
 TAG=${TAG:-ab}; ROUNDS=${ROUNDS:-2}

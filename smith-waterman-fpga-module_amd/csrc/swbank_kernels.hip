@@ -56,6 +56,7 @@
 #ifndef SWK_PRIO_SHIFT
 #define SWK_PRIO_SHIFT 18
 #endif
+
 #ifndef SWK_PRIO_END
 #define SWK_PRIO_END 3  // the last 1/16 of a workgroup's phases rotate 8 times faster
 #endif
@@ -2832,12 +2833,22 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
     // the K = 8 profile (2-byte entries, PS = 1024 bytes per letter) as words {s, 1.0}, 2048
     // bytes per letter: row r = 16 l + 4 q + j (lane l of a half, piece q, word j) at word
     // 128 q + 4 l + j, so lane l reads its 16 rows as 4 x 16 bytes, 512 apart
-    const uint32_t rows = (a.pad + 1) * 512;
-    const uint16_t* src = reinterpret_cast<const uint16_t*>(a.qtab);
-    for (uint32_t i = threadIdx.x; i < rows; i += blockDim.x) {
-      const uint32_t r = i & 511u;
-      reinterpret_cast<uint32_t*>(prof)[(i & ~511u) | ((r >> 2) & 3u) << 7 | (r >> 4) << 2 |
-                                        (r & 3u)] = src[i] | 0x3C000000u;
+    // (16-byte loads of 8 entries, rows 8 m .. 8 m + 7 of a letter = pieces q, q + 1 of lane
+    // l: two 16-byte LDS stores; the loads of a thread's iterations are independent)
+    const uint32_t groups = (a.pad + 1) * 64;
+    const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
+    uint4* dst = reinterpret_cast<uint4*>(prof);
+    const auto widen = [](uint32_t x) {  // two entries -> two {s, 1.0} words
+      return make_uint2((x & 0xFFFFu) | 0x3C000000u, (x >> 16) | 0x3C000000u);
+    };
+#pragma unroll 4
+    for (uint32_t i = threadIdx.x; i < groups; i += blockDim.x) {
+      const uint4 v = src[i];
+      const uint32_t r = (i & 63u) * 8;  // first row of the group
+      const uint32_t w = (i & ~63u) * 8 | ((r >> 2) & 3u) << 7 | (r >> 4) << 2;  // word index
+      const uint2 a0 = widen(v.x), a1 = widen(v.y), a2 = widen(v.z), a3 = widen(v.w);
+      dst[w / 4] = make_uint4(a0.x, a0.y, a1.x, a1.y);            // rows r .. r + 3
+      dst[w / 4 + 32] = make_uint4(a2.x, a2.y, a3.x, a3.y);       // rows r + 4 .. r + 7
     }
     __syncthreads();
   } else {  // the K = 8 profile (64 16-byte row groups per letter, PS = 1024) with group 2l + q
