@@ -2811,6 +2811,28 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
   const int lane = threadIdx.x & 63;
+#if SWK_STAMPS
+  // (measurement builds: launch_wave_half passes the record buffer in tctr) per wave: entry,
+  // exit, the profile copy's end, ticks in hand-off waits, HW_ID, XCC, visits, block
+  const uint64_t st_t0 = __builtin_amdgcn_s_memtime();
+  uint64_t st_copy = 0, st_wait = 0;
+  const auto stamp_out = [&](int wave_, int nvis_) {
+    uint64_t* g = reinterpret_cast<uint64_t*>(a.tctr);
+    if (!g || lane != 0) return;
+    uint64_t* o = g + ((size_t)blockIdx.x * 4 + wave_) * 8;
+    unsigned hw = 0, xcc = 0;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    o[0] = st_t0;
+    o[1] = __builtin_amdgcn_s_memtime();
+    o[2] = st_copy;
+    o[3] = st_wait;
+    o[4] = hw;
+    o[5] = xcc & 15;
+    o[6] = (uint64_t)nvis_;
+    o[7] = blockIdx.x;
+  };
+#endif
   if (blockIdx.x < a.split_blocks) {  // block-uniform
     if (a.split_P == 4) wave_split_block<2, 4, false, true, GOTOH, true>(a, smem, lane);
     else wave_split_block<4, 2, false, true, GOTOH, true>(a, smem, lane);
@@ -2851,6 +2873,9 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
       dst[w / 4 + 32] = make_uint4(a2.x, a2.y, a3.x, a3.y);       // rows r + 4 .. r + 7
     }
     __syncthreads();
+#if SWK_STAMPS
+    st_copy = __builtin_amdgcn_s_memtime();
+#endif
   } else {  // the K = 8 profile (64 16-byte row groups per letter, PS = 1024) with group 2l + q
             // at 32 q + l: lane l of a half reads its rows 16 l .. 16 l + 15 as 16 + 16 bytes,
             // 512 apart
@@ -2895,6 +2920,9 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
     const uint32_t unit = __builtin_amdgcn_readfirstlane(
         head ? u1 : tail ? u0 : whole0 + (uint32_t)(v - (b1 ? 1 : 0)));
     if (tail) {  // wave g - 1's head is done (a bounded poll, as DESIGN §3.8)
+#if SWK_STAMPS
+      const uint64_t sw0 = __builtin_amdgcn_s_memtime();
+#endif
       uint32_t it = 0;
       for (; it < a.poll_limit; ++it) {
         if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(
@@ -2904,6 +2932,9 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
       }
       if (it == a.poll_limit && lane == 0) report_fault(a.fault, SWK_FAULT_WBAL);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if SWK_STAMPS
+      st_wait += __builtin_amdgcn_s_memtime() - sw0;
+#endif
     }
     const uint2 b = wave_two_pairs<GOTOH>(
         a, prof, cring, lane, 2 * (size_t)unit, tail ? 32 * b0 : 0, head ? 32 * b1 : 0x7FFFFFFF,
@@ -2918,6 +2949,9 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
       wave_half_finish<GOTOH>(a, b, lane, 2 * (size_t)unit);
     }
   }
+#if SWK_STAMPS
+  stamp_out(wave, nvis);
+#endif
 }
 
 // The end of a two-pairs unit: a pair above the optimistic f16 threshold is re-scored in u16 by
@@ -2975,6 +3009,14 @@ static hipError_t launch_wave_half(const ScoreArgs& a, uint32_t prof_bytes, hipS
     attr_set = true;
   }
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
+#if SWK_STAMPS
+  if (g_stamps_host) {  // (measurement builds) the record buffer in tctr, unused here
+    ScoreArgs b = a;
+    b.tctr = reinterpret_cast<uint32_t*>(g_stamps_host);
+    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(256), (unsigned)lds, st, b);
+    return hipGetLastError();
+  }
+#endif
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(256), (unsigned)lds, st, a);
   return hipGetLastError();
 }
