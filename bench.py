@@ -65,7 +65,7 @@ OPS_PER_CELL = {"merged": 10, "gotoh": 11}
 VALU_PEAK_TOPS_16 = CUS * SIMD_PER_CU * 16 * 2 * CLK_GHZ / 1e3  # 78.6
 VALU_ISSUE_PER_SIMD_CLK = 0.25
 MIN_INSTR_PER_ROW = {"merged": 5.5, "gotoh": 7.5}
-# the kernels' own column bodies (csrc/swbank_kernels.hip): f16 merged 6.5 (5.5 with the
+# the kernels' own column bodies (csrc/swbank_ktile.hip, swbank_kwave.hip): f16 merged 6.5 (5.5 with the
 # letter-pair table), f16 Gotoh 8.5, u16 merged 9, u16 Gotoh 11; the tile kernel adds 0.1-0.7
 # per row of loop overhead, the wave kernel ~7 per step of K rows plus the 63-step lane skew
 VALU_INSTR_PER_ROW = {"f16": 6.5, "f16-pair": 5.5, "f16-gotoh": 8.5, "u16": 9.0,

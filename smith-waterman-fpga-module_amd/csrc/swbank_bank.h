@@ -539,7 +539,7 @@ struct sw_bank {
   std::vector<Ev> events;
 };
 
-// Scores in the f16 kernels are f16 multiples of 2^-11 (x as x/2048, swbank_kernels.hip), so
+// Scores in the f16 kernels are f16 multiples of 2^-11 (x as x/2048, swbank_kcommon.h), so
 // the packed add's [0, 1] clamp is max(0, x); -2048 (padding rows / letters) is 0xBC00.
 inline uint16_t f16_score_bits(int v) {
   return __builtin_bit_cast(uint16_t, (_Float16)((float)v * (1.0f / 2048.0f)));

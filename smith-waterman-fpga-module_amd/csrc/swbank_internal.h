@@ -90,7 +90,7 @@ typedef struct SwkDeal {
 } SwkDeal;
 
 #ifdef __cplusplus
-/* (declared here so the definition in swbank_kernels.hip and the call in swbank_device.hip are
+/* (declared here so the definition in swbank_ktile.hip and the call in swbank_stream.hip are
  * checked against one signature) */
 extern "C" hipError_t swk_launch_stream(int R, int gotoh, int f16, int pair, const uint8_t* res,
                                         size_t n, uint32_t ulen, const SwkStreamChunk* sc,

@@ -1,6 +1,6 @@
 """GPU: streamed host batches (sw_score_batch on equal-length DNA targets): one kernel launch
 for the whole call, chunks of whole tiles published to the running kernel as their copies land
-(swbank_device.hip stream_feed, swbank_kernels.hip STREAM variants).  Scores must equal the
+(swbank_stream.hip stream_feed, swbank_ktile.hip STREAM variants).  Scores must equal the
 chunked feeder's (SWBANK_STREAM=0, itself checked against the oracle in test_gpu_feeder.py) and
 the oracle's on a sample; the best hit the lowest index of the maximum; a bad code or a target
 outside the residues fails the call and leaves the bank usable."""

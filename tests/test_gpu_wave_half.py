@@ -1,4 +1,4 @@
-"""GPU parity for the wave kernel's two-pairs-per-wave form (swbank_kernels.hip wave_two_pairs:
+"""GPU parity for the wave kernel's two-pairs-per-wave form (swbank_kwave.hip wave_two_pairs:
 f16 profile, queries of 257-512 rows, lanes 0-31 on one pair and 32-63 on the next, 16 rows per
 lane).  Every case against the oracle and against one pair per wave (SWBANK_WAVE_HALF=0):
 odd pair counts (a last wave with one real half), empty and ragged targets, the split tail
