@@ -647,7 +647,17 @@ extern "C" sw_status sw_score_batch_device_range(sw_bank* b, const uint8_t* d_re
 extern "C" sw_status sw_batch_best(sw_bank* b, uint64_t* best_id, int32_t* best_score,
                                    uint64_t* best_index) {
   if (!b) return SW_ERR_ARG;
-  if (b->is_multi() && b->best_root) return sw_batch_best(b->kids[0], best_id, best_score, best_index);
+  if (b->is_multi() && b->best_root) {
+    // the root tracked it after the scatter, which waited for every device's work: once it is
+    // in, every device's hand-off faults of the call are visible too
+    const sw_status st = sw_batch_best(b->kids[0], best_id, best_score, best_index);
+    if (st != SW_OK) return fail(b, st, "device %d: %s", b->kids[0]->device, b->kids[0]->err);
+    if (const sw_status fs = take_fault(b, 0); fs != SW_OK) {
+      b->kids[0]->best_kind = 0;
+      return fs;
+    }
+    return SW_OK;
+  }
   if (b->best_kind == 2) {
     uint64_t h[3];
     HIPOK(b, hipSetDevice(b->device));
