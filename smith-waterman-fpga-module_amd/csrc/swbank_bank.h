@@ -511,6 +511,7 @@ struct sw_bank {
   // on-device longest-first order of a ragged device batch (sw_score_batch_device):
   // dperm = visiting order + count, dsort = histogram / scan scratch
   DevBuf<uint32_t> dperm, dsort;
+  DevBuf<uint32_t> one_word;  // a device word holding 1 (an "identity order" flag)
   bool is_multi() const { return !kids.empty(); }
   bool gotoh() const { return cfg.gap_model == SW_GAP_GOTOH; }
 

@@ -440,3 +440,41 @@ def test_host_batch_target_outside_residues():
             bank.score_batch(res, bad, lens)
         got = bank.score_batch(res, offs, lens)  # still usable
     assert (got == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 129])
+def test_multi_device_deal_small_batches(n, poisoned_buffers):
+    """The device-call deal with fewer targets than devices (some devices get none), a single
+    target, empty targets, a batch of one length and a ragged one: exact against the oracle,
+    the best hit with ids, device records dealt as contiguous ranges."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(n)
+    q = _codes(rng, 60)
+    seqs = [_codes(rng, int(rng.integers(0, 90))) for _ in range(n)]
+    seqs[0] = q[:40].copy()
+    if n > 2:
+        seqs[1] = np.zeros(0, np.uint8)
+    res, offs, lens = O.pack_residues(seqs)
+    res = np.concatenate([res, np.zeros(16, np.uint8)])
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    d_ids = torch.from_numpy((np.arange(n, dtype=np.uint64) * 3 + 1).view(np.int64)).to(dev)
+    d_rec = torch.from_numpy(S.make_records(seqs).reshape(-1)).to(dev)
+    with S.ScoreBank(devices=[0, 0, 0]) as multi:
+        multi.set_penalties(*REF)
+        multi.load_query(q)
+        sc = torch.full((n,), -5, dtype=torch.int32, device=dev)
+        multi.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n,
+                                 max(1, int(lens.max())), sc.data_ptr(), d_ids=d_ids.data_ptr())
+        best = multi.best()
+        rec = torch.full((n,), -5, dtype=torch.int32, device=dev)
+        multi.score_records_device(d_rec.data_ptr(), n, rec.data_ptr())
+        multi.sync()
+        got, got_rec = sc.cpu().numpy(), rec.cpu().numpy()
+    assert np.array_equal(got, want), (got.tolist(), want.tolist())
+    assert np.array_equal(got_rec, want)
+    k = int(np.argmax(want))
+    assert best == (k * 3 + 1, int(want[k]), k)
