@@ -87,6 +87,7 @@ typedef struct SwkDeal {
   unsigned* lens[SWK_DEAL_MAX];
   const int* scores[SWK_DEAL_MAX];
   unsigned long long cnt[SWK_DEAL_MAX];
+  unsigned nib; /* codes written 4-bit (SWK_PACK_NIBBLE: low nibble first), stride in bytes */
 } SwkDeal;
 
 #ifdef __cplusplus

@@ -97,7 +97,17 @@ __global__ void __launch_bounds__(256) deal_gather(const uint8_t* res, const uin
     const uint32_t L = lens[t];
     const uint8_t* src = res + offs[t];
     uint8_t* dst = dl.codes[d] + i * dl.stride;
-    for (uint32_t j = lane; j < L; j += 64) dst[j] = src[j];
+    if (dl.nib) {  // 8 codes per lane -> one u32, code k of the 8 in nibble k
+      for (uint32_t j = lane * 8; j < L; j += 512) {
+        uint32_t w = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k)
+          if (j + k < L) w |= (uint32_t)(src[j + k] & 15u) << (4 * k);
+        *reinterpret_cast<uint32_t*>(dst + j / 2) = w;
+      }
+    } else {
+      for (uint32_t j = lane; j < L; j += 64) dst[j] = src[j];
+    }
     if (lane == 0) {
       dl.offs[d][i] = (unsigned long long)i * dl.stride;
       dl.lens[d][i] = L;

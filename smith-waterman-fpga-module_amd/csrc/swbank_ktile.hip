@@ -919,12 +919,14 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           uint32_t gen, unsigned grid, const uint32_t* idx,
                                           const uint32_t* nidx, const uint32_t* ident,
                                           const void* plan, uint32_t* fault, uint32_t poll_limit,
-                                          uint32_t stall, int trim, hipStream_t st) {
+                                          uint32_t stall, int trim, uint32_t packed,
+                                          hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (W > 4 || !flag || !state || !plan || !fault || poll_limit == 0 || (idx && !nidx))
+  if (W > 4 || !flag || !state || !plan || !fault || poll_limit == 0 || (idx && !nidx) ||
+      (packed != SWK_PACK_BYTES && packed != SWK_PACK_NIBBLE))
     return hipErrorInvalidValue;
   swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
-                   O,    E,    PS,   pad, scores, nullptr, nullptr, 0u, 0u, (uint32_t)SWK_PACK_BYTES,
+                   O,    E,    PS,   pad, scores, nullptr, nullptr, 0u, 0u, packed,
                    idx, nidx, 0u, ident, pS1, pS2,
                    swk::f16_pair(-(int)(O + E)), swk::f16_pair(-(int)E),
                    swk::f16_pair(-(int)O), nullptr, 0u, 0u, 0};

@@ -407,10 +407,14 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
           // 16-byte aligned stride (swk_deal_gather, one device), scored without the
           // permutation, the scores scattered back (swk_deal_scatter): a tile's targets are then
           // neighbours in memory (the codes' scatter)
-          const bool gat = rbal && env_int("SWBANK_RAGGED_GATHER", 0) != 0;
+          // (=2: 4-bit codes, SWK_PACK_NIBBLE, for alphabets of <= 16 codes)
+          const int gmode = rbal ? env_int("SWBANK_RAGGED_GATHER", 0) : 0;
+          const bool gat = gmode != 0;
+          const bool gnib = gmode == 2 && b->alpha <= 16;
           SwkDeal dl{};
           if (gat) {
-            const size_t stride = ((size_t)max_len + 15) & ~(size_t)15;
+            const size_t stride = ((gnib ? ((size_t)max_len + 7) / 8 * 4 : (size_t)max_len) + 15) &
+                                  ~(size_t)15;
             HIPOK(b, b->res.reserve(n * stride + 16));
             HIPOK(b, b->offs.reserve(n));
             HIPOK(b, b->lens.reserve(n));
@@ -427,6 +431,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
             dl.lens[0] = b->lens.p;
             dl.scores[0] = b->scores.p;
             dl.cnt[0] = n;
+            dl.nib = gnib ? 1u : 0u;
             HIPOK(b, swk_deal_gather(res, offs, lens, idx, ident, n, &dl, st));
           }
           HIPOK(b, swk_launch_pair_bal(gat ? b->res.p : res, gat ? b->offs.p : offs,
@@ -438,7 +443,8 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                                        gat ? b->one_word.p : ident, b->bal_plan.p,
                                        fw + (b->host_call ? 1 : 0), poll_limit(1u << 23),
                                        (uint32_t)std::max(0, env_int("SWBANK_STALL", 0)),
-                                       rbal && ragged_trim(), st));
+                                       rbal && ragged_trim(),
+                                       gnib ? (uint32_t)SWK_PACK_NIBBLE : (uint32_t)SWK_PACK_BYTES, st));
           if (gat) HIPOK(b, swk_deal_scatter(idx, ident, n, 1, n, &dl, scores, st));
           ++b->ctr.balanced_calls;
           const size_t L = strlen(b->last_kernel);
