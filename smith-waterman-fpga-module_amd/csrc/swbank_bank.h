@@ -73,7 +73,7 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           const uint32_t* nidx, const uint32_t* ident,
                                           const void* plan, uint32_t* fault, uint32_t poll_limit,
                                           uint32_t stall, int trim, uint32_t packed,
-                                          hipStream_t st);
+                                          const uint32_t* sidx, hipStream_t st);
 extern "C" hipError_t swk_best_hit(const int32_t* scores, const uint64_t* ids, size_t n,
                                    unsigned long long* key, uint64_t* out, uint64_t* out_index,
                                    hipStream_t st);
@@ -512,7 +512,6 @@ struct sw_bank {
   // on-device longest-first order of a ragged device batch (sw_score_batch_device):
   // dperm = visiting order + count, dsort = histogram / scan scratch
   DevBuf<uint32_t> dperm, dsort;
-  DevBuf<uint32_t> one_word;  // a device word holding 1 (an "identity order" flag)
   bool is_multi() const { return !kids.empty(); }
   bool gotoh() const { return cfg.gap_model == SW_GAP_GOTOH; }
 

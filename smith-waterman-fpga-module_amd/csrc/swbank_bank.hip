@@ -187,7 +187,6 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->i32scr.release();
   b->dperm.release();
   b->dsort.release();
-  b->one_word.release();
   b->bal_state.release();
   b->bal_flag.release();
   b->wbal_state.release();

@@ -81,34 +81,55 @@ namespace swk {
 __device__ __forceinline__ size_t deal_target(const uint32_t* perm, bool id, size_t p) {
   return id ? p : (size_t)perm[p];
 }
-// one wave per position (grid-stride): the target's bytes, lane-strided, to its device's slot
+// 8-code chunks per target slot (K); a wave's lanes take the chunks of 64 / K positions
+// (K <= 64) or of one, each lane 8 codes -> one u64 of bytes or one u32 of 4-bit codes.  (One
+// lane per position, each looping over its chunks: 3.1x slower, every load instruction touching
+// 64 lines; one wave per position: 2.9x slower, a third of the lanes busy.  DESIGN 3.6)
+__host__ __device__ __forceinline__ uint32_t deal_chunks(const SwkDeal& dl) {
+  return dl.nib ? dl.stride / 4 : (dl.stride + 7) / 8;
+}
 __global__ void __launch_bounds__(256) deal_gather(const uint8_t* res, const uint64_t* offs,
                                                    const uint32_t* lens, const uint32_t* perm,
                                                    const uint32_t* ident, size_t n,
                                                    const SwkDeal dl) {
-  const int lane = threadIdx.x & 63;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t K = deal_chunks(dl);
+  const uint32_t tpw = K >= 64 ? 1u : 64u / K;  // positions per wave
+  const uint32_t g = K >= 64 ? 0u : lane / K, c0 = K >= 64 ? lane : lane - g * K;
   const size_t w0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const size_t nw = ((size_t)gridDim.x * blockDim.x) >> 6;
   const bool id = !perm || (ident && *ident != 0);
-  for (size_t p = w0; p < n; p += nw) {
+  const bool wide = (dl.stride & 7u) == 0;  // whole u64 stores stay inside the slot
+  for (size_t w = w0; w * tpw < n; w += nw) {
+    const size_t p = w * tpw + g;
+    if (g >= tpw || p >= n) continue;
     const size_t t = deal_target(perm, id, p);
     const unsigned d = (unsigned)(p % dl.D);
     const size_t i = p / dl.D;
     const uint32_t L = lens[t];
     const uint8_t* src = res + offs[t];
     uint8_t* dst = dl.codes[d] + i * dl.stride;
-    if (dl.nib) {  // 8 codes per lane -> one u32, code k of the 8 in nibble k
-      for (uint32_t j = lane * 8; j < L; j += 512) {
-        uint32_t w = 0;
+    for (uint32_t c = c0; c < K && c * 8 < L; c += 64) {
+      const uint32_t j = c * 8;
+      uint32_t v[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) v[k] = j + k < L ? src[j + k] : 0u;
+      if (dl.nib) {  // code k of the chunk in nibble k (SWK_PACK_NIBBLE)
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) x |= (v[k] & 15u) << (4 * k);
+        *reinterpret_cast<uint32_t*>(dst + (size_t)c * 4) = x;
+      } else if (wide) {
+        *reinterpret_cast<uint2*>(dst + j) =
+            make_uint2(v[0] | v[1] << 8 | v[2] << 16 | v[3] << 24,
+                       v[4] | v[5] << 8 | v[6] << 16 | v[7] << 24);
+      } else {
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
-          if (j + k < L) w |= (uint32_t)(src[j + k] & 15u) << (4 * k);
-        *reinterpret_cast<uint32_t*>(dst + j / 2) = w;
+          if (j + k < L) dst[j + k] = (uint8_t)v[k];
       }
-    } else {
-      for (uint32_t j = lane; j < L; j += 64) dst[j] = src[j];
     }
-    if (lane == 0) {
+    if (c0 == 0) {
       dl.offs[d][i] = (unsigned long long)i * dl.stride;
       dl.lens[d][i] = L;
     }
@@ -134,7 +155,8 @@ extern "C" hipError_t swk_deal_gather(const uint8_t* res, const uint64_t* offs,
                                       hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (!deal || deal->D == 0 || deal->D > SWK_DEAL_MAX || deal->stride == 0) return hipErrorInvalidValue;
-  const size_t blocks = std::min<size_t>((n + 3) / 4, 8192);
+  const uint32_t K = swk::deal_chunks(*deal), tpw = K >= 64 ? 1u : 64u / K;
+  const size_t blocks = std::min<size_t>(((n + tpw - 1) / tpw + 3) / 4, (size_t)1 << 20);
   hipLaunchKernelGGL(swk::deal_gather, dim3((unsigned)blocks), dim3(256), 0, st, res, offs, lens,
                      perm, ident, n, *deal);
   return hipGetLastError();

@@ -790,8 +790,12 @@ struct ScoreArgs {
   // scored in two visits, the head by wave g - 1 first, the tail by wave g last, the lane state
   // handed over through bal_state (WBAL_WORDS x 64 words a wave) and bal_flag[g] = bal_gen
   uint32_t wbal_blocks, wbal_grid;
+  // (TRIM variants) sidx: position k's score goes to sidx[k] (the sort's permutation, ident
+  // honoured) while its codes, offsets and lengths are read at k (a copy of the batch in its
+  // visiting order, SWBANK_RAGGED_GATHER)
+  const uint32_t* sidx;
 };
-static_assert(sizeof(ScoreArgs) == 368, "ScoreArgs layout (kernel argument block) changed");
+static_assert(sizeof(ScoreArgs) == 376, "ScoreArgs layout (kernel argument block) changed");
 
 // a hand-off wait ran out: mark the launch's fault word (a vector store to host memory; only the
 // host reads it, after the launch completed)

@@ -35,6 +35,8 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
   size_t n = a.n;
   const uint32_t* idx = a.idx;
   if (idx && a.ident && __builtin_amdgcn_readfirstlane(*a.ident)) idx = nullptr;
+  const uint32_t* sidx = TRIM ? a.sidx : nullptr;  // (scores only, see ScoreArgs.sidx)
+  if (TRIM && sidx && a.ident && __builtin_amdgcn_readfirstlane(*a.ident)) sidx = nullptr;
   if (idx) {
     const uint32_t cnt = __builtin_amdgcn_readfirstlane(*a.nidx);
     n = cnt > a.idx_base ? min(a.n, (size_t)(cnt - a.idx_base)) : 0;
@@ -635,8 +637,9 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
             blo = f16_unscore((uint32_t)blo);
             bhi = f16_unscore((uint32_t)bhi);
           }
-          size_t slo = idx && tlo < n ? idx[tlo] : tlo;
-          size_t shi = idx && thi < n ? idx[thi] : thi;
+          const uint32_t* sx = TRIM && sidx ? sidx : idx;
+          size_t slo = sx && tlo < n ? sx[tlo] : tlo;
+          size_t shi = sx && thi < n ? sx[thi] : thi;
           if constexpr (STREAM) {  // ragged: through the chunk's visiting order
             if (wperm) {
               const size_t b0 = (size_t)wst0 * SWB_TILE;
@@ -920,10 +923,10 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
                                           const uint32_t* nidx, const uint32_t* ident,
                                           const void* plan, uint32_t* fault, uint32_t poll_limit,
                                           uint32_t stall, int trim, uint32_t packed,
-                                          hipStream_t st) {
+                                          const uint32_t* sidx, hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (W > 4 || !flag || !state || !plan || !fault || poll_limit == 0 || (idx && !nidx) ||
-      (packed != SWK_PACK_BYTES && packed != SWK_PACK_NIBBLE))
+      (packed != SWK_PACK_BYTES && packed != SWK_PACK_NIBBLE) || (sidx && (!trim || idx)))
     return hipErrorInvalidValue;
   swk::ScoreArgs a{res,  offs, lens, n,  qtab, nv, S,
                    O,    E,    PS,   pad, scores, nullptr, nullptr, 0u, 0u, packed,
@@ -940,6 +943,7 @@ extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* of
   a.fault = fault;
   a.poll_limit = poll_limit;
   a.stall = stall;
+  a.sidx = sidx;
   if (trim)  // (a ragged batch: its tiles' last chunks stop at their last column)
     return swk::launch_score<32, 4, false, false, false, true, true, false, false, 8, true, true>(
         a, W, 0, st, grid);

@@ -405,12 +405,12 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
           }
           // (A/B, SWBANK_RAGGED_GATHER=1) a ragged batch copied in its sorted order first, at a
           // 16-byte aligned stride (swk_deal_gather, one device), scored without the
-          // permutation, the scores scattered back (swk_deal_scatter): a tile's targets are then
-          // neighbours in memory (the codes' scatter)
-          // (=2: 4-bit codes, SWK_PACK_NIBBLE, for alphabets of <= 16 codes)
-          const int gmode = rbal ? env_int("SWBANK_RAGGED_GATHER", 0) : 0;
+          // permutation, each score written through it (ScoreArgs.sidx): a tile's targets are
+          // then neighbours in memory (the codes' scatter).  =2: the copy in 4-bit
+          // codes (SWK_PACK_NIBBLE), for alphabets of <= 16 codes
+          const int gmode = rbal && ragged_trim() ? env_int("SWBANK_RAGGED_GATHER", 0) : 0;
           const bool gat = gmode != 0;
-          const bool gnib = gmode == 2 && b->alpha <= 16;
+          const bool gnib = gat && gmode == 2 && b->alpha <= 16;
           SwkDeal dl{};
           if (gat) {
             const size_t stride = ((gnib ? ((size_t)max_len + 7) / 8 * 4 : (size_t)max_len) + 15) &
@@ -418,18 +418,11 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
             HIPOK(b, b->res.reserve(n * stride + 16));
             HIPOK(b, b->offs.reserve(n));
             HIPOK(b, b->lens.reserve(n));
-            HIPOK(b, b->scores.reserve(n));
-            if (!b->one_word.p) {
-              HIPOK(b, b->one_word.reserve(1));
-              const uint32_t one = 1;
-              HIPOK(b, hipMemcpyAsync(b->one_word.p, &one, 4, hipMemcpyHostToDevice, st));
-            }
             dl.D = 1;
             dl.stride = (unsigned)stride;
             dl.codes[0] = b->res.p;
             dl.offs[0] = reinterpret_cast<unsigned long long*>(b->offs.p);
             dl.lens[0] = b->lens.p;
-            dl.scores[0] = b->scores.p;
             dl.cnt[0] = n;
             dl.nib = gnib ? 1u : 0u;
             HIPOK(b, swk_deal_gather(res, offs, lens, idx, ident, n, &dl, st));
@@ -437,18 +430,19 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
           HIPOK(b, swk_launch_pair_bal(gat ? b->res.p : res, gat ? b->offs.p : offs,
                                        gat ? b->lens.p : lens, np, b->qpair.p, b->nv16, b->S, b->O,
                                        b->E, b->pair_bytes, b->pad, Wl,
-                                       gat ? b->scores.p : scores, b->pS1, b->pS2, ulen,
+                                       scores, b->pS1, b->pS2, ulen,
                                        ustride, b->bal_flag.p, b->bal_state.p, ++b->bal_gen, grid,
                                        gat ? nullptr : idx, gat ? nullptr : nidx,
-                                       gat ? b->one_word.p : ident, b->bal_plan.p,
+                                       ident, b->bal_plan.p,
                                        fw + (b->host_call ? 1 : 0), poll_limit(1u << 23),
                                        (uint32_t)std::max(0, env_int("SWBANK_STALL", 0)),
                                        rbal && ragged_trim(),
-                                       gnib ? (uint32_t)SWK_PACK_NIBBLE : (uint32_t)SWK_PACK_BYTES, st));
-          if (gat) HIPOK(b, swk_deal_scatter(idx, ident, n, 1, n, &dl, scores, st));
+                                       gnib ? (uint32_t)SWK_PACK_NIBBLE : (uint32_t)SWK_PACK_BYTES,
+                                       gat ? idx : nullptr, st));
           ++b->ctr.balanced_calls;
           const size_t L = strlen(b->last_kernel);
-          snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " balanced grid=%u", grid);
+          snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " balanced grid=%u%s", grid,
+                   gnib ? " gather4" : gat ? " gather" : "");
           continue;
         }
       }
