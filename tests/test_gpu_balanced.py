@@ -153,3 +153,46 @@ def test_balanced_ranges_ragged(qlen, lo, hi, n, poisoned_buffers, monkeypatch):
     want = O.score_batch(q, res, np.ascontiguousarray(offs[rows]), np.ascontiguousarray(lens[rows]),
                          O.dna_matrix(*REF[:2]), *REF[2:])
     assert np.array_equal(a1[rows], want)
+
+
+@pytest.mark.parametrize("mode,tag", [("1", "gather"), ("2", "gather4")])
+def test_ragged_sorted_copy(mode, tag, poisoned_buffers, monkeypatch):
+    """SWBANK_RAGGED_GATHER (opt-in): the ragged batch copied in its sorted order
+    (bytes, or 4-bit codes) and scored without the permutation, each score written through it;
+    bit-exact against the default permuted reads on every target, N codes included."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(17)
+    n, lo, hi, qlen = 700_001, 64, 150, 128  # (balanced: tiles x 8 >= 2 x grid x 19 chunks)
+    q = O.random_codes(71, qlen, 4)
+    lens = rng.integers(lo, hi + 1, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    res = O.random_codes(72, int(lens.sum(dtype=np.uint64)), 4)
+    res[rng.choice(res.size, res.size // 100, replace=False)] = 4  # N
+    for k in rng.choice(n, n // 50, replace=False):
+        m = int(min(lens[k], qlen))
+        res[int(offs[k]):int(offs[k]) + m] = q[:m]
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+
+    def run(gather):
+        monkeypatch.setenv("SWBANK_RAGGED_GATHER", gather)
+        with S.ScoreBank() as bank:
+            bank.set_penalties(*REF)
+            bank.load_query(q)
+            sc = torch.full((n,), -7, dtype=torch.int32, device=dev)
+            bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, hi,
+                                    sc.data_ptr(), min_len=lo)
+            torch.cuda.synchronize()
+            return sc.cpu().numpy(), bank.last_kernel()
+
+    got, kern = run(mode)
+    want, kern0 = run("0")
+    assert kern.endswith(tag) and "gather" not in kern0, (kern, kern0)
+    assert np.array_equal(got, want)
+    rows = np.unique(np.concatenate([rng.choice(n, 2000, replace=False), np.arange(100)]))
+    ref = O.score_batch(q, res, np.ascontiguousarray(offs[rows]), np.ascontiguousarray(lens[rows]),
+                        O.dna_matrix(*REF[:2]), *REF[2:])
+    assert np.array_equal(got[rows], ref)
