@@ -17,6 +17,6 @@ for r in $(seq 1 $ROUNDS); do
     env $ev timeout -k 10 300 python bench.py --workload $W --cpu-seconds 0 ${BENCH_ARGS:-} \
       > "$OUT/ab_${TAG}_${i}_$r.json" 2> "$OUT/ab_${TAG}_${i}_$r.err"
     rc=$?; [ $rc -eq 0 ] || { echo "bench ${E[$i]} rc=$rc"; tail -3 "$OUT/ab_${TAG}_${i}_$r.err"; exit $rc; }
-    python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['kernel_ms']['score'], d['roofline']['frac'], d['parity_sample']['mismatches'], d['kernel'][-50:])" "$OUT/ab_${TAG}_${i}_$r.json" "${E[$i]}"
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['kernel_ms']['score'], d['roofline']['frac'], d['parity_sample']['mismatches'], (d.get('pcie_inclusive') or {}).get('ms'), d['kernel'][-50:])" "$OUT/ab_${TAG}_${i}_$r.json" "${E[$i]}"
   done
 done

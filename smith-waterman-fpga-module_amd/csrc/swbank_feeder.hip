@@ -89,12 +89,16 @@ static size_t chunk_target(size_t total) {
 
 // Cumulative chunk boundaries (in input bytes) of a host batch: the first chunk a quarter of
 // chunk_target() (at least 1 MiB) so the GPU starts early, then doubling up to chunk_target()
-// (SWBANK_CHUNK_MB: fixed size).  Boundaries strictly inside (0, total).
-static std::vector<size_t> chunk_bounds(size_t total) {
+// (SWBANK_CHUNK_MB: fixed size).  Boundaries strictly inside (0, total).  min_bytes: no chunk
+// smaller (the last one included), unless SWBANK_CHUNK_MB is set.
+static std::vector<size_t> chunk_bounds(size_t total, size_t min_bytes = 0) {
   std::vector<size_t> bounds;
-  const size_t cap = chunk_target(total);
-  size_t sz = env_int("SWBANK_CHUNK_MB", 0) > 0 ? cap : std::max<size_t>(1 << 20, cap / 4);
-  for (size_t at = sz; at < total; at += sz, sz = std::min(cap, sz * 2)) bounds.push_back(at);
+  const bool fixed = env_int("SWBANK_CHUNK_MB", 0) > 0;
+  if (fixed) min_bytes = 0;
+  const size_t cap = std::max(chunk_target(total), min_bytes);
+  size_t sz = fixed ? cap : std::max<size_t>({(size_t)1 << 20, cap / 4, min_bytes});
+  for (size_t at = sz; at < total && total - at >= min_bytes; at += sz, sz = std::min(cap, sz * 2))
+    bounds.push_back(at);
   return bounds;
 }
 
@@ -518,7 +522,17 @@ static sw_status batch_feed_once(sw_bank* b, const uint8_t* residues, size_t nre
   // residue, or, for a DNA chunk without N, the 2-bit stream (a quarter of the PCIe bytes;
   // SWBANK_PACK2=0 disables), each target from a byte boundary, 16 zero bytes after the last
   const auto codes_at = [](size_t cnt) { return align16(cnt * 16 + 8); };
-  std::vector<size_t> bounds = chunk_bounds(total);
+  // A batch for the wave kernel: every launch holds at least one unit per resident wave slot (a
+  // launch of fewer units leaves SIMDs idle for a whole unit's time: configs[4]'s 12,500
+  // targets in 2 + 4 + 6.5 MB chunks took 1.63 ms through this path, in one chunk 1.22 ms,
+  // the kernel alone 0.81)
+  size_t min_chunk = 0;
+  if (max_len && wave_preferred(b, n, max_len, b->f16 && b->f16_neg >= -2048 &&
+                                                   env_int("SWBANK_F16", 1) != 0)) {
+    const unsigned grid = swk_wave_half_grid(b->gotoh() ? 1 : 0, (b->pad + 1) * b->wPS16);
+    min_chunk = (size_t)(grid ? grid : 1024) * 16 * max_len;  // 4 waves x 2 pairs x 2 targets
+  }
+  std::vector<size_t> bounds = chunk_bounds(total, min_chunk);
   bounds.push_back(SIZE_MAX);  // sentinel
   for (size_t i = 0; i < nblk; ++i) cpre[i + 1] += cpre[i];
   std::vector<Chunk> chunks;
