@@ -102,6 +102,12 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
 #ifndef SWK_HALF_AHEAD
 #define SWK_HALF_AHEAD 1  // two-pairs wave kernel: profile words one step ahead
 #endif
+#ifndef SWK_HALF_DPPSEL
+// two-pairs wave kernel: the row above moves down and each half's lane 0 takes the row -1
+// boundary in ONE v_cndmask_b32_dpp per value (the shift as the select's DPP operand, the
+// boundary lanes in VCC) instead of a DPP move and a v_cndmask
+#define SWK_HALF_DPPSEL 1
+#endif
 #ifndef SWK_HALF_FMA
 // two-pairs wave kernel: LDS profile words {s, 1.0} (4 B per letter and row) added with one
 // op_sel FMA per row (gen_f16_rows.py mode F) instead of 2-byte entries interleaved by a v_perm
@@ -814,6 +820,11 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
     botX = __hip_atomic_load(sp + (2 * K + 3) * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const bool top = hl == 0;  // row -1 of this half's pair
+  // (SWK_HALF_DPPSEL) the boundary lanes 0 and 32, and row -1's H and F / T in VGPRs
+  const uint64_t topmask = 0x0000000100000001ull;
+  uint32_t h0v = as_u32(H0), x0v = as_u32(X0);
+  asm volatile("" : "+v"(h0v), "+v"(x0v));
+  (void)topmask;
   // the codes of column c of this half's targets (pad past the end) as {A, B << 8}
   const auto load_codes = [&](const uint32_t c) __attribute__((always_inline)) -> uint32_t {
     uint32_t x = pad, y = pad;
@@ -908,15 +919,33 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
     if constexpr (AHEAD) {
       lk = lkn;
       load_prof(lkn, nra, nrb);
-      const RingT* np = rp + (t & 1);
+      const RingT* np = rp + (even ? 0 : 1);  // (t is even in an even step: an immediate offset)
       nra = np[0];
       nrb = np[64];
       __builtin_amdgcn_sched_barrier(0);
     }
-    u16x2 upH = as_u16x2(dpp_shr1_zero(botH));
-    u16x2 upX = as_u16x2(GOTOH ? dpp_shr1_zero(botX) : dpp_shr1(as_u32(X0), botX));
-    upH = top ? H0 : upH;
-    upX = top ? X0 : upX;
+    u16x2 upH, upX;
+    if constexpr (SWK_HALF_DPPSEL != 0) {
+      // lanes 0 and 32 in VCC: v_cndmask_b32 D = VCC ? src1 : src0, src0 read through
+      // wave_shr:1 (bound_ctrl: lane 0 reads 0 and is written); s_nop 1: the two wait states a
+      // DPP read needs after the VALU write of its source (inside asm LLVM inserts none)
+      uint32_t uh, ux;
+      asm volatile(
+          "s_nop 1\n\t"
+          "s_mov_b64 vcc, %[m]\n\t"
+          "v_cndmask_b32_dpp %[uh], %[bh], %[h0], vcc wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+          "v_cndmask_b32_dpp %[ux], %[bx], %[x0], vcc wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+          : [uh] "=&v"(uh), [ux] "=&v"(ux)
+          : [bh] "v"(botH), [bx] "v"(botX), [h0] "v"(h0v), [x0] "v"(x0v), [m] "s"(topmask)
+          : "vcc");
+      upH = as_u16x2(uh);
+      upX = as_u16x2(ux);
+    } else {
+      upH = as_u16x2(dpp_shr1_zero(botH));
+      upX = as_u16x2(GOTOH ? dpp_shr1_zero(botX) : dpp_shr1(as_u32(X0), botX));
+      upH = top ? H0 : upH;
+      upX = top ? X0 : upX;
+    }
     u16x2 diag = prevUpH;
     prevUpH = upH;
     __builtin_amdgcn_sched_barrier(0);
