@@ -177,6 +177,8 @@ def test_ragged_sorted_copy(mode, tag, poisoned_buffers, monkeypatch):
     d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
     d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
 
+    monkeypatch.setenv("SWBANK_TRIM", "1")  # (the copy's scores go through the trimmed kernel)
+
     def run(gather):
         monkeypatch.setenv("SWBANK_RAGGED_GATHER", gather)
         with S.ScoreBank() as bank:
