@@ -314,7 +314,13 @@ def main():
 
     wl = Workload(args, rank, dev, S, torch)
     gdev = dev if backend == "nccl" else torch.device("cpu")
-    stream = torch.cuda.current_stream()
+    # The scoring stream, made torch's current one: on ROCm the default current stream's handle
+    # is 0, which the library reads as "the bank's own (non-blocking) stream", so a score copy
+    # or collective enqueued by torch on the default stream would not wait for the kernel (the
+    # gathered scores of a 2-rank run were then stale now and then: tests/test_gpu_bench.py)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    assert stream.cuda_stream != 0
     # Two score buffers: step i scores into one while the async gather of step i-1 (RCCL's
     # stream) still reads the other (swbank.dist.StepGather; gloo gathers a host copy).  The
     # CPU tests run this same class under gloo (tests/test_dist.py).
@@ -514,7 +520,7 @@ def parity_sample(wl, per_rank, m=4096, full_cells=2e10):
         pick = np.random.default_rng(12345).integers(0, wl.n, m // 2)
         rows = np.unique(np.concatenate([np.arange(min(m // 4, wl.n)),
                                          np.arange(max(0, wl.n - m // 4), wl.n), pick]))
-    mism, checked = 0, 0
+    mism, checked, by_rank = 0, 0, []
     for r, sc in enumerate(per_rank):
         gpu = sc.cpu().numpy()
         if r == wl.rank:  # this rank's own batch is on the host already
@@ -522,13 +528,18 @@ def parity_sample(wl, per_rank, m=4096, full_cells=2e10):
                 np.ascontiguousarray(wl.lens[rows])
         else:
             res, offs, lens = wl.regen_rows(r, rows)
+        m0 = mism
         for k, q in enumerate(wl.queries):
             cpu = O.score_batch(q, res, offs, lens, sub, go, ge, model)
             mism += int((cpu != gpu[k][rows]).sum())
             checked += len(rows)
-    return {"targets": checked, "ranks": len(per_rank), "mismatches": mism,
+        by_rank.append(mism - m0)
+    out = {"targets": checked, "ranks": len(per_rank), "mismatches": mism,
             "of_targets": len(per_rank) * len(wl.queries) * wl.n,
             "full": bool(len(rows) == wl.n)}
+    if len(per_rank) > 1:
+        out["mismatches_by_rank"] = by_rank
+    return out
 
 
 def cpu_baseline(q, tg, d_sc, L, budget_s):

@@ -367,7 +367,10 @@ class ScoreBank:
         """Device pointers (ints, e.g. torch.Tensor.data_ptr()); async on `stream`.  With d_ids
         the call also records the batch best hit on the device (best()).  With min_len (every
         length in [min_len, max_len]) the call is sw_score_batch_device_range: a range of one
-        length skips the on-device length sort."""
+        length skips the on-device length sort.  stream 0 is the BANK's own non-blocking stream
+        (the C ABI's NULL), not HIP's default stream; torch's default current stream has handle
+        0 on ROCm, so pass a torch.cuda.Stream's cuda_stream (or sync()) before torch reads the
+        scores."""
         if min_len is None:
             self._check(lib().sw_score_batch_device(self._h, d_res, d_offs, d_lens,
                                                     d_ids or None, n, max_len, d_scores,
