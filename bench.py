@@ -319,6 +319,7 @@ def main():
     # or collective enqueued by torch on the default stream would not wait for the kernel (the
     # gathered scores of a 2-rank run were then stale now and then: tests/test_gpu_bench.py)
     stream = torch.cuda.Stream(device=dev)
+    stream.wait_stream(torch.cuda.current_stream())  # (the workload's uploads and fills)
     torch.cuda.set_stream(stream)
     assert stream.cuda_stream != 0
     # Two score buffers: step i scores into one while the async gather of step i-1 (RCCL's
