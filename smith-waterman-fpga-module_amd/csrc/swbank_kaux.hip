@@ -81,57 +81,118 @@ namespace swk {
 __device__ __forceinline__ size_t deal_target(const uint32_t* perm, bool id, size_t p) {
   return id ? p : (size_t)perm[p];
 }
-// 8-code chunks per target slot (K); a wave's lanes take the chunks of 64 / K positions
-// (K <= 64) or of one, each lane 8 codes -> one u64 of bytes or one u32 of 4-bit codes.  (One
-// lane per position, each looping over its chunks: 3.1x slower, every load instruction touching
-// 64 lines; one wave per position: 2.9x slower, a third of the lanes busy.  DESIGN 3.6)
-__host__ __device__ __forceinline__ uint32_t deal_chunks(const SwkDeal& dl) {
-  return dl.nib ? dl.stride / 4 : (dl.stride + 7) / 8;
+// A wave takes 64 positions at a time: lane l reads position l's metadata (one coalesced load
+// per array), then each 16-lane quarter copies one position per step, 4 per step, lane k of a
+// quarter chunk k (8 codes), the chunks past the 16th (targets over 128 codes) after.  A chunk
+// is read as the 2-3 aligned dwords that hold it, each loaded only when it holds a byte of the
+// target (an aligned dword never crosses a page, so no read can fault past the buffer), and
+// funnel-shifted (v_alignbyte): no branch around a load, so all 16 steps' loads are in flight
+// before the first store.  Each chunk goes out as one u64 of bytes or one u32 of 4-bit codes.
+// (Byte loads for a target's last chunk serialised the steps on their waits: 134 us for the
+// ragged bench batch; one wave per position, or one lane per position looping over its chunks:
+// 3-4x slower still.  DESIGN 3.6)
+__device__ __forceinline__ uint32_t nib_pack4(uint32_t w) {  // 4 code bytes -> 16 bits
+  uint32_t t = w & 0x0F0F0F0Fu;
+  t = (t | (t >> 4)) & 0x00FF00FFu;
+  return (t | (t >> 8)) & 0x0000FFFFu;
+}
+struct DealWords {  // the aligned dwords holding one 8-code chunk
+  uint32_t w0, w1, w2;
+};
+__device__ __forceinline__ DealWords deal_load(const uint8_t* src, uint32_t L, uint32_t j) {
+  DealWords r{0u, 0u, 0u};
+  const uint32_t m = (uint32_t)(reinterpret_cast<uintptr_t>(src + j) & 3);
+  // (pointer arithmetic from src, not from an integer: the loads stay global, not flat)
+  const uint32_t* ap = reinterpret_cast<const uint32_t*>(src + j - m);
+  const uint32_t e = L - j + m;  // bytes from the first dword's start to the target's end
+  if (j < L) r.w0 = ap[0];
+  if (j < L && e > 4) r.w1 = ap[1];
+  if (j < L && m && e > 8) r.w2 = ap[2];
+  return r;
+}
+// the chunk's 8 codes (zero past the target's end)
+__device__ __forceinline__ uint2 deal_codes(const DealWords& w, const uint8_t* src, uint32_t L,
+                                            uint32_t j) {
+  const uint32_t m = (uint32_t)((reinterpret_cast<uintptr_t>(src) + j) & 3);
+  uint2 v = make_uint2(__builtin_amdgcn_alignbyte(w.w1, w.w0, m),
+                       __builtin_amdgcn_alignbyte(w.w2, w.w1, m));
+  const uint32_t nv = L > j ? min(L - j, 8u) : 0u;
+  if (nv < 8) {
+    const uint64_t keep = (1ull << (8 * nv)) - 1;
+    const uint64_t x = ((uint64_t)v.y << 32 | v.x) & keep;
+    v = make_uint2((uint32_t)x, (uint32_t)(x >> 32));
+  }
+  return v;
 }
 __global__ void __launch_bounds__(256) deal_gather(const uint8_t* res, const uint64_t* offs,
                                                    const uint32_t* lens, const uint32_t* perm,
                                                    const uint32_t* ident, size_t n,
                                                    const SwkDeal dl) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t K = deal_chunks(dl);
-  const uint32_t tpw = K >= 64 ? 1u : 64u / K;  // positions per wave
-  const uint32_t g = K >= 64 ? 0u : lane / K, c0 = K >= 64 ? lane : lane - g * K;
+  const uint32_t lane = threadIdx.x & 63, qd = lane >> 4, ql = lane & 15;
   const size_t w0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const size_t nw = ((size_t)gridDim.x * blockDim.x) >> 6;
   const bool id = !perm || (ident && *ident != 0);
   const bool wide = (dl.stride & 7u) == 0;  // whole u64 stores stay inside the slot
-  for (size_t w = w0; w * tpw < n; w += nw) {
-    const size_t p = w * tpw + g;
-    if (g >= tpw || p >= n) continue;
-    const size_t t = deal_target(perm, id, p);
-    const unsigned d = (unsigned)(p % dl.D);
-    const size_t i = p / dl.D;
-    const uint32_t L = lens[t];
-    const uint8_t* src = res + offs[t];
-    uint8_t* dst = dl.codes[d] + i * dl.stride;
-    for (uint32_t c = c0; c < K && c * 8 < L; c += 64) {
-      const uint32_t j = c * 8;
-      uint32_t v[8];
+  const auto store = [&](uint8_t* dst, uint32_t L, uint32_t c, uint2 v) {
+    const uint32_t j = c * 8;
+    if (dl.nib) {  // code k of the chunk in nibble k (SWK_PACK_NIBBLE)
+      *reinterpret_cast<uint32_t*>(dst + (size_t)c * 4) = nib_pack4(v.x) | nib_pack4(v.y) << 16;
+    } else if (wide) {
+      *reinterpret_cast<uint2*>(dst + j) = v;
+    } else {
+      const uint64_t x = (uint64_t)v.y << 32 | v.x;
 #pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) v[k] = j + k < L ? src[j + k] : 0u;
-      if (dl.nib) {  // code k of the chunk in nibble k (SWK_PACK_NIBBLE)
-        uint32_t x = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) x |= (v[k] & 15u) << (4 * k);
-        *reinterpret_cast<uint32_t*>(dst + (size_t)c * 4) = x;
-      } else if (wide) {
-        *reinterpret_cast<uint2*>(dst + j) =
-            make_uint2(v[0] | v[1] << 8 | v[2] << 16 | v[3] << 24,
-                       v[4] | v[5] << 8 | v[6] << 16 | v[7] << 24);
-      } else {
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k)
-          if (j + k < L) dst[j + k] = (uint8_t)v[k];
-      }
+      for (uint32_t k = 0; k < 8; ++k)
+        if (j + k < L) dst[j + k] = (uint8_t)(x >> (8 * k));
     }
-    if (c0 == 0) {
-      dl.offs[d][i] = (unsigned long long)i * dl.stride;
-      dl.lens[d][i] = L;
+  };
+  for (size_t base = w0 * 64; base < n; base += nw * 64) {
+    const size_t p = base + lane;
+    const bool live = p < n;
+    const size_t t = live ? deal_target(perm, id, p) : 0;
+    const uint32_t Lm = live ? lens[t] : 0u;
+    const uint64_t om = live ? offs[t] : 0u;
+    const uint32_t dm = (uint32_t)(p % dl.D);
+    const uint64_t im = p / dl.D;
+    if (live) {
+      dl.offs[dm][im] = im * dl.stride;
+      dl.lens[dm][im] = Lm;
+    }
+    // position 4 s + qd's source and slot (the metadata from its lane; every lane active)
+    const auto src_of = [&](int sl) {
+      const uint64_t o = (uint64_t)(uint32_t)__shfl((int)(uint32_t)om, sl) |
+                         (uint64_t)(uint32_t)__shfl((int)(uint32_t)(om >> 32), sl) << 32;
+      return res + o;
+    };
+    const auto dst_of = [&](int sl) {
+      const uint32_t d = (uint32_t)__shfl((int)dm, sl);
+      const uint64_t i = (uint64_t)(uint32_t)__shfl((int)(uint32_t)im, sl) |
+                         (uint64_t)(uint32_t)__shfl((int)(uint32_t)(im >> 32), sl) << 32;
+      return dl.codes[d] + i * dl.stride;
+    };
+    DealWords w[16];
+    uint32_t Ls[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {  // loads: position 4 s + qd, chunk ql
+      const int sl = 4 * s + (int)qd;
+      Ls[s] = (uint32_t)__shfl((int)Lm, sl);  // (0 past the batch end)
+      w[s] = deal_load(src_of(sl), Ls[s], ql * 8);
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int sl = 4 * s + (int)qd;
+      const uint8_t* src = src_of(sl);
+      uint8_t* dst = dst_of(sl);
+      if (ql * 8 < Ls[s]) store(dst, Ls[s], ql, deal_codes(w[s], src, Ls[s], ql * 8));
+    }
+    for (int s = 0; s < 16; ++s) {  // chunks 16 on (targets of more than 128 codes)
+      const int sl = 4 * s + (int)qd;
+      if (__builtin_amdgcn_readfirstlane(__ballot(Ls[s] > 128u) != 0)) {
+        const uint8_t* src = src_of(sl);
+        uint8_t* dst = dst_of(sl);
+        for (uint32_t c = ql + 16; c * 8 < Ls[s]; c += 16)
+          store(dst, Ls[s], c, deal_codes(deal_load(src, Ls[s], c * 8), src, Ls[s], c * 8));
+      }
     }
   }
 }
@@ -155,8 +216,7 @@ extern "C" hipError_t swk_deal_gather(const uint8_t* res, const uint64_t* offs,
                                       hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (!deal || deal->D == 0 || deal->D > SWK_DEAL_MAX || deal->stride == 0) return hipErrorInvalidValue;
-  const uint32_t K = swk::deal_chunks(*deal), tpw = K >= 64 ? 1u : 64u / K;
-  const size_t blocks = std::min<size_t>(((n + tpw - 1) / tpw + 3) / 4, (size_t)1 << 20);
+  const size_t blocks = std::min<size_t>((n + 255) / 256, (size_t)1 << 20);  // 64 per wave
   hipLaunchKernelGGL(swk::deal_gather, dim3((unsigned)blocks), dim3(256), 0, st, res, offs, lens,
                      perm, ident, n, *deal);
   return hipGetLastError();
