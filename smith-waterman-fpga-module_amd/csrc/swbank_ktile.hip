@@ -9,6 +9,13 @@ namespace swk {
 // TRIM: a tile's last chunk stops after its last column holding a code of some lane (ragged
 // batches: a tile's lengths are one sort bin, rarely a multiple of C; the per-column test costs
 // a uniform batch ~25 VALU per chunk in register copies, so only the ragged launches take it).
+#ifndef SWK_TRIM_BREAK
+// TRIM: leave the chunk's column loop at the first column past the tile's last code (break)
+// rather than skipping each later column (continue): the continue form's per-column joins cost
+// 25 register copies per chunk on every chunk (1,475 VALU against 1,450), the break form's
+// exits are out of line (1,458)
+#define SWK_TRIM_BREAK 1
+#endif
 template <int R, int RB, bool COL0, bool PROF, bool GOTOH, bool F16, bool PAIR = false,
           bool MQ = false, bool STREAM = false, int C = 8, bool BAL = false, bool TRIM = false>
 __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const ScoreArgs a) {
@@ -448,7 +455,11 @@ __global__ void __launch_bounds__(R >= 64 ? 512 : 1024) score_kernel(const Score
       for (int jj = 0; jj < C; ++jj) {
         if (TRIM && jj > 0 && __builtin_expect(jj >= ncols, 0)) {
           trimmed = true;
+#if SWK_TRIM_BREAK
+          break;  // (every later column is past ncols too: one exit edge per column, out of line)
+#else
           continue;
+#endif
         }
         const u16x2 upH = as_u16x2(rv.x);
         u16x2 upX = as_u16x2(rv.y);
