@@ -339,3 +339,46 @@ def test_feeder_mixed_bad_code(monkeypatch):
             bank.score_batch(bad, offs, lens)
         assert ei.value.status == S.ERR_ARG and f"target {k}" in str(ei.value)
         assert (bank.score_batch(res, offs, lens) >= 0).all()
+
+
+@pytest.mark.parametrize("n,want_chunks", [(12_500, 1), (60_000, None)])
+def test_feeder_wave_batch_chunk_floor(monkeypatch, n, want_chunks):
+    """A host batch the wave kernel takes (configs[4]'s protein shape) is cut in chunks of at
+    least one unit per resident wave slot: 12,500 x 1,000 aa go as ONE launch (they went as
+    three, each leaving SIMDs idle for a unit's time), a larger batch as several whose every
+    launch still fills the slots; scores equal the device API's and the oracle's."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.delenv("SWBANK_CHUNK_MB", raising=False)
+    rng = np.random.default_rng(n)
+    L = 1000
+    res = rng.integers(0, 20, n * L, dtype=np.uint8)
+    offs = np.arange(n, dtype=np.uint64) * L
+    lens = np.full(n, L, np.uint32)
+    q = rng.integers(0, 20, 512, dtype=np.uint8)
+    with S.ScoreBank(alphabet=S.ALPHABET_PROTEIN, gap_model=S.GAP_GOTOH) as bank:
+        bank.set_matrix(O.BLOSUM62, -11, -1)
+        bank.load_query(q)
+        bank.timing()
+        bank.set_timing(True)
+        got = bank.score_batch(res, offs, lens)
+        launches, _, _ = bank.timing()
+        bank.set_timing(False)
+        kern = bank.last_kernel()
+        dev = torch.device("cuda", 0)
+        d_sc = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        d_res = torch.from_numpy(res).to(dev)
+        d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+        d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+        bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,
+                                d_sc.data_ptr(), min_len=L)
+        torch.cuda.synchronize()
+    assert kern.startswith("wave"), kern
+    if want_chunks is not None:
+        assert launches == want_chunks, (launches, kern)
+    else:
+        assert 1 < launches <= n // 12_000, (launches, kern)  # each >= 16 x 768 targets
+    assert np.array_equal(got, d_sc.cpu().numpy())
+    sel = rng.choice(n, 120, replace=False)
+    sub = [res[int(offs[k]):int(offs[k]) + L] for k in sel]
+    want = O.score_batch(q, *S.pack_targets(sub), O.BLOSUM62, -11, -1, O.GAP_GOTOH)
+    assert np.array_equal(got[sel], want), kern
