@@ -270,7 +270,7 @@ sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_t* scor
 //     and position p goes to device p % D -- the length-balanced deal of the host path
 //     (multi_batch); a batch of one length keeps its order;
 //  2. one gather kernel on the root copies each device's targets into its region of a staging
-//     buffer at a fixed stride of max_len bytes (offsets rebased, lengths kept);
+//     buffer at a fixed stride of max_len bytes rounded up to 16 (offsets rebased, lengths kept);
 //  3. device d copies its region into its own buffers (hipMemcpyPeerAsync on its stream: codes
 //     cnt_d x max_len bytes + 12 bytes per target), scores them there (launch / launch_set) and
 //     copies its nq x cnt_d int32 scores back into the root's receive buffer;
@@ -321,7 +321,8 @@ sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       cnt[d] = n > d ? (n - d + D - 1) / D : 0;
     }
   }
-  const size_t stride = records ? SWB_RECORD : std::max<uint32_t>(max_len, 1u);
+  // (a 16-byte multiple: the deal gather stores whole 8-code chunks, not bytes)
+  const size_t stride = records ? SWB_RECORD : align16(std::max<uint32_t>(max_len, 1u));
   SwkDeal dl{};
   dl.D = (unsigned)D;
   dl.stride = (unsigned)stride;
