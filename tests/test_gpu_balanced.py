@@ -198,3 +198,61 @@ def test_ragged_sorted_copy(mode, tag, poisoned_buffers, monkeypatch):
     ref = O.score_batch(q, res, np.ascontiguousarray(offs[rows]), np.ascontiguousarray(lens[rows]),
                         O.dna_matrix(*REF[:2]), *REF[2:])
     assert np.array_equal(got[rows], ref)
+
+
+#  SWBANK_BAL_SOAK_SEEDS=n (default 3) / SWBANK_BAL_SOAK_BASE=b: seeds b .. b+n-1 (soak runs)
+_SOAK_BASE = int(__import__("os").environ.get("SWBANK_BAL_SOAK_BASE", "0"))
+_SOAK_SEEDS = int(__import__("os").environ.get("SWBANK_BAL_SOAK_SEEDS", "3"))
+
+
+@pytest.mark.parametrize("seed", range(_SOAK_BASE, _SOAK_BASE + _SOAK_SEEDS))
+def test_balanced_ragged_soak(seed, monkeypatch):
+    """Seeded ragged device batches for the balanced ranges over the device sort's plan: random
+    length ranges (short to 2,047 codes), 4-wave query lengths, N rates and homologs, the
+    batch sized just past the point where balanced ranges apply; bit-exact against whole tiles
+    per workgroup (SWBANK_BAL=0) on every target and against the oracle on a sample."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(40_000 + seed)
+    lo = int(rng.integers(1, 200))
+    hi = int(min(2047, lo + rng.integers(1, 3 * lo + 8)))
+    kmin, kmax = max(1, (lo + 7) // 8), (hi + 7) // 8
+    # balanced ranges need tiles x kmin >= 2 x grid x kmax (grid <= 1024 slots)
+    n = int(2 * 1024 * kmax * 128 / kmin * float(rng.uniform(1.05, 1.5))) + int(rng.integers(0, 128))
+    if n > 3_000_000:
+        pytest.skip(f"lengths {lo}-{hi}: {n} targets")
+    qlen = int(rng.choice([97, 100, 113, 128]))  # 4 waves: the 1,024-slot grid assumed above
+    q = O.random_codes(seed + 17, qlen, 4)
+    lens = rng.integers(lo, hi + 1, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    res = O.random_codes(seed + 23, int(lens.sum(dtype=np.uint64)), 4)
+    if rng.random() < 0.5:
+        res[rng.random(res.size) < float(rng.uniform(0.0, 0.02))] = 4  # N
+    for k in rng.choice(n, n // 40, replace=False):
+        m = int(min(lens[k], qlen))
+        res[int(offs[k]):int(offs[k]) + m] = q[:m]
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+
+    def run(bal):
+        monkeypatch.setenv("SWBANK_BAL", bal)
+        with S.ScoreBank() as bank:
+            bank.set_penalties(*REF)
+            bank.load_query(q)
+            sc = torch.full((n,), -7, dtype=torch.int32, device=dev)
+            bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, hi,
+                                    sc.data_ptr(), min_len=lo)
+            torch.cuda.synchronize()
+            return sc.cpu().numpy(), bank.last_kernel()
+
+    got, kern = run("1")
+    want, kern0 = run("0")
+    assert "balanced" in kern and "balanced" not in kern0, (kern, kern0, lo, hi, n)
+    assert np.array_equal(got, want), (kern, lo, hi, n, int((got != want).sum()))
+    rows = np.unique(np.concatenate([rng.choice(n, 1500, replace=False), np.arange(64),
+                                     np.arange(n - 64, n)]))
+    ref = O.score_batch(q, res, np.ascontiguousarray(offs[rows]), np.ascontiguousarray(lens[rows]),
+                        O.dna_matrix(*REF[:2]), *REF[2:])
+    assert np.array_equal(got[rows], ref), kern
