@@ -132,3 +132,51 @@ def test_wave_balanced_stall_fails_loudly(monkeypatch):
                                 sc.data_ptr(), min_len=L)
         bank.sync()
         assert np.array_equal(sc.cpu().numpy(), want)
+
+
+#  SWBANK_WBAL_SOAK_SEEDS=n (default 3) / SWBANK_WBAL_SOAK_BASE=b: seeds b .. b+n-1
+_WS_BASE = int(__import__("os").environ.get("SWBANK_WBAL_SOAK_BASE", "0"))
+_WS_SEEDS = int(__import__("os").environ.get("SWBANK_WBAL_SOAK_SEEDS", "3"))
+
+
+@pytest.mark.parametrize("seed", range(_WS_BASE, _WS_BASE + _WS_SEEDS))
+def test_wave_balanced_soak(seed, monkeypatch):
+    """Seeded protein batches for the balanced two-pairs kernel: random target length (equal in
+    a batch), query length (500-512 rows), batch size from one unit per wave slot to three, gap
+    model and penalties; bit-exact against the segmented-tail
+    path (SWBANK_WAVE_BAL=0) on every target and against the oracle on a sample."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(70_000 + seed)
+    # (shapes the kernel choice sends to the balanced two-pairs kernel: a query of nearly 512
+    # rows against long targets -- else the tile kernel wins -- and, for merged gaps, o + e
+    # above BLOSUM62's largest score, so the column-0 rule is off)
+    L = int(rng.integers(850, 1300))
+    qlen = int(rng.integers(500, 513))
+    n = int(rng.integers(12_300, 37_000))
+    model = S.GAP_GOTOH if rng.random() < 0.6 else S.GAP_MERGED
+    go, ge = -int(rng.integers(10, 15)), -int(rng.integers(1, 4))
+    q, res, offs, lens = _batch(rng, n, qlen, L)
+    dev = torch.device("cuda", 0)
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+
+    def run(bal):
+        monkeypatch.setenv("SWBANK_WAVE_BAL", bal)
+        with S.ScoreBank(alphabet=S.ALPHABET_PROTEIN, gap_model=model) as bank:
+            bank.set_matrix(O.BLOSUM62, go, ge)
+            bank.load_query(q)
+            sc = torch.full((n,), -7, dtype=torch.int32, device=dev)
+            bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,
+                                    sc.data_ptr(), min_len=L)
+            bank.sync()
+            return sc.cpu().numpy(), bank.last_kernel()
+
+    got, kern = run("1")
+    want, kern0 = run("0")
+    assert "pairs/wave=2" in kern and "balanced" in kern and "balanced" not in kern0, (kern, kern0)
+    assert np.array_equal(got, want), (kern, L, qlen, n, int((got != want).sum()))
+    rows = np.unique(np.concatenate([rng.choice(n, 300, replace=False), np.arange(n - 40, n)]))
+    ref = O.score_batch(q, res, np.ascontiguousarray(offs[rows]), np.ascontiguousarray(lens[rows]),
+                        O.BLOSUM62, go, ge, O.GAP_GOTOH if model == S.GAP_GOTOH else O.GAP_MERGED)
+    assert np.array_equal(got[rows], ref), kern
