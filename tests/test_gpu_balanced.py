@@ -207,8 +207,9 @@ _SOAK_SEEDS = int(__import__("os").environ.get("SWBANK_BAL_SOAK_SEEDS", "3"))
 
 @pytest.mark.parametrize("seed", range(_SOAK_BASE, _SOAK_BASE + _SOAK_SEEDS))
 def test_balanced_ragged_soak(seed, monkeypatch):
-    """Seeded ragged device batches for the balanced ranges over the device sort's plan: random
-    length ranges (short to 2,047 codes), 4-wave query lengths, N rates and homologs, the
+    """Seeded device batches for the balanced ranges, ragged over the device sort's plan (or, one
+    in four, uniform over the host's): random length ranges (short to 2,047 codes), 4-wave query
+    lengths, N rates and homologs, the
     batch sized just past the point where balanced ranges apply; bit-exact against whole tiles
     per workgroup (SWBANK_BAL=0) on every target and against the oracle on a sample."""
     torch = pytest.importorskip("torch")
@@ -216,6 +217,8 @@ def test_balanced_ragged_soak(seed, monkeypatch):
     rng = np.random.default_rng(40_000 + seed)
     lo = int(rng.integers(1, 200))
     hi = int(min(2047, lo + rng.integers(1, 3 * lo + 8)))
+    if rng.random() < 0.25:  # a uniform batch: the host's plan instead of the sort's
+        lo = hi = int(rng.integers(1, 400))
     kmin, kmax = max(1, (lo + 7) // 8), (hi + 7) // 8
     # balanced ranges need tiles x kmin >= 2 x grid x kmax (grid <= 1024 slots)
     n = int(2 * 1024 * kmax * 128 / kmin * float(rng.uniform(1.05, 1.5))) + int(rng.integers(0, 128))
