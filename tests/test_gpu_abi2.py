@@ -478,3 +478,50 @@ def test_multi_device_deal_small_batches(n, poisoned_buffers):
     assert np.array_equal(got_rec, want)
     k = int(np.argmax(want))
     assert best == (k * 3 + 1, int(want[k]), k)
+
+
+#  SWBANK_DEAL_SOAK_SEEDS=n (default 3) / SWBANK_DEAL_SOAK_BASE=b: seeds b .. b+n-1
+_DS_BASE = int(os.environ.get("SWBANK_DEAL_SOAK_BASE", "0"))
+_DS_SEEDS = int(os.environ.get("SWBANK_DEAL_SOAK_SEEDS", "3"))
+
+
+@pytest.mark.parametrize("seed", range(_DS_BASE, _DS_BASE + _DS_SEEDS))
+def test_multi_device_deal_soak(seed):
+    """Seeded device calls on multi-device banks (2-4 devices, every one the box's GPU): random
+    batch sizes, ragged lengths with empties, N codes, scattered offsets; the deal (sort, gather
+    to each device's staging, copies, scatter back) equals a one-device bank on every target."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(90_000 + seed)
+    D = int(rng.integers(2, 5))
+    n = int(rng.choice([int(rng.integers(1, 64)), int(rng.integers(64, 5000)),
+                        int(rng.integers(5000, 60000))]))
+    maxl = int(rng.choice([8, 31, 150, 600]))
+    q = _codes(rng, int(rng.integers(20, 300)))
+    lens = rng.integers(0, maxl + 1, n).astype(np.uint32)
+    gap = rng.integers(0, 9, n).astype(np.uint64) if rng.random() < 0.5 else np.zeros(n, np.uint64)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gap[:-1])
+    total = int(offs[-1] + lens[-1]) + 16
+    res = rng.integers(0, 4, total, dtype=np.uint8)
+    res[rng.random(total) < 0.005] = 4
+    perm = rng.permutation(n) if rng.random() < 0.5 else np.arange(n)
+    offs, lens = np.ascontiguousarray(offs[perm]), np.ascontiguousarray(lens[perm])
+    d_res = torch.from_numpy(res).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    L = max(1, int(lens.max()))
+
+    def run(devices):
+        with S.ScoreBank(devices=devices) as bank:
+            bank.set_penalties(*REF)
+            bank.load_query(q)
+            sc = torch.full((n,), -5, dtype=torch.int32, device=dev)
+            bank.score_batch_device(d_res.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, L,
+                                    sc.data_ptr())
+            bank.sync()
+            return sc.cpu().numpy()
+
+    got = run([0] * D)
+    want = run([0])
+    assert np.array_equal(got, want), (D, n, maxl, int((got != want).sum()))
