@@ -83,7 +83,10 @@ PEN = (5, -4, -12, -4)
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a launcher (no WORLD_SIZE) and N > 1, "
+                         "bench.py starts torch.distributed.run with N ranks itself; under a "
+                         "launcher N must equal WORLD_SIZE (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="q100xdata500",
@@ -287,12 +290,52 @@ class Workload:
                                          d_sc[k].data_ptr(), stream, min_len=self.Lmin)
 
 
+def resolve_world(args) -> int | None:
+    """The rank count `--gpus` asks for, checked against the launcher's WORLD_SIZE BEFORE any
+    GPU call.  Returns the world size to run with, or None when this process has started the
+    N ranks itself (it then only waits for them).  A mismatch exits non-zero: a line printed
+    with the wrong n_gpus would be worse than none."""
+    env = os.environ.get("WORLD_SIZE")
+    if env is not None:
+        world = int(env)
+        if args.gpus is not None and args.gpus != world:
+            sys.stderr.write(f"bench.py: --gpus {args.gpus} but the launcher started "
+                             f"WORLD_SIZE={world} ranks\n")
+            raise SystemExit(2)
+        return world
+    if args.gpus is None or args.gpus == 1:
+        return 1
+    if args.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {args.gpus}")
+    # No launcher: start the N ranks as a CHILD launcher (never exec from this process) and
+    # exit with its return code.  Nothing here has touched the GPU yet.
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    import subprocess
+    rc = subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    raise SystemExit(rc)
+
+
+def rank_device(torch, dev) -> dict:
+    """This rank's GPU as the driver can check it: PCI address and UUID."""
+    p = torch.cuda.get_device_properties(dev)
+    return {"pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+            "uuid": str(getattr(p, "uuid", "")), "index": dev.index,
+            "name": p.name}
+
+
 def main():
     args = parse()
+    world = resolve_world(args)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs (not used by the driver): SWBENCH_BACKEND=gloo with SWBENCH_SHARE_GPU=1
@@ -309,6 +352,18 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    # What the collective actually saw: its world size and every rank's GPU, gathered to rank 0
+    devices = [rank_device(torch, dev)]
+    dist_info = {"world_size": 1, "backend": None}
+    if world > 1:
+        devices = [None] * world
+        dist.all_gather_object(devices, rank_device(torch, dev))
+        dist_info = {"world_size": dist.get_world_size(), "backend": dist.get_backend()}
+        if dist_info["world_size"] != world:
+            raise SystemExit(f"bench.py: process group has {dist_info['world_size']} ranks, "
+                             f"expected {world}")
+    dist_info["devices"] = devices
+    dist_info["distinct_gpus"] = len({d["pci"] + d["uuid"] for d in devices})
 
     import swbank as S
 
@@ -428,6 +483,7 @@ def main():
             "parallelism": f"dp{world}: pairs sharded, RCCL gather of scores to rank 0",
         },
         "kernel": kernel,
+        "dist": dist_info,
         **({"emulated_ingest_mb": args.emulate_ingest} if args.emulate_ingest > 0 else {}),
         "kernel_ms": {"pack": round(pack_s * 1e3, 4), "score": round(score_s * 1e3, 4)},
         "roofline": {

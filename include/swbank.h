@@ -58,8 +58,11 @@ extern "C" {
  * ABI 5: SW_ERR_TIMEOUT and sw_bank_sync (device-side hand-off waits that run out fail the call,
  *        ≙ the CAPI host failing on the AFU's error bits, main_test.c:64-100); sw_bank_counters
  *        is the two-argument ABI-3 form again, sw_bank_counters_ex takes the struct size;
- *        multi-device device calls copy each device's share into its own HBM. */
-#define SWBANK_ABI_VERSION 5
+ *        multi-device device calls copy each device's share into its own HBM.
+ * ABI 6: sw_counters.wave_balanced_timeouts; sw_score_batch_device_multi (each device scores
+ *        a batch already resident in its own HBM, only the int32 scores cross xGMI); every entry
+ *        point leaves the caller's current HIP device as it found it. */
+#define SWBANK_ABI_VERSION 6
 
 typedef int32_t sw_status;
 enum {
@@ -183,6 +186,33 @@ sw_status sw_score_batch_device_range(sw_bank *bank, const uint8_t *d_residues,
                                       const uint64_t *d_ids, size_t n, uint32_t min_len,
                                       uint32_t max_len, int32_t *d_scores, void *stream);
 
+/* ABI 6: one batch per device, each ALREADY RESIDENT in that device's HBM (≙ every
+ * ScoringModule's feeder latching its own targets before scoring them, ScoreBank_v2.v:117-137,
+ * SM_Feeder3.v:104-182; BASELINE north_star: "RCCL over xGMI only to gather the final score
+ * vector").  batches[d] belongs to the bank's d-th device (sw_bank_devices order; a single-device
+ * bank takes one): its buffers and stream (NULL = that device's bank stream) are on that device,
+ * and it is scored there against the loaded query (or query set) like
+ * sw_score_batch_device_range -- no target byte crosses xGMI.  Its int32 scores go to
+ * batches[d].d_scores (on device d, may be NULL; nq x n query-major for a query set) and/or are
+ * gathered to the root device (devices[0]) into d_gathered (may be NULL if every d_scores is
+ * given): query-major over the concatenated batch, N = sum of the n, query i, device d, target k at
+ * d_gathered[i * N + (n_0 + ... + n_{d-1}) + k], written on `stream` (a root-device stream,
+ * NULL = the bank's).  Distinct devices gather with one ncclGather (RCCL over xGMI: nq x max n
+ * int32 per device), a device listed twice with peer copies.  Asynchronous: each device's work
+ * follows its stream, `stream` follows every device's work.  No best hit is tracked (d_ids are
+ * not taken); sw_bank_sync waits for it and returns a latched hand-off fault. */
+typedef struct sw_device_batch {
+  const uint8_t *d_residues;  /* codes on this device                                      */
+  const uint64_t *d_offsets;
+  const uint32_t *d_lens;
+  size_t n;                   /* targets (0: the device scores nothing, still joins the gather) */
+  uint32_t min_len, max_len;  /* every d_lens[k] in [min_len, max_len]                     */
+  int32_t *d_scores;          /* this device's scores, or NULL                             */
+  void *stream;               /* a hipStream_t of this device, or NULL                     */
+} sw_device_batch;
+sw_status sw_score_batch_device_multi(sw_bank *bank, const sw_device_batch *batches,
+                                      size_t n_batches, int32_t *d_gathered, void *stream);
+
 /* Best hit of the last batch call (≙ the bank's max / vld_max outputs, ScoreBank_v2.v:42-43):
  * the lowest input index with the maximum score, its id (ids[index], the record's ID for
  * sw_score_records, else the index) and score.  Waits for a device call's stream.
@@ -255,11 +285,14 @@ typedef struct sw_counters {
    * hand-offs because one did (counted when a synchronising call observed them) */
   uint64_t tail_timeouts;
   uint64_t handoff_reruns;
+  /* ABI 6: hand-off waits of the protein wave kernel's balanced ranges that ran out (the
+   * tile kernel's are balanced_timeouts); each kind of time-out in a call is counted once */
+  uint64_t wave_balanced_timeouts;
 } sw_counters;
 /* The first 8 counters (the ABI-3 struct, 64 bytes): safe for a caller of any ABI. */
 sw_status sw_bank_counters(const sw_bank *bank, sw_counters *out);
-/* out_size = sizeof(sw_counters) as the caller compiled it: 64 (ABI 3), 80 (ABI 4) or 96
- * (ABI 5); any other size is SW_ERR_ARG.  No HIP call: the counts are host-side. */
+/* out_size = sizeof(sw_counters) as the caller compiled it: 64 (ABI 3), 80 (ABI 4), 96 (ABI 5)
+ * or 104 (ABI 6); any other size is SW_ERR_ARG.  No HIP call: the counts are host-side. */
 sw_status sw_bank_counters_ex(const sw_bank *bank, sw_counters *out, size_t out_size);
 
 /* Device-side failure reporting (≙ the CAPI host decoding the AFU's error bits and failing the

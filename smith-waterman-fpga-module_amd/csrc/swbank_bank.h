@@ -468,6 +468,11 @@ struct sw_bank {
   DevBuf<uint64_t> offs;
   DevBuf<uint32_t> lens;
   DevBuf<int32_t> scores;
+  // the sorted copy of SWBANK_RAGGED_GATHER (launch): its own buffers, never the batch it
+  // copies from (a multi-device child's batch IS res / offs / lens: ADVICE r5)
+  DevBuf<uint8_t> gres;
+  DevBuf<uint64_t> goffs;
+  DevBuf<uint32_t> glens;
 
   char last_kernel[160] = {0};
 
@@ -540,6 +545,24 @@ struct sw_bank {
   std::vector<Ev> events;
 };
 
+// Every C-ABI entry point works on its bank's device and hands the calling thread back on the
+// device it was on (a one-thread caller holding several banks, or torch beside a
+// bank, got its next allocation on the wrong GPU after a library call).
+struct DevGuard {
+  int prev = -1;
+  DevGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  explicit DevGuard(const sw_bank* b) : DevGuard() {
+    if (b && b->device >= 0) (void)hipSetDevice(b->device);
+  }
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DevGuard(const DevGuard&) = delete;
+  DevGuard& operator=(const DevGuard&) = delete;
+};
+
 // Scores in the f16 kernels are f16 multiples of 2^-11 (x as x/2048, swbank_kcommon.h), so
 // the packed add's [0, 1] clamp is max(0, x); -2048 (padding rows / letters) is 0xBC00.
 inline uint16_t f16_score_bits(int v) {
@@ -568,6 +591,8 @@ struct Rccl {
   decltype(&ncclGetErrorString) errorString = nullptr;
   decltype(&ncclCommAbort) commAbort = nullptr;
   decltype(&ncclCommGetAsyncError) asyncError = nullptr;
+  decltype(&ncclGroupStart) groupStart = nullptr;  // one thread issuing every device's gather
+  decltype(&ncclGroupEnd) groupEnd = nullptr;
 };
 const Rccl& rccl();
 
@@ -666,6 +691,10 @@ sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_t* scor
 sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                        const uint32_t* d_lens, const uint64_t* d_ids, size_t n, uint32_t min_len,
                        uint32_t max_len, int32_t* d_scores, hipStream_t hs, bool records);
+// One batch per device, resident in that device's HBM (ABI 6, sw_score_batch_device_multi):
+// scored in place, only the int32 scores gathered to the root into d_gathered (may be null).
+sw_status multi_resident(sw_bank* b, const sw_device_batch* per, int32_t* d_gathered,
+                         hipStream_t hs);
 // ---- swbank_launch.hip (device batches against a query set; sstride: between query rows)
 sw_status launch_set(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                      const uint32_t* d_lens, size_t n, uint32_t min_len, uint32_t max_len,

@@ -36,6 +36,7 @@ static sw_status check_device(int dev) {
 
 
 extern "C" sw_status sw_bank_create(sw_bank** out, const sw_config* cfg_in) {
+  DevGuard dev_guard;  // the caller's current device is restored on return (ABI 6)
   if (!out) return SW_ERR_ARG;
   *out = nullptr;
   sw_config cfg;
@@ -140,6 +141,7 @@ extern "C" sw_status sw_bank_create(sw_bank** out, const sw_config* cfg_in) {
 }
 
 extern "C" void sw_bank_destroy(sw_bank* b) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b) return;
   if (b->is_multi() || !b->comms.empty()) {
     const Rccl& r = rccl();
@@ -235,6 +237,9 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   b->offs.release();
   b->lens.release();
   b->scores.release();
+  b->gres.release();
+  b->goffs.release();
+  b->glens.release();
   if (b->stream) (void)hipStreamDestroy(b->stream);
   delete b;
 }
@@ -269,19 +274,31 @@ sw_status take_fault(sw_bank* b, int which) {
     return st;
   }
   if (!b->faultw.p) return SW_OK;
-  volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(b->faultw.p) + which;
-  const uint32_t f = *w;
+  // the call kind's group: one word per fault kind (SWK_FAULT_WORDS, swbank_internal.h)
+  volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(b->faultw.p) + which * SWK_FAULT_WORDS;
+  uint32_t f = 0;
+  for (int i = 0; i < SWK_FAULT_WORDS; ++i) {
+    f |= w[i];
+    w[i] = 0;
+  }
   if (f == 0) return SW_OK;
-  *w = 0;
   if (f & SWK_FAULT_BAL) ++b->ctr.balanced_timeouts;
   if (f & SWK_FAULT_TAIL) ++b->ctr.tail_timeouts;
+  if (f & SWK_FAULT_WBAL) ++b->ctr.wave_balanced_timeouts;
+  char kinds[96] = "";
+  const char* names[3] = {"balanced ranges", "protein tail", "wave balanced ranges"};
+  for (int i = 0; i < 3; ++i)
+    if (f & (1u << i)) {
+      if (kinds[0]) strncat(kinds, ", ", sizeof(kinds) - strlen(kinds) - 1);
+      strncat(kinds, names[i], sizeof(kinds) - strlen(kinds) - 1);
+    }
   return fail(b, SW_ERR_TIMEOUT,
-              "a cross-workgroup hand-off wait ran out (%s%s) in a %s call: its scores are invalid",
-              f & SWK_FAULT_BAL ? "balanced ranges " : "", f & SWK_FAULT_TAIL ? "protein tail" : "",
-              which ? "host-buffer" : "device");
+              "a cross-workgroup hand-off wait ran out (%s) in a %s call: its scores are invalid",
+              kinds, which ? "host-buffer" : "device");
 }
 
 extern "C" sw_status sw_bank_sync(sw_bank* b) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b) return SW_ERR_ARG;
   if (b->is_multi()) {
     for (sw_bank* k : b->kids) {
@@ -325,14 +342,15 @@ static void sum_counters(sw_counters& c, const sw_bank* b) {
   c.balanced_timeouts += b->ctr.balanced_timeouts;
   c.tail_timeouts += b->ctr.tail_timeouts;
   c.handoff_reruns += b->ctr.handoff_reruns;
+  c.wave_balanced_timeouts += b->ctr.wave_balanced_timeouts;
 }
 
 // Host-side counts only (no HIP call): a hand-off time-out is counted when a synchronising call
 // takes it from the fault word.
 extern "C" sw_status sw_bank_counters_ex(const sw_bank* b, sw_counters* out, size_t out_size) {
   if (!b || !out) return SW_ERR_ARG;
-  // the struct sizes of ABI 3 (8 counters), ABI 4 (10) and ABI 5 (12)
-  if (out_size != 64 && out_size != 80 && out_size != sizeof(sw_counters))
+  // the struct sizes of ABI 3 (8 counters), ABI 4 (10), ABI 5 (12) and ABI 6 (13)
+  if (out_size != 64 && out_size != 80 && out_size != 96 && out_size != sizeof(sw_counters))
     return SW_ERR_ARG;
   sw_counters c{};
   sum_counters(c, b);
@@ -368,6 +386,7 @@ static sw_status set_matrix_impl(sw_bank* b, const int8_t* m, int alpha, int32_t
 
 extern "C" sw_status sw_set_penalties(sw_bank* b, int32_t match, int32_t mismatch,
                                       int32_t gap_open, int32_t gap_extend) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b) return SW_ERR_ARG;
   if (b->is_multi())
     return each_kid(b, [&](sw_bank* k) {
@@ -383,6 +402,7 @@ extern "C" sw_status sw_set_penalties(sw_bank* b, int32_t match, int32_t mismatc
 
 extern "C" sw_status sw_set_matrix(sw_bank* b, const int8_t* m, int32_t alpha, int32_t gap_open,
                                    int32_t gap_extend) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b || !m) return SW_ERR_ARG;
   if (b->is_multi())
     return each_kid(b, [&](sw_bank* k) { return sw_set_matrix(k, m, alpha, gap_open, gap_extend); });
@@ -392,6 +412,7 @@ extern "C" sw_status sw_set_matrix(sw_bank* b, const int8_t* m, int32_t alpha, i
 }
 
 extern "C" sw_status sw_load_query(sw_bank* b, uint64_t id, const uint8_t* codes, uint32_t len) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b || (!codes && len)) return SW_ERR_ARG;
   if (b->is_multi()) {  // the query goes to every device (ScoreBank_v2.v:101-102)
     const sw_status st = each_kid(b, [&](sw_bank* k) { return sw_load_query(k, id, codes, len); });
@@ -418,6 +439,7 @@ extern "C" sw_status sw_load_query(sw_bank* b, uint64_t id, const uint8_t* codes
 extern "C" sw_status sw_load_queries(sw_bank* b, size_t nq, const uint64_t* ids,
                                      const uint8_t* codes, const uint64_t* offsets,
                                      const uint32_t* lens) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b || nq == 0 || !offsets || !lens) return SW_ERR_ARG;
   if (b->is_multi()) {  // the set goes to every device (ScoreBank_v2.v:101-102)
     const sw_status st = each_kid(
@@ -912,6 +934,7 @@ sw_status prepare_i32(sw_bank* b) {
 }
 
 extern "C" sw_status sw_bank_set_timing(sw_bank* b, int32_t enable) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b) return SW_ERR_ARG;
   if (b->is_multi()) return each_kid(b, [&](sw_bank* k) { return sw_bank_set_timing(k, enable); });
   b->timing = enable != 0;
@@ -920,6 +943,7 @@ extern "C" sw_status sw_bank_set_timing(sw_bank* b, int32_t enable) {
 
 extern "C" sw_status sw_bank_timing(sw_bank* b, uint64_t* launches, double* pack_ms,
                                     double* score_ms) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b) return SW_ERR_ARG;
   double p = 0, s = 0;
   uint64_t n = 0;
@@ -967,6 +991,7 @@ extern "C" sw_status sw_bank_timing(sw_bank* b, uint64_t* launches, double* pack
 
 extern "C" sw_status sw_best_hit_device(sw_bank* b, const int32_t* d_scores, const uint64_t* d_ids,
                                         size_t n, uint64_t* d_out, void* stream) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b) return SW_ERR_ARG;
   if (b->is_multi())  // on the root device, where the multi-device calls leave the scores
     return sw_best_hit_device(b->kids[0], d_scores, d_ids, n, d_out,
@@ -982,6 +1007,7 @@ extern "C" sw_status sw_best_hit_device(sw_bank* b, const int32_t* d_scores, con
 
 extern "C" sw_status sw_best_hit(sw_bank* b, const int32_t* scores, const uint64_t* ids, size_t n,
                                  uint64_t* best_id, int32_t* best_score) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!scores || !best_id || !best_score || n == 0)
     return b ? fail(b, SW_ERR_ARG, "sw_best_hit: empty or null input") : SW_ERR_ARG;
   size_t bi = 0;

@@ -99,6 +99,13 @@ static std::vector<size_t> chunk_bounds(size_t total, size_t min_bytes = 0) {
   size_t sz = fixed ? cap : std::max<size_t>({(size_t)1 << 20, cap / 4, min_bytes});
   for (size_t at = sz; at < total && total - at >= min_bytes; at += sz, sz = std::min(cap, sz * 2))
     bounds.push_back(at);
+  // A remainder below min_bytes stays with the last chunk, which can then pass the cap (up to
+  // cap + min_bytes); such a last chunk is halved when both halves keep min_bytes, so
+  // every chunk stays within max(cap, 2 min_bytes) -- and so do the slots sized to it.
+  if (!bounds.empty()) {
+    const size_t last = total - bounds.back();
+    if (last > cap && last / 2 >= min_bytes) bounds.push_back(bounds.back() + last / 2);
+  }
   return bounds;
 }
 
@@ -855,6 +862,7 @@ static sw_status batch_feed_once(sw_bank* b, const uint8_t* residues, size_t nre
 // ---- CAPI record path (row f2): sequence_t arrays as the reference host builds them ------
 
 extern "C" sw_status sw_load_query_record(sw_bank* b, const void* record) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b || !record) return SW_ERR_ARG;
   if (b->alpha != SW_DNA_ALPHA) return fail(b, SW_ERR_UNSUPPORTED, "records carry DNA only");
   const uint8_t* rec = static_cast<const uint8_t*>(record);
@@ -869,6 +877,7 @@ extern "C" sw_status sw_load_query_record(sw_bank* b, const void* record) {
 
 extern "C" sw_status sw_score_records_device(sw_bank* b, const void* d_records, size_t n,
                                              int32_t* d_scores, void* stream) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (b && b->qset.size() > 1)
     return fail(b, SW_ERR_STATE, "a query set is loaded: score it with sw_score_batch_device");
   if (!b) return SW_ERR_ARG;
@@ -980,6 +989,7 @@ static sw_status records_feed_once(sw_bank* b, const uint8_t* recs, size_t n, in
 extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, size_t residues_len,
                                     const uint64_t* offsets, const uint32_t* lens,
                                     const uint64_t* ids, size_t n, int32_t* scores_out) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (b && b->qset.size() > 1)
     return fail(b, SW_ERR_STATE, "a query set is loaded: score it with sw_score_batch_device");
   if (!b) return SW_ERR_ARG;
@@ -1005,6 +1015,7 @@ extern "C" sw_status sw_score_batch(sw_bank* b, const uint8_t* residues, size_t 
 
 extern "C" sw_status sw_score_records(sw_bank* b, const void* records, size_t n,
                                       int32_t* scores_out) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (b && b->qset.size() > 1)
     return fail(b, SW_ERR_STATE, "a query set is loaded: score it with sw_score_batch_device");
   if (!b) return SW_ERR_ARG;

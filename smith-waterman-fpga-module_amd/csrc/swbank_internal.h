@@ -58,10 +58,14 @@ typedef struct SwkWaveSplit {
   unsigned* wbal_state;
 } SwkWaveSplit;
 
-/* Bits of a launch's fault word (cross-workgroup hand-off waits that ran out). */
+/* Kinds of a launch's fault marks (cross-workgroup hand-off waits that ran out).  Each kind has
+ * its own word in the call's group of SWK_FAULT_WORDS words (word ctz(bit) holds bit), so a call
+ * whose launches run out in two kinds keeps both (a plain store per kind, no read-modify-write
+ * on host memory); a bank has one group for device calls and one for host-buffer calls. */
 #define SWK_FAULT_BAL 1u
 #define SWK_FAULT_TAIL 2u
 #define SWK_FAULT_WBAL 4u
+#define SWK_FAULT_WORDS 4
 
 /* One chunk of a streamed host batch (uploaded before the launch): its first tile and the
  * offset of its codes in the device batch buffer.  Its code layout travels in a flag word per

@@ -797,10 +797,12 @@ struct ScoreArgs {
 };
 static_assert(sizeof(ScoreArgs) == 376, "ScoreArgs layout (kernel argument block) changed");
 
-// a hand-off wait ran out: mark the launch's fault word (a vector store to host memory; only the
-// host reads it, after the launch completed)
+// a hand-off wait ran out: mark the kind's word of the call's fault group (a vector store to
+// host memory, one word per kind so two kinds in one call are both kept; only the host reads
+// it, after the launch completed)
 __device__ __forceinline__ void report_fault(uint32_t* fault, uint32_t bit) {
-  if (fault) __hip_atomic_store(fault, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (fault) __hip_atomic_store(fault + __builtin_ctz(bit), bit, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;

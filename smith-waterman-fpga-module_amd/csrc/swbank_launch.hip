@@ -191,7 +191,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
         sp.wbal_gen = ++b->wbal_gen;
         sp.wbal_flag = b->wbal_flag.p;
         sp.wbal_state = b->wbal_state.p;
-        sp.fault = fw + (b->host_call ? 1 : 0);
+        sp.fault = fw + (b->host_call ? SWK_FAULT_WORDS : 0);
         sp.poll_limit = poll_limit(1u << 23);
         sp.stall = (unsigned)std::max(0, env_int("SWBANK_STALL", 0));
         wbal = true;
@@ -228,7 +228,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
         sp.ring = b->sring.p;
         sp.cols = ecols;
         sp.prog = b->tprog.p;
-        sp.fault = fw + (b->host_call ? 1 : 0);
+        sp.fault = fw + (b->host_call ? SWK_FAULT_WORDS : 0);
         sp.poll_limit = poll_limit(1u << 24);
         sp.stall = (unsigned)std::max(0, env_int("SWBANK_STALL", 0));
         const size_t L = strlen(b->last_kernel);
@@ -415,26 +415,26 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
           if (gat) {
             const size_t stride = ((gnib ? ((size_t)max_len + 7) / 8 * 4 : (size_t)max_len) + 15) &
                                   ~(size_t)15;
-            HIPOK(b, b->res.reserve(n * stride + 16));
-            HIPOK(b, b->offs.reserve(n));
-            HIPOK(b, b->lens.reserve(n));
+            HIPOK(b, b->gres.reserve(n * stride + 16));
+            HIPOK(b, b->goffs.reserve(n));
+            HIPOK(b, b->glens.reserve(n));
             dl.D = 1;
             dl.stride = (unsigned)stride;
-            dl.codes[0] = b->res.p;
-            dl.offs[0] = reinterpret_cast<unsigned long long*>(b->offs.p);
-            dl.lens[0] = b->lens.p;
+            dl.codes[0] = b->gres.p;
+            dl.offs[0] = reinterpret_cast<unsigned long long*>(b->goffs.p);
+            dl.lens[0] = b->glens.p;
             dl.cnt[0] = n;
             dl.nib = gnib ? 1u : 0u;
             HIPOK(b, swk_deal_gather(res, offs, lens, idx, ident, n, &dl, st));
           }
-          HIPOK(b, swk_launch_pair_bal(gat ? b->res.p : res, gat ? b->offs.p : offs,
-                                       gat ? b->lens.p : lens, np, b->qpair.p, b->nv16, b->S, b->O,
+          HIPOK(b, swk_launch_pair_bal(gat ? b->gres.p : res, gat ? b->goffs.p : offs,
+                                       gat ? b->glens.p : lens, np, b->qpair.p, b->nv16, b->S, b->O,
                                        b->E, b->pair_bytes, b->pad, Wl,
                                        scores, b->pS1, b->pS2, ulen,
                                        ustride, b->bal_flag.p, b->bal_state.p, ++b->bal_gen, grid,
                                        gat ? nullptr : idx, gat ? nullptr : nidx,
                                        ident, b->bal_plan.p,
-                                       fw + (b->host_call ? 1 : 0), poll_limit(1u << 23),
+                                       fw + (b->host_call ? SWK_FAULT_WORDS : 0), poll_limit(1u << 23),
                                        (uint32_t)std::max(0, env_int("SWBANK_STALL", 0)),
                                        rbal && ragged_trim(),
                                        gnib ? (uint32_t)SWK_PACK_NIBBLE : (uint32_t)SWK_PACK_BYTES,
@@ -638,6 +638,7 @@ extern "C" sw_status sw_score_batch_device(sw_bank* b, const uint8_t* d_res,
                                            const uint64_t* d_offs, const uint32_t* d_lens,
                                            const uint64_t* d_ids, size_t n, uint32_t max_len,
                                            int32_t* d_scores, void* stream) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   return sw_score_batch_device_range(b, d_res, d_offs, d_lens, d_ids, n, 0, max_len, d_scores,
                                      stream);
 }
@@ -647,6 +648,7 @@ extern "C" sw_status sw_score_batch_device_range(sw_bank* b, const uint8_t* d_re
                                                  const uint64_t* d_ids, size_t n,
                                                  uint32_t min_len, uint32_t max_len,
                                                  int32_t* d_scores, void* stream) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b) return SW_ERR_ARG;
   if (min_len > max_len) return fail(b, SW_ERR_ARG, "min_len %u > max_len %u", min_len, max_len);
   b->best_kind = 0;
@@ -676,6 +678,7 @@ extern "C" sw_status sw_score_batch_device_range(sw_bank* b, const uint8_t* d_re
 
 extern "C" sw_status sw_batch_best(sw_bank* b, uint64_t* best_id, int32_t* best_score,
                                    uint64_t* best_index) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
   if (!b) return SW_ERR_ARG;
   if (b->is_multi() && b->best_root) {
     // the root tracked it after the scatter, which waited for every device's work: once it is

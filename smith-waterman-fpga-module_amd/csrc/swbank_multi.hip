@@ -24,8 +24,10 @@ const Rccl& rccl() {
     r.commAbort = reinterpret_cast<decltype(&ncclCommAbort)>(dlsym(h, "ncclCommAbort"));
     r.asyncError =
         reinterpret_cast<decltype(&ncclCommGetAsyncError)>(dlsym(h, "ncclCommGetAsyncError"));
+    r.groupStart = reinterpret_cast<decltype(&ncclGroupStart)>(dlsym(h, "ncclGroupStart"));
+    r.groupEnd = reinterpret_cast<decltype(&ncclGroupEnd)>(dlsym(h, "ncclGroupEnd"));
     r.ok = r.commInitAll && r.commDestroy && r.gather && r.errorString && r.commAbort &&
-           r.asyncError;
+           r.asyncError && r.groupStart && r.groupEnd;
     if (!r.ok)
       snprintf(r.err, sizeof(r.err),
                "librccl.so.1 lacks ncclCommInitAll/ncclGather/ncclCommAbort/ncclCommGetAsyncError");
@@ -44,6 +46,12 @@ template <class FeedF>
 static sw_status multi_gather(sw_bank* b, const std::vector<size_t>& cnt, FeedF feed_kid) {
   const size_t D = b->kids.size();
   const size_t cmax = *std::max_element(cnt.begin(), cnt.end());
+  // A device call before this one (multi_device, asynchronous) may still read grecv (its
+  // scatter) or a child's scores (its copy-out): its ev_used follows both.
+  if (b->ev_used) {
+    HIPOK(b, hipSetDevice(b->device));
+    HIPOK(b, hipEventSynchronize(b->ev_used));
+  }
   for (size_t d = 0; d < D; ++d) {  // padded send buffers, sized before any score lands
     sw_bank* k = b->kids[d];
     HIPOK(b, hipSetDevice(k->device));
@@ -391,9 +399,10 @@ sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
         break;
       st = launch(k, k->res.p, nullptr, nullptr, c, SWB_RECORD_MAX, k->scores.p, ks,
                   SWK_PACK_RECORDS);
-      if (st == SW_OK)
-        (void)hip(hipMemcpyPeerAsync(d_scores + lo[d], root->device, k->scores.p, k->device,
-                                     c * 4, ks), "scores out");
+      if (st == SW_OK &&
+          hip(hipMemcpyPeerAsync(d_scores + lo[d], root->device, k->scores.p, k->device, c * 4,
+                                 ks), "scores out"))
+        (void)hip(hipEventRecord(k->ev_used, ks), "event");  // the copy-out read k->scores
     } else {
       if (!hip(hipMemcpyPeerAsync(k->res.p, k->device, dl.codes[d], root->device, c * stride, ks),
                "codes in") ||
@@ -407,9 +416,10 @@ sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                : launch(k, k->res.p, k->offs.p, k->lens.p, c, max_len, k->scores.p, ks,
                         SWK_PACK_BYTES, nullptr, nullptr, true, true, nullptr, nullptr, 0, 0,
                         min_len);
-      if (st == SW_OK)
-        (void)hip(hipMemcpyPeerAsync(const_cast<int*>(dl.scores[d]), root->device, k->scores.p,
-                                     k->device, c * nq * 4, ks), "scores out");
+      if (st == SW_OK &&
+          hip(hipMemcpyPeerAsync(const_cast<int*>(dl.scores[d]), root->device, k->scores.p,
+                                 k->device, c * nq * 4, ks), "scores out"))
+        (void)hip(hipEventRecord(k->ev_used, ks), "event");  // the copy-out read k->scores
     }
   }
   // (recorded even after a failure: the caller's stream must not run ahead of what was enqueued)
@@ -438,6 +448,176 @@ sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
     if ((st = track_best_device(root, d_scores, d_ids, n, hs)) != SW_OK)
       return fail(b, st, "device %d: %s", root->device, root->err);
     b->best_root = true;
+  }
+  return SW_OK;
+}
+
+// ABI 6: every device scores a batch that already lives in its own HBM (≙ each ScoringModule's
+// feeder latching its own targets, ScoreBank_v2.v:117-137, SM_Feeder3.v:104-182): no target byte
+// crosses xGMI, only the int32 scores -- north_star's "RCCL over xGMI only to gather the final
+// score vector".  Device d scores batches[d] on its stream into its padded send buffer (nq rows of
+// cmax = max_d n_d words), copies them to batches[d].d_scores when given, and the send buffers are
+// gathered to the root: one ncclGather (grouped, issued from this thread) into grecv when the
+// devices are distinct, then one 2-D copy per device into d_gathered on the caller's stream
+// (query-major over the concatenated batch, N = sum n_d: query i, device d, target k at
+// d_gathered[i * N + off_d + k]); a device listed twice copies its rows with hipMemcpyPeerAsync.
+// Asynchronous: each device's work is ordered after the previous call's readers of the shared
+// buffers (ev_used) and the caller's stream after every device's work.
+sw_status multi_resident(sw_bank* b, const sw_device_batch* per, int32_t* d_gathered,
+                         hipStream_t hs) {
+  const size_t D = b->kids.size();
+  sw_bank* root = b->kids[0];
+  const bool set = b->qset.size() > 1;
+  const size_t nq = set ? b->qset.size() : 1;
+  size_t N = 0, cmax = 1;
+  std::vector<size_t> off(D);
+  for (size_t d = 0; d < D; ++d) {
+    off[d] = N;
+    N += per[d].n;
+    cmax = std::max(cmax, per[d].n);
+  }
+  HIPOK(b, hipSetDevice(root->device));
+  if (!hs) hs = root->stream;
+  if (!b->ev_join) HIPOK(b, hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
+  const bool first = !b->ev_used;
+  if (first) HIPOK(b, hipEventCreateWithFlags(&b->ev_used, hipEventDisableTiming));
+  const bool use_rccl = d_gathered && !b->comms.empty();
+  if (use_rccl) HIPOK(b, b->grecv.reserve(D * nq * cmax));
+  // 1. every device scores its own batch (its own length sort and balanced ranges included)
+  std::vector<hipStream_t> ks(D, nullptr);
+  sw_status st = SW_OK;
+  for (sw_bank* k : b->kids) k->err[0] = 0;
+  for (size_t d = 0; d < D && st == SW_OK; ++d) {
+    sw_bank* k = b->kids[d];
+    const sw_device_batch& bt = per[d];
+    if ((st = prepare(k)) != SW_OK) break;
+    const auto hip = [&](hipError_t e, const char* what) {
+      if (e != hipSuccess && st == SW_OK)
+        st = fail(k, SW_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+      return st == SW_OK;
+    };
+    if (!hip(hipSetDevice(k->device), "hipSetDevice")) break;
+    ks[d] = bt.stream ? reinterpret_cast<hipStream_t>(bt.stream) : k->stream;
+    if (!k->ev_join && !hip(hipEventCreateWithFlags(&k->ev_join, hipEventDisableTiming), "event"))
+      break;
+    // the previous device call's gather / scatter read this device's send buffer and grecv
+    if (!first && !hip(hipStreamWaitEvent(ks[d], b->ev_used, 0), "stream wait")) break;
+    if (!hip(k->scores.reserve(nq * cmax), "device buffer")) break;
+    if (bt.n) {
+      st = set ? launch_set(k, bt.d_residues, bt.d_offsets, bt.d_lens, bt.n, bt.min_len,
+                            bt.max_len, k->scores.p, ks[d], cmax)
+               : launch(k, bt.d_residues, bt.d_offsets, bt.d_lens, bt.n, bt.max_len, k->scores.p,
+                        ks[d], SWK_PACK_BYTES, nullptr, nullptr, true, true, nullptr, nullptr, 0,
+                        0, bt.min_len);
+      if (st == SW_OK && bt.d_scores)
+        (void)hip(hipMemcpy2DAsync(bt.d_scores, bt.n * 4, k->scores.p, cmax * 4, bt.n * 4, nq,
+                                   hipMemcpyDeviceToDevice, ks[d]),
+                  "scores to the device's own buffer");
+    }
+  }
+  // 2. the gather of the int32 scores to the root
+  const Rccl& r = rccl();
+  if (st == SW_OK && use_rccl) {
+    ncclResult_t e = r.groupStart();
+    for (size_t d = 0; d < D && e == ncclSuccess; ++d)
+      e = r.gather(b->kids[d]->scores.p, d == 0 ? b->grecv.p : nullptr, nq * cmax, ncclInt32, 0,
+                   static_cast<ncclComm_t>(b->comms[d]), ks[d]);
+    const ncclResult_t e2 = r.groupEnd();
+    if (e == ncclSuccess) e = e2;
+    if (e != ncclSuccess) {  // the communicators are re-created by the next host call
+      for (size_t d = 0; d < D; ++d) {
+        (void)hipSetDevice(b->kids[d]->device);
+        (void)r.commAbort(static_cast<ncclComm_t>(b->comms[d]));
+      }
+      b->comms.clear();
+      st = fail(b, SW_ERR_HIP, "ncclGather of the resident scores: %s", r.errorString(e));
+    }
+  } else if (st == SW_OK && d_gathered) {
+    for (size_t d = 0; d < D && st == SW_OK; ++d) {
+      sw_bank* k = b->kids[d];
+      if (!per[d].n) continue;
+      HIPOK(b, hipSetDevice(k->device));
+      for (size_t i = 0; i < nq; ++i)
+        HIPOK(b, hipMemcpyPeerAsync(d_gathered + i * N + off[d], root->device,
+                                    k->scores.p + i * cmax, k->device, per[d].n * 4, ks[d]));
+    }
+  }
+  // 3. the caller's stream after every device's work (recorded even after a failure: the
+  //    caller's stream must not run ahead of what was enqueued)
+  for (size_t d = 0; d < D; ++d) {
+    sw_bank* k = b->kids[d];
+    if (!ks[d]) continue;  // (set once the device's work could be enqueued)
+    (void)hipSetDevice(k->device);
+    (void)hipEventRecord(k->ev_used, ks[d]);  // the send buffer's readers are done after it
+    if (hipEventRecord(k->ev_join, ks[d]) == hipSuccess) {
+      (void)hipSetDevice(root->device);
+      HIPOK(b, hipStreamWaitEvent(hs, k->ev_join, 0));
+    }
+  }
+  HIPOK(b, hipSetDevice(root->device));
+  if (st == SW_OK && use_rccl)
+    for (size_t d = 0; d < D; ++d)
+      if (per[d].n)
+        HIPOK(b, hipMemcpy2DAsync(d_gathered + off[d], N * 4, b->grecv.p + d * nq * cmax,
+                                  cmax * 4, per[d].n * 4, nq, hipMemcpyDeviceToDevice, hs));
+  HIPOK(b, hipEventRecord(b->ev_used, hs));
+  if (st != SW_OK) {
+    if (!b->err[0])
+      for (sw_bank* k : b->kids)
+        if (k->err[0]) return fail(b, st, "device %d: %s", k->device, k->err);
+    return st;
+  }
+  snprintf(b->last_kernel, sizeof(b->last_kernel), "multi[%zu] resident gather=%s: %s", D,
+           !d_gathered ? "none" : use_rccl ? "rccl" : "copy", root->last_kernel);
+  return SW_OK;
+}
+
+extern "C" sw_status sw_score_batch_device_multi(sw_bank* b, const sw_device_batch* batches,
+                                                 size_t n_batches, int32_t* d_gathered,
+                                                 void* stream) {
+  DevGuard dev_guard(b);  // on the bank's device; the caller's is restored on return (ABI 6)
+  if (!b || !batches) return SW_ERR_ARG;
+  const size_t D = b->is_multi() ? b->kids.size() : 1;
+  if (n_batches != D)
+    return fail(b, SW_ERR_ARG, "%zu device batches for a bank of %zu devices", n_batches, D);
+  b->err[0] = 0;
+  b->best_kind = 0;
+  b->best_root = false;
+  if (const sw_status fs = take_fault(b, 0); fs != SW_OK) return fs;
+  size_t N = 0;
+  for (size_t d = 0; d < D; ++d) {
+    const sw_device_batch& bt = batches[d];
+    if (bt.min_len > bt.max_len)
+      return fail(b, SW_ERR_ARG, "device batch %zu: min_len %u > max_len %u", d, bt.min_len,
+                  bt.max_len);
+    if (bt.n > 0xFFFFFFFFull) return fail(b, SW_ERR_RANGE, "device batch %zu: n >= 2^32", d);
+    if (bt.n && (!bt.d_residues || !bt.d_offsets || !bt.d_lens))
+      return fail(b, SW_ERR_ARG, "device batch %zu: null device buffer", d);
+    if (bt.n && !bt.d_scores && !d_gathered)
+      return fail(b, SW_ERR_ARG, "device batch %zu: no d_scores and no d_gathered", d);
+    N += bt.n;
+  }
+  if (N > 0xFFFFFFFFull) return fail(b, SW_ERR_RANGE, "more than 2^32 targets");
+  if (N == 0) return SW_OK;
+  if (b->is_multi()) return multi_resident(b, batches, d_gathered, reinterpret_cast<hipStream_t>(stream));
+  // one device: sw_score_batch_device_range on the one batch, its scores in both places asked for
+  const sw_device_batch& bt = batches[0];
+  hipStream_t hs = stream ? reinterpret_cast<hipStream_t>(stream) : b->stream;
+  hipStream_t bs = bt.stream ? reinterpret_cast<hipStream_t>(bt.stream) : b->stream;
+  int32_t* out = bt.d_scores ? bt.d_scores : d_gathered;
+  sw_status st = sw_score_batch_device_range(b, bt.d_residues, bt.d_offsets, bt.d_lens, nullptr,
+                                             bt.n, bt.min_len, bt.max_len, out, bs);
+  if (st != SW_OK) return st;
+  const size_t nq = b->qset.size() > 1 ? b->qset.size() : 1;
+  if (bt.d_scores && d_gathered) {
+    if (!b->ev_join) HIPOK(b, hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
+    HIPOK(b, hipEventRecord(b->ev_join, bs));
+    HIPOK(b, hipStreamWaitEvent(hs, b->ev_join, 0));
+    HIPOK(b, hipMemcpyAsync(d_gathered, bt.d_scores, nq * bt.n * 4, hipMemcpyDeviceToDevice, hs));
+  } else if (hs != bs) {
+    if (!b->ev_join) HIPOK(b, hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming));
+    HIPOK(b, hipEventRecord(b->ev_join, bs));
+    HIPOK(b, hipStreamWaitEvent(hs, b->ev_join, 0));
   }
   return SW_OK;
 }

@@ -43,12 +43,12 @@ EXPORTS = (
     "sw_last_kernel", "sw_load_query_record", "sw_score_records", "sw_score_records_device",
     "sw_best_hit_device", "sw_batch_best", "sw_bank_devices", "sw_load_queries",
     "sw_query_count", "sw_score_batch_device_range", "sw_bank_counters",
-    "sw_bank_counters_ex", "sw_bank_sync",
+    "sw_bank_counters_ex", "sw_bank_sync", "sw_score_batch_device_multi",
 )
-ABI_VERSION = 5
+ABI_VERSION = 6
 COUNTERS = ("stream_calls", "stream_reruns", "stream_declined", "chunked_calls", "device_sorts",
             "gather_timeouts", "mixed_chunks", "mixed_runs", "balanced_calls",
-            "balanced_timeouts", "tail_timeouts", "handoff_reruns")
+            "balanced_timeouts", "tail_timeouts", "handoff_reruns", "wave_balanced_timeouts")
 MAX_DEVICES = 16
 RECORD_BYTES, RECORD_MAX_BASES = 64, 232
 
@@ -57,6 +57,14 @@ class SwbankError(RuntimeError):
     def __init__(self, status: int, msg: str):
         super().__init__(f"swbank status {status}: {msg}")
         self.status = status
+
+
+class DeviceBatch(ctypes.Structure):
+    """sw_device_batch (ABI 6): one device's resident batch for sw_score_batch_device_multi."""
+    _fields_ = [("d_residues", ctypes.c_void_p), ("d_offsets", ctypes.c_void_p),
+                ("d_lens", ctypes.c_void_p), ("n", ctypes.c_size_t),
+                ("min_len", ctypes.c_uint32), ("max_len", ctypes.c_uint32),
+                ("d_scores", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
 
 
 class _Config(ctypes.Structure):
@@ -124,6 +132,7 @@ def lib() -> ctypes.CDLL:
         "sw_best_hit_device": (i32, [P, P, P, sz, P, P]),
         "sw_load_queries": (i32, [P, sz, P, P, P, P]),
         "sw_query_count": (sz, [P]),
+        "sw_score_batch_device_multi": (i32, [P, P, sz, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -379,6 +388,19 @@ class ScoreBank:
             self._check(lib().sw_score_batch_device_range(self._h, d_res, d_offs, d_lens,
                                                           d_ids or None, n, min_len, max_len,
                                                           d_scores, stream or None))
+
+    def score_batch_device_multi(self, batches, d_gathered: int = 0, stream: int = 0):
+        """sw_score_batch_device_multi (ABI 6): batches[d] = dict(d_res, d_offs, d_lens, n,
+        max_len, min_len=0, d_scores=0, stream=0) resident on the bank's d-th device; each device
+        scores its own batch in place, the int32 scores are gathered to the root into d_gathered
+        (query-major over the concatenated batch) and/or left in each d_scores.  Async."""
+        arr = (DeviceBatch * len(batches))()
+        for i, bt in enumerate(batches):
+            arr[i] = DeviceBatch(bt["d_res"] or None, bt["d_offs"] or None, bt["d_lens"] or None,
+                                 bt["n"], bt.get("min_len", 0), bt["max_len"],
+                                 bt.get("d_scores", 0) or None, bt.get("stream", 0) or None)
+        self._check(lib().sw_score_batch_device_multi(self._h, arr, len(batches),
+                                                      d_gathered or None, stream or None))
 
     def counters(self) -> dict:
         """sw_bank_counters: feeder / fallback counts since the bank was created."""

@@ -166,6 +166,26 @@ static int score(const char *qpath, const char *lpath) {
   CHECK(sw_best_hit(bank, s1, NULL, (size_t)n, &best_id, &best) == SW_OK, "best hit");
   printf("best %s %d\n", ln[best_id], best);
 
+  /* the AFU error-bit check (main_test.c:64-100): nothing latched after good calls */
+  CHECK(sw_bank_sync(bank) == SW_OK, sw_last_error(bank));
+  /* an ABI-3 caller's 8-counter struct through the two-argument call: 64 bytes written, the
+   * word after them untouched */
+  {
+    uint64_t v3[9];
+    memset(v3, 0xA5, sizeof v3);
+    CHECK(sw_bank_counters(bank, (sw_counters *)v3) == SW_OK, "counters (ABI 3 form)");
+    CHECK(v3[8] == 0xA5A5A5A5A5A5A5A5ull, "counters wrote past the ABI-3 struct");
+    CHECK(v3[0] + v3[3] >= 1, "stream_calls + chunked_calls count the host-buffer calls");
+    sw_counters c;
+    memset(&c, 0xFF, sizeof c);
+    CHECK(sw_bank_counters_ex(bank, &c, sizeof c) == SW_OK, "counters_ex");
+    CHECK(c.stream_calls == v3[0] && c.chunked_calls == v3[3] && c.balanced_timeouts == 0 && c.tail_timeouts == 0 &&
+              c.wave_balanced_timeouts == 0 && c.handoff_reruns == 0,
+          "counters_ex = the ABI-3 prefix, no time-outs");
+    CHECK(sw_bank_counters_ex(bank, &c, sizeof c - 4) == SW_ERR_ARG, "odd counter size");
+    printf("counters host_calls=%llu\n", (unsigned long long)(c.stream_calls + c.chunked_calls));
+  }
+
   /* argument errors */
   CHECK(sw_score_batch(bank, res, total, NULL, lens, NULL, (size_t)n, s1) == SW_ERR_ARG, "null offsets");
   /* a target past the residues is refused before anything is read */

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_status_strings():
-    assert S.lib().sw_abi_version() == S.ABI_VERSION == 5
+    assert S.lib().sw_abi_version() == S.ABI_VERSION == 6
     assert "timed out" in S.status_string(S.ERR_TIMEOUT)
     assert S.status_string(0) == "ok"
     assert "gfx950" in S.status_string(S.ERR_NO_DEVICE)

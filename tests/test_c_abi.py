@@ -46,12 +46,13 @@ def test_c_client_scores_golden(client, lib):
     assert r.returncode == 0, r.stderr
     lines = r.stdout.splitlines()
     assert lines[0].startswith("kernel ") and lines[-1] == "score ok"
-    got = dict(ln.split() for ln in lines[1:-2])
+    assert lines[-3].startswith("best ") and lines[-2].startswith("counters host_calls=")
+    got = dict(ln.split() for ln in lines[1:-3])
     want = {t: s for src, lb, q, t, s in O.load_ref_scores()
             if lb == lib and q == "query100.fa" and src == "hdl"}
     assert want and all(int(got[t]) == s for t, s in want.items())
     best = max(want.values())
-    assert lines[-2].startswith("best ") and int(lines[-2].split()[2]) == best
+    assert int(lines[-3].split()[2]) == best
 
 
 @pytest.fixture(scope="module")

@@ -525,3 +525,118 @@ def test_multi_device_deal_soak(seed):
     got = run([0] * D)
     want = run([0])
     assert np.array_equal(got, want), (D, n, maxl, int((got != want).sum()))
+
+
+@pytest.mark.parametrize("devices,gather", [([0, 0], "copy"), ([0, 0, 0], "copy"),
+                                            ([0], "rccl"), (None, None)])
+def test_multi_device_resident_batches(devices, gather, monkeypatch, poisoned_buffers):
+    """ABI 6, sw_score_batch_device_multi: each device's batch already sits in its own HBM (the
+    RTL's modules each latch their own targets, ScoreBank_v2.v:117-137) and is scored in place;
+    only the int32 scores are gathered to the root -- by ncclGather on a real 1-rank
+    communicator for [0] with SWBANK_GATHER=rccl, by peer copies for a device listed twice.
+    Ragged, uniform and empty per-device batches, a query set, the per-device score buffers and
+    the gathered vector: bit-exact against the oracle on every target, twice in a row on
+    different streams (the shared gather buffer's reuse is ordered)."""
+    torch = pytest.importorskip("torch")
+    if gather:
+        monkeypatch.setenv("SWBANK_GATHER", gather)
+    dev = torch.device("cuda", 0)
+    D = len(devices) if devices else 1
+    rng = np.random.default_rng(500 + D)
+    q = _codes(rng, 130)
+    shapes = [(3000, 0, 180), (2049, 90, 90), (0, 0, 1), (777, 1, 300)][:D]
+    if D == 1:
+        shapes = [(4500, 0, 200)]
+    per, want, dev_bufs = [], [], []
+    for n, lo, hi in shapes:
+        seqs = [_codes(rng, int(l)) for l in rng.integers(lo, hi + 1, n)]
+        if n > 10:
+            seqs[n // 3] = q.copy()
+        res, offs, lens = O.pack_residues(seqs) if n else (np.zeros(16, np.uint8),
+                                                           np.zeros(0, np.uint64),
+                                                           np.zeros(0, np.uint32))
+        res = np.concatenate([res, np.zeros(16, np.uint8)])
+        want.append((res, offs, lens))
+        t = [torch.from_numpy(res).to(dev), torch.from_numpy(offs.view(np.int64)).to(dev),
+             torch.from_numpy(lens.view(np.int32)).to(dev)]
+        dev_bufs.append(t)
+        per.append((n, lo, max(hi, 1)))
+    qs = [q, q[:70].copy(), _codes(rng, 260)]
+    N = sum(n for n, _, _ in per)
+
+    def oracle_rows(qq):
+        return np.concatenate([O.score_batch(qq, r, o, l, O.dna_matrix(), -12, -4) if len(l) else
+                               np.zeros(0, np.int32) for r, o, l in want])
+
+    kw = dict(devices=devices) if devices else {}
+    with S.ScoreBank(**kw) as bank:
+        bank.set_penalties(*REF)
+        for rnd, queries in enumerate([[q], qs]):
+            if len(queries) == 1:
+                bank.load_query(queries[0])
+            else:
+                bank.load_queries(queries)
+            nq = len(queries)
+            own = [torch.full((nq, max(n, 1)), -3, dtype=torch.int32, device=dev) for n, _, _ in per]
+            gathered = torch.full((nq, N), -3, dtype=torch.int32, device=dev)
+            st = torch.cuda.Stream()
+            batches = [dict(d_res=b[0].data_ptr(), d_offs=b[1].data_ptr(), d_lens=b[2].data_ptr(),
+                            n=n, min_len=lo, max_len=hi, d_scores=o.data_ptr())
+                       for b, (n, lo, hi), o in zip(dev_bufs, per, own)]
+            bank.score_batch_device_multi(batches, gathered.data_ptr(), st.cuda_stream)
+            st.synchronize()
+            bank.sync()
+            if devices:
+                assert bank.last_kernel().startswith(f"multi[{D}] resident gather={gather}"), \
+                    bank.last_kernel()
+            g = gathered.cpu().numpy()
+            for i, qq in enumerate(queries):
+                ref = oracle_rows(qq)
+                assert np.array_equal(g[i], ref), (rnd, i, int((g[i] != ref).sum()))
+                at = 0
+                for (n, _, _), o in zip(per, own):
+                    assert np.array_equal(o.cpu().numpy()[i][:n], ref[at:at + n])
+                    at += n
+        # gathered only (no per-device buffers), the bank's own streams
+        bank.load_query(q)
+        only = torch.full((N,), -3, dtype=torch.int32, device=dev)
+        bank.score_batch_device_multi([dict(d_res=b[0].data_ptr(), d_offs=b[1].data_ptr(),
+                                            d_lens=b[2].data_ptr(), n=n, min_len=lo, max_len=hi)
+                                       for b, (n, lo, hi) in zip(dev_bufs, per)], only.data_ptr())
+        bank.sync()
+        torch.cuda.synchronize()
+        assert np.array_equal(only.cpu().numpy(), oracle_rows(q))
+        with pytest.raises(S.SwbankError) as e:  # one batch per device, exactly
+            bank.score_batch_device_multi([], only.data_ptr())
+        assert e.value.status == S.ERR_ARG
+
+
+def test_multi_device_ragged_gather_knob(monkeypatch):
+    """with SWBANK_RAGGED_GATHER=1/2 a child's launch copied the batch in its sorted
+    order into the same buffers the multi-device deal had handed it as input (in place, so lanes
+    overwrote targets others had not read).  The sorted copy now has its own buffers: a [0, 0]
+    deal large enough for the children's ragged balanced ranges, bit-exact with the knob."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(77)
+    q = _codes(rng, 128)
+    n = 1_300_000  # each child's share must allow ragged balanced ranges (>= 4,864 tiles)
+    lens = rng.integers(64, 151, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    res = rng.integers(0, 4, int(lens.sum()) + 16, dtype=np.uint8)
+    want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)
+    d = [torch.from_numpy(x).to(dev) for x in (res, offs.view(np.int64), lens.view(np.int32))]
+    for mode in ("1", "2"):
+        monkeypatch.setenv("SWBANK_RAGGED_GATHER", mode)
+        with S.ScoreBank(devices=[0, 0]) as bank:
+            bank.set_penalties(*REF)
+            bank.load_query(q)
+            sc = torch.full((n,), -3, dtype=torch.int32, device=dev)
+            bank.score_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), n, 150,
+                                    sc.data_ptr(), min_len=64)
+            bank.sync()
+            kern = bank.last_kernel()
+            got = sc.cpu().numpy()
+        assert "gather" in kern and "balanced" in kern, kern
+        assert np.array_equal(got, want), (mode, int((got != want).sum()))

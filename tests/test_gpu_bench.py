@@ -49,8 +49,29 @@ def test_bench_two_ranks_gathered_parity(workload, steps, extra):
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["scaling"] == "weak"
+    assert d["dist"]["world_size"] == 2 and len(d["dist"]["devices"]) == 2
     ps = d["parity_sample"]
     assert ps["ranks"] == 2 and ps["mismatches"] == 0 and ps["targets"] >= 2 * 256, ps
+
+
+def test_bench_gpus_flag_starts_the_ranks():
+    """`python bench.py --gpus 2` with NO launcher (how the driver runs the N=1 leg): bench.py
+    starts the two ranks itself, and the line proves it -- n_gpus 2, the process group's world
+    size 2, both ranks' devices listed, rank 1's gathered slice bit-exact."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(SWBENCH_BACKEND="gloo", SWBENCH_SHARE_GPU="1")
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--reps", "64", "--cpu-seconds", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2, d
+    assert d["dist"]["world_size"] == 2 and d["dist"]["backend"] == "gloo"
+    assert len(d["dist"]["devices"]) == 2 and all(x["pci"] for x in d["dist"]["devices"])
+    assert d["dist"]["distinct_gpus"] == 1  # both ranks share the box's one GPU here
+    ps = d["parity_sample"]
+    assert ps["ranks"] == 2 and ps["mismatches"] == 0, ps
 
 
 @pytest.mark.parametrize("workload", ["ragged", "data500", "reads150x1k", "protein512x1k"])

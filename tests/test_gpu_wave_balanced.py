@@ -126,6 +126,10 @@ def test_wave_balanced_stall_fails_loudly(monkeypatch):
         with pytest.raises(S.SwbankError) as ei:
             bank.sync()
         assert ei.value.status == S.ERR_TIMEOUT
+        # the kind is counted and named (it used to count nothing, name nothing)
+        assert "wave balanced ranges" in str(ei.value), str(ei.value)
+        ctr = bank.counters()
+        assert ctr["wave_balanced_timeouts"] == 1 and ctr["balanced_timeouts"] == 0, ctr
         monkeypatch.delenv("SWBANK_STALL")
         monkeypatch.delenv("SWBANK_POLL_LIMIT")
         bank.score_batch_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), n, L,
