@@ -60,7 +60,7 @@ extern "C" hipError_t swk_launch_score(int R, int RB, int col0, int prof, int go
                                        uint32_t pS2, uint32_t ulen, uint32_t ustride, uint32_t nq,
                                        uint32_t qwords, size_t sstride, hipStream_t st);
 extern "C" unsigned swk_bal_slots(int W, uint32_t PS, int trim);
-extern "C" unsigned swk_wave_half_grid(int gotoh, uint32_t prof_bytes);
+extern "C" unsigned swk_wave_half_grid(int gotoh, uint32_t prof_bytes, int W);
 extern "C" hipError_t swk_bal_plan_uniform(void* plan, uint32_t ntiles, uint32_t K, uint32_t G,
                                            hipStream_t st);
 extern "C" hipError_t swk_launch_pair_bal(const uint8_t* res, const uint64_t* offs,

@@ -536,7 +536,7 @@ static sw_status batch_feed_once(sw_bank* b, const uint8_t* residues, size_t nre
   size_t min_chunk = 0;
   if (max_len && wave_preferred(b, n, max_len, b->f16 && b->f16_neg >= -2048 &&
                                                    env_int("SWBANK_F16", 1) != 0)) {
-    const unsigned grid = swk_wave_half_grid(b->gotoh() ? 1 : 0, (b->pad + 1) * b->wPS16);
+    const unsigned grid = swk_wave_half_grid(b->gotoh() ? 1 : 0, (b->pad + 1) * b->wPS16, 4);
     min_chunk = (size_t)(grid ? grid : 1024) * 16 * max_len;  // 4 waves x 2 pairs x 2 targets
     min_chunk = std::min(min_chunk, (size_t)256 << 20);          // (chunk_target's cap)
   }

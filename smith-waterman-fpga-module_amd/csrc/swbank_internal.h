@@ -54,6 +54,10 @@ typedef struct SwkWaveSplit {
    * the hand-off flags ((4 wbal_grid + 1) words, zeroed once, compared with wbal_gen) and lane
    * states ((4 wbal_grid + 1) x 36 x 64 words); fault / poll_limit / stall as above */
   unsigned wbal_blocks, wbal_grid, wbal_gen;
+  /* waves per block of the balanced launch (swk_wave_half_grid): 4 = one LDS profile copy per
+   * 4 waves (3 blocks, 3 waves per SIMD), 8 = one copy per 8 waves (2 blocks per CU, 4 waves
+   * per SIMD at <= 128 VGPRs); other launches of the two-pairs kernel use 4 */
+  unsigned wbal_waves;
   unsigned* wbal_flag;
   unsigned* wbal_state;
 } SwkWaveSplit;
@@ -66,6 +70,7 @@ typedef struct SwkWaveSplit {
 #define SWK_FAULT_TAIL 2u
 #define SWK_FAULT_WBAL 4u
 #define SWK_FAULT_WORDS 4
+
 
 /* One chunk of a streamed host batch (uploaded before the launch): its first tile and the
  * offset of its codes in the device batch buffer.  Its code layout travels in a flag word per

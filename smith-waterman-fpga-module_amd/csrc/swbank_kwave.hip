@@ -1166,8 +1166,10 @@ template <bool GOTOH>
 __device__ __forceinline__ void wave_half_finish(const ScoreArgs& a, uint2 b, int lane,
                                                  size_t p0);
 
-template <bool GOTOH>
-__global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
+// W waves per block share one LDS copy of the profile: W = 4 (3 blocks per CU: 3 waves per
+// SIMD) or W = 8 (2 blocks per CU: 4 waves per SIMD, <= 128 VGPRs; balanced launches only)
+template <bool GOTOH, int W>
+__global__ void __launch_bounds__(64 * W, W == 8 ? 4 : 1) score_wave_half(const ScoreArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint8_t* prof = reinterpret_cast<uint8_t*>(smem);
   const int lane = threadIdx.x & 63;
@@ -1257,8 +1259,8 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
   // least one unit, so a unit is cut at most once and every wait points to an earlier wave.
   // Without: one unit per wave.  One call site of wave_two_pairs for every visit (an inlined
   // copy per visit kind spills).
-  const uint32_t G = gridDim.x * 4,
-                 g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (uint32_t)wave);
+  const uint32_t G = gridDim.x * W,
+                 g = __builtin_amdgcn_readfirstlane(blockIdx.x * W + (uint32_t)wave);
   uint32_t u0 = 0, u1 = 0, whole0 = 0;
   int b0 = 0, b1 = 0, nvis = 1;
   if (a.wbal_blocks) {
@@ -1271,7 +1273,7 @@ __global__ void __launch_bounds__(256) score_wave_half(const ScoreArgs a) {
     whole0 = b0 ? u0 + 1 : u0;  // whole units [whole0, u1)
     nvis = (b1 ? 1 : 0) + (int)(u1 - whole0) + (b0 ? 1 : 0);
   } else {
-    whole0 = (blockIdx.x - a.split_blocks) * 4 + (uint32_t)wave;
+    whole0 = (blockIdx.x - a.split_blocks) * W + (uint32_t)wave;
     if (2 * (size_t)whole0 >= a.main_pairs || 4 * (size_t)whole0 >= a.n) return;  // whole wave
   }
   const size_t sw = (size_t)WBAL_WORDS * 64;
@@ -1346,21 +1348,23 @@ __device__ __forceinline__ void wave_half_finish(const ScoreArgs& a, uint2 b, in
 
 // the main blocks' LDS: the profile (prof_bytes at PS = 1024: 2 bytes per letter and row;
 // SWK_HALF_FMA: 4) + each wave's code rings
-static size_t wave_half_lds(uint32_t prof_bytes) {
-  return (size_t)prof_bytes / 1024 * SWK_HALF_LS + SWK_HALF_RING * 4;
+static size_t wave_half_lds(uint32_t prof_bytes, int W) {
+  return (size_t)prof_bytes / 1024 * SWK_HALF_LS + SWK_HALF_RING * (size_t)W;
 }
 
-template <bool GOTOH>
+template <bool GOTOH, int W>
 static hipError_t launch_wave_half(const ScoreArgs& a, uint32_t prof_bytes, hipStream_t st) {
   // 4 waves per block = 8 pairs, sharing one LDS copy of the profile; the split tail's blocks
   // hold every segment's profile
+  // (W = 8: balanced launches only, which have no split or segmented tail)
+  if (W != 4 && !a.wbal_blocks) return hipErrorInvalidValue;
   const size_t blocks = a.wbal_blocks ? (size_t)a.wbal_grid
                                       : a.split_blocks + ((size_t)a.main_pairs + 7) / 8 +
                                             ((size_t)a.tail_pairs * a.split_P + 3) / 4;
-  size_t lds = wave_half_lds(prof_bytes);
+  size_t lds = wave_half_lds(prof_bytes, W);
   if (a.split_blocks) lds = std::max<size_t>(lds, (size_t)a.split_words * 4 * a.split_P);
   if (a.tail_pairs) lds = std::max<size_t>(lds, (size_t)a.split_words * 4 * 4);  // a slice a wave
-  auto fn = &score_wave_half<GOTOH>;
+  auto fn = &score_wave_half<GOTOH, W>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -1373,27 +1377,30 @@ static hipError_t launch_wave_half(const ScoreArgs& a, uint32_t prof_bytes, hipS
   if (g_stamps_host) {  // (measurement builds) the record buffer in tctr, unused here
     ScoreArgs b = a;
     b.tctr = reinterpret_cast<uint32_t*>(g_stamps_host);
-    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(256), (unsigned)lds, st, b);
+    hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(64 * W), (unsigned)lds, st, b);
     return hipGetLastError();
   }
 #endif
-  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(256), (unsigned)lds, st, a);
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(64 * W), (unsigned)lds, st, a);
   return hipGetLastError();
 }
 
 }  // namespace swk
 
-// Resident 4-wave blocks of the two-pairs kernel (the balanced grid) for a profile of
-// prof_bytes at PS = 1024 (0 when the occupancy query fails).
-extern "C" unsigned swk_wave_half_grid(int gotoh, uint32_t prof_bytes) {
-  const void* fn = gotoh ? reinterpret_cast<const void*>(&swk::score_wave_half<true>)
-                         : reinterpret_cast<const void*>(&swk::score_wave_half<false>);
+// Resident W-wave blocks of the two-pairs kernel (the balanced grid) for a profile of
+// prof_bytes at PS = 1024 (0 when the occupancy query fails); W = 4 or 8.
+extern "C" unsigned swk_wave_half_grid(int gotoh, uint32_t prof_bytes, int W) {
+  const void* fn =
+      W == 8 ? (gotoh ? reinterpret_cast<const void*>(&swk::score_wave_half<true, 8>)
+                      : reinterpret_cast<const void*>(&swk::score_wave_half<false, 8>))
+             : (gotoh ? reinterpret_cast<const void*>(&swk::score_wave_half<true, 4>)
+                      : reinterpret_cast<const void*>(&swk::score_wave_half<false, 4>));
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
       hipSuccess)
     return 0;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
-  const int occ = swk::cached_occupancy(fn, 256, swk::wave_half_lds(prof_bytes), dev, &cus);
+  const int occ = swk::cached_occupancy(fn, 64 * W, swk::wave_half_lds(prof_bytes, W), dev, &cus);
   return occ > 0 && cus > 0 ? (unsigned)(occ * cus) : 0u;
 }
 
@@ -1427,7 +1434,9 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
     // balanced ranges of the two-pairs kernel (ScoreArgs.wbal_*): no split or tail
     if (!half || K != 8 || edge_in || edge_out || accum || split->pairs || !split->wbal_grid ||
         !split->wbal_flag || !split->wbal_state || !split->fault || split->poll_limit == 0 ||
-        (pairs + 1) / 2 < 4ull * split->wbal_grid || pairs > 0xFFFFFFFFull)
+        (split->wbal_waves != 4 && split->wbal_waves != 8) || pairs > 0xFFFFFFFFull ||
+        // every range at least 4 blocks: U B >= 4 G (a unit may be cut more than once)
+        (pairs + 1) / 2 * split->wbal_blocks < 4ull * split->wbal_waves * split->wbal_grid)
       return hipErrorInvalidValue;
     a.wbal_blocks = split->wbal_blocks;
     a.wbal_grid = split->wbal_grid;
@@ -1477,8 +1486,11 @@ extern "C" hipError_t swk_launch_wave(int K, int col0, int prof, int gotoh, int 
   if (half) {
     if (K != 8 || PS != 1024 || col0 || !prof || !f16 || edge_in || edge_out || accum)
       return hipErrorInvalidValue;
-    return gotoh ? swk::launch_wave_half<true>(a, prof_bytes, st)
-                 : swk::launch_wave_half<false>(a, prof_bytes, st);
+    if (a.wbal_blocks && split->wbal_waves == 8)
+      return gotoh ? swk::launch_wave_half<true, 8>(a, prof_bytes, st)
+                   : swk::launch_wave_half<false, 8>(a, prof_bytes, st);
+    return gotoh ? swk::launch_wave_half<true, 4>(a, prof_bytes, st)
+                 : swk::launch_wave_half<false, 4>(a, prof_bytes, st);
   }
 #define SWK_WCASE(KK, C0, PF, GT)                                                         \
   if (K == KK && col0 == C0 && prof == PF && gotoh == GT)                                 \

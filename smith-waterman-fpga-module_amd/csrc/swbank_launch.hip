@@ -171,23 +171,40 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
     const int sforce = env_int("SWBANK_WAVE_SPLIT", -1);
     // Balanced ranges (two pairs per wave, equal target lengths): every resident
     // wave slot scores the same number of 32-step blocks of the unit sequence, a unit cut by a
-    // range boundary handed between two waves, instead of a tail of pairs % slots pairs.  Needs
-    // at least one unit (two pairs) per slot and a remainder; SWBANK_WAVE_BAL=0 disables.
+    // range boundary handed between waves, instead of a tail of pairs % slots pairs.
+    // * 8-wave blocks (one LDS profile per 8 waves: 4 waves per SIMD, 4,096 slots) when there is
+    //   a unit per slot: +4-5 % over 4-wave blocks from 16,384 targets up.  Below, a unit is
+    //   longer than a range and its pieces form a chain (a middle visit waits for its
+    //   predecessor): the unit's serial length at a quarter of a SIMD outlasts the whole launch
+    //   at 3 waves per SIMD (12,500 targets: -11 %), so 4-wave blocks stay.
+    // * 4-wave blocks (3 waves per SIMD, 3,072 slots) with at least one unit per slot and a
+    //   remainder.
+    // SWBANK_WAVE_BAL=0 disables; SWBANK_WAVE_W=4 / =8 forces the block size (=8 down to ranges
+    // of 4 blocks: tests of the chained visits).
     bool wbal = false;
     if (half && b->wsegs == 1 && n == wspan && !b->no_handoff && (ustride || min_len == max_len) &&
         sforce < 0 && pairs <= 0xFFFFFFFFull && env_int("SWBANK_WAVE_BAL", 1) != 0) {
-      const unsigned grid = swk_wave_half_grid(gotoh ? 1 : 0, (b->pad + 1) * b->wPS16);
-      const size_t U = (pairs + 1) / 2, G = 4 * (size_t)grid;
+      const size_t U = (pairs + 1) / 2, B = (max_len + 31 + 31) / 32;
+      const int wforce = env_int("SWBANK_WAVE_W", 0);
+      int W = wforce == 4 ? 4 : 8;
+      unsigned grid = swk_wave_half_grid(gotoh ? 1 : 0, (b->pad + 1) * b->wPS16, W);
+      if (W == 8 && !(grid && (wforce == 8 ? U * B >= 4 * (size_t)W * grid
+                                            : U >= (size_t)W * grid))) {
+        W = 4;
+        grid = swk_wave_half_grid(gotoh ? 1 : 0, (b->pad + 1) * b->wPS16, W);
+      }
+      const size_t G = (size_t)W * grid;
       uint32_t* fw = grid ? fault_word(b) : nullptr;
-      if (grid && fw && U >= G && U % G) {
+      if (grid && fw && (W == 8 || (U >= G && U % G))) {
         const size_t sw = (G + 1) * 36 * 64;  // (WBAL_WORDS per lane)
         HIPOK(b, b->wbal_state.reserve(sw));
         if (b->wbal_flag.cap < G + 1) {  // zeroed once: flags carry wbal_gen
           HIPOK(b, b->wbal_flag.reserve(G + 1));
           HIPOK(b, hipMemsetAsync(b->wbal_flag.p, 0, b->wbal_flag.cap * 4, st));
         }
-        sp.wbal_blocks = (max_len + 31 + 31) / 32;
+        sp.wbal_blocks = (uint32_t)B;
         sp.wbal_grid = grid;
+        sp.wbal_waves = (unsigned)W;
         sp.wbal_gen = ++b->wbal_gen;
         sp.wbal_flag = b->wbal_flag.p;
         sp.wbal_state = b->wbal_state.p;
@@ -196,7 +213,7 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
         sp.stall = (unsigned)std::max(0, env_int("SWBANK_STALL", 0));
         wbal = true;
         const size_t L = strlen(b->last_kernel);
-        snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " balanced grid=%u", grid);
+        snprintf(b->last_kernel + L, sizeof(b->last_kernel) - L, " balanced grid=%ux%d", grid, W);
       }
     }
     if (!wbal && b->sK[0] && b->wsegs == 1 && n == wspan && pairs <= 0xFFFFFFFFull) {

@@ -1,10 +1,12 @@
 """GPU: balanced ranges of the two-pairs protein wave kernel.
 
 Every resident wave slot scores the same number of 32-step blocks of the unit sequence (a unit =
-two pairs = four targets); a unit cut by a range boundary is scored in two visits by two waves,
-the lane state (rows, running best, diagonal, bottom row) handed over through global memory and
-a flag.  configs[4]'s 12,500 targets per GPU are 3,125 units on 3,072 wave slots: without the
-balance the last 53 units would set the kernel's length (or run as a segmented tail).
+two pairs = four targets); a unit cut by a range boundary is scored in two visits by two waves
+(or, with fewer units than slots, in up to four: middle visits), the lane state (rows, running
+best, diagonal, bottom row) handed over through global memory and a flag.  configs[4]'s 12,500
+targets per GPU are 3,125 units on 3,072 wave slots of 4-wave blocks: without the balance the
+last 53 units would set the kernel's length (or run as a segmented tail); from 16,384 targets
+the launch takes 8-wave blocks (4,096 slots, 4 waves per SIMD).
 
 Checked: bit-exact against SWBANK_WAVE_BAL=0 (the segmented-tail path) and against the oracle on
 every target, over batch sizes just past one unit per slot to 1.5 units per slot, an odd target
@@ -30,10 +32,23 @@ def _batch(rng, n, qlen, L):
     return q, res, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32)
 
 
-@pytest.mark.parametrize("n,model", [(12_500, S.GAP_GOTOH), (12_290, S.GAP_GOTOH),
-                                     (18_001, S.GAP_MERGED), (12_500, S.GAP_MERGED)])
-def test_wave_balanced_exact(n, model, monkeypatch, poisoned_buffers):
+@pytest.mark.parametrize("n,model,w", [(12_500, S.GAP_GOTOH, 8), (12_290, S.GAP_GOTOH, 8),
+                                       (18_001, S.GAP_MERGED, 8), (12_500, S.GAP_MERGED, 8),
+                                       (8_000, S.GAP_GOTOH, 8), (5_001, S.GAP_MERGED, 8),
+                                       (12_500, S.GAP_GOTOH, 4), (18_001, S.GAP_MERGED, 4),
+                                       (12_500, S.GAP_GOTOH, 0), (18_001, S.GAP_GOTOH, 0)])
+def test_wave_balanced_exact(n, model, w, monkeypatch, poisoned_buffers):
+    """w = 8 (default): 8-wave blocks, 4 waves per SIMD, 4,096 wave slots: configs[4]'s 3,125
+    units are fewer than the slots, so units are cut up to twice (8,000 / 5,001 targets: up to
+    three and four times), middle visits waiting for their predecessor and handing on to their
+    successor.  w = 4 (SWBANK_WAVE_W=4): 3,072 slots, each unit cut at most once.  w = 0: the
+    library's choice -- 8-wave blocks from a unit per slot (18,001 targets), else 4."""
     torch = pytest.importorskip("torch")
+    if w:
+        monkeypatch.setenv("SWBANK_WAVE_W", str(w))
+    else:
+        monkeypatch.delenv("SWBANK_WAVE_W", raising=False)
+        w = 8 if n >= 16_384 else 4
     rng = np.random.default_rng(n + model)
     qlen, L = 512, 1000
     q, res, offs, lens = _batch(rng, n, qlen, L)
@@ -59,7 +74,7 @@ def test_wave_balanced_exact(n, model, monkeypatch, poisoned_buffers):
 
     (a1, a2), kern, ctr = run("1")
     (b1, _), kern0, _ = run("0")
-    assert "pairs/wave=2" in kern and "balanced" in kern, kern
+    assert "pairs/wave=2" in kern and "balanced" in kern and f"x{w}" in kern, kern
     assert "balanced" not in kern0, kern0
     assert ctr["tail_timeouts"] == 0 and ctr["balanced_timeouts"] == 0, ctr
     want = O.score_batch(q, res, offs, lens, O.BLOSUM62, -11, -1,
