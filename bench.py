@@ -368,6 +368,18 @@ def main():
     import swbank as S
 
     wl = Workload(args, rank, dev, S, torch)
+    probe_host = {}
+    if os.environ.get("SWBENCH_PROBE_HOST") == "1":  # (tuning aid) host-API medians by phase
+        def _hmed(tag):
+            o = np.empty(wl.n, np.int32)
+            wl.bank.score_batch(wl.res, wl.offs, wl.lens, out=o)
+            ts = []
+            for _ in range(9):
+                t0 = time.perf_counter()
+                wl.bank.score_batch(wl.res, wl.offs, wl.lens, out=o)
+                ts.append(time.perf_counter() - t0)
+            probe_host[tag] = round(float(np.median(ts)) * 1e3, 3)
+        _hmed("after_workload")
     gdev = dev if backend == "nccl" else torch.device("cpu")
     # The scoring stream, made torch's current one: on ROCm the default current stream's handle
     # is 0, which the library reads as "the bank's own (non-blocking) stream", so a score copy
@@ -444,6 +456,7 @@ def main():
     # the bank's per-call HIP-event time, summed over the timed steps (one call per step, which
     # runs several launches for long queries / query sets)
     score_s = score_ms / args.steps / 1e3
+    wl.bank_kernel_ms = score_s * 1e3  # (the host-buffer path's bound, host_api_rate)
     pack_s = pack_ms / args.steps / 1e3
     kernel = wl.bank.last_kernel()
     arith = "f16" if " f16" in kernel else "u16"
@@ -517,6 +530,9 @@ def main():
 
     last = sg.last()
     gather = sg.gathered
+    if probe_host:
+        _hmed("before_host_api_rate")
+        out["probe_host"] = probe_host
     if rank == 0 and world == 1 and wl.d_rec is None and len(wl.queries) == 1:
         out["pcie_inclusive"] = host_api_rate(wl, last)
     if rank == 0 and world == 1 and args.cpu_seconds > 0 and wl.kind == "q100xdata500":
@@ -543,7 +559,12 @@ def host_api_rate(wl, d_sc, iters=15):
     best-of-N figure overstates the rate).  Also checks its scores against the device-API run."""
     got = wl.bank.score_batch(wl.res, wl.offs, wl.lens)
     out = np.empty_like(got)  # the caller's output buffer, pages already touched
-    wl.bank.score_batch(wl.res, wl.offs, wl.lens, out=out)
+    warm = []
+    for _ in range(int(os.environ.get("SWBENCH_HOST_WARM", "1"))):
+        t0 = time.perf_counter()
+        wl.bank.score_batch(wl.res, wl.offs, wl.lens, out=out)
+        warm.append(round((time.perf_counter() - t0) * 1e3, 3))
+    h2d0 = wl.bank.counters()["h2d_bytes"]
     ts = []
     for _ in range(iters):
         t0 = time.perf_counter()
@@ -551,11 +572,43 @@ def host_api_rate(wl, d_sc, iters=15):
         ts.append(time.perf_counter() - t0)
     q1, med, q3 = np.percentile(ts, [25, 50, 75])
     same = bool(np.array_equal(got, d_sc[0].cpu().numpy()) and np.array_equal(out, got))
+    # The path's own ceiling: its host->device bytes per call (the library's count) at this
+    # box's pinned H2D rate (one timed copy of that many bytes), or the kernel, whichever is
+    # longer; frac = that bound / the median call.
+    nb = (wl.bank.counters()["h2d_bytes"] - h2d0) // iters
+    rate = h2d_rate(max(nb, 1 << 20))
+    kernel_ms = wl.bank_kernel_ms
+    bound_ms = max(kernel_ms, nb / rate / 1e6)
     return {"value": round(wl.cells / med / 1e9, 1), "unit": "GCUPS",
             "ms": round(med * 1e3, 3), "ms_iqr": [round(q1 * 1e3, 3), round(q3 * 1e3, 3)],
             "ms_best": round(min(ts) * 1e3, 3), "calls": iters, "matches_device_api": same,
+            "ms_warm": warm, "ms_calls": [round(t * 1e3, 3) for t in ts],
+            "bytes_h2d": int(nb), "h2d_gbs": round(rate, 1),
+            "bound_ms": round(bound_ms, 3),
+            "frac": round(bound_ms / (med * 1e3), 3),
+            "frac_of_device_rate": round(kernel_ms / (med * 1e3), 3),
             "api": "sw_score_batch: host buffers, gather + PCIe + kernel + scores back; median "
-                   f"of {iters} calls after 2 warm calls (value = cells / median)"}
+                   f"of {iters} calls after 2 warm calls (value = cells / median); bound_ms = "
+                   "max(score kernel, bytes_h2d / h2d_gbs), frac = bound_ms / median"}
+
+
+def h2d_rate(nbytes: int) -> float:
+    """This box's pinned host -> device copy rate (GB/s) for one copy of nbytes: best of 3,
+    HIP events on the copy's stream."""
+    import torch
+    src = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.Stream()
+    best = float("inf")
+    for _ in range(4):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s):
+            a.record(s)
+            dst.copy_(src, non_blocking=True)
+            b.record(s)
+        b.synchronize()
+        best = min(best, a.elapsed_time(b))
+    return nbytes / (best / 1e3) / 1e9
 
 
 def parity_sample(wl, per_rank, m=4096, full_cells=2e10):

@@ -288,11 +288,14 @@ typedef struct sw_counters {
   /* ABI 6: hand-off waits of the protein wave kernel's balanced ranges that ran out (the
    * tile kernel's are balanced_timeouts); each kind of time-out in a call is counted once */
   uint64_t wave_balanced_timeouts;
+  /* ABI 6: bytes the host-buffer calls copied host -> device (packed codes and metadata): the
+   * PCIe traffic of the drop-in path */
+  uint64_t h2d_bytes;
 } sw_counters;
 /* The first 8 counters (the ABI-3 struct, 64 bytes): safe for a caller of any ABI. */
 sw_status sw_bank_counters(const sw_bank *bank, sw_counters *out);
 /* out_size = sizeof(sw_counters) as the caller compiled it: 64 (ABI 3), 80 (ABI 4), 96 (ABI 5)
- * or 104 (ABI 6); any other size is SW_ERR_ARG.  No HIP call: the counts are host-side. */
+ * or 112 (ABI 6); any other size is SW_ERR_ARG.  No HIP call: the counts are host-side. */
 sw_status sw_bank_counters_ex(const sw_bank *bank, sw_counters *out, size_t out_size);
 
 /* Device-side failure reporting (≙ the CAPI host decoding the AFU's error bits and failing the

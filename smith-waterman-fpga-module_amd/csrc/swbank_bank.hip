@@ -343,13 +343,14 @@ static void sum_counters(sw_counters& c, const sw_bank* b) {
   c.tail_timeouts += b->ctr.tail_timeouts;
   c.handoff_reruns += b->ctr.handoff_reruns;
   c.wave_balanced_timeouts += b->ctr.wave_balanced_timeouts;
+  c.h2d_bytes += __atomic_load_n(&b->ctr.h2d_bytes, __ATOMIC_RELAXED);
 }
 
 // Host-side counts only (no HIP call): a hand-off time-out is counted when a synchronising call
 // takes it from the fault word.
 extern "C" sw_status sw_bank_counters_ex(const sw_bank* b, sw_counters* out, size_t out_size) {
   if (!b || !out) return SW_ERR_ARG;
-  // the struct sizes of ABI 3 (8 counters), ABI 4 (10), ABI 5 (12) and ABI 6 (13)
+  // the struct sizes of ABI 3 (8 counters), ABI 4 (10), ABI 5 (12) and ABI 6 (14)
   if (out_size != 64 && out_size != 80 && out_size != 96 && out_size != sizeof(sw_counters))
     return SW_ERR_ARG;
   sw_counters c{};

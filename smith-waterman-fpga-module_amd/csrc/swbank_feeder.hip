@@ -200,6 +200,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
     if (i >= (size_t)nds) HIPOK(b, hipStreamWaitEvent(b->copy_stream, b->kern_done[d], 0));
     HIPOK(b, hipMemcpyAsync(b->dslot[d].p + from, b->hslot[s].p + from, bytes - from,
                             hipMemcpyHostToDevice, b->copy_stream));
+    __atomic_fetch_add(&b->ctr.h2d_bytes, (uint64_t)(bytes - from), __ATOMIC_RELAXED);
     HIPOK(b, hipEventRecord(b->h2d_done[s], b->copy_stream));
     hipStream_t ks = overlap && (i & 1) ? b->stream2 : b->stream;
     HIPOK(b, hipStreamWaitEvent(ks, b->h2d_done[s], 0));

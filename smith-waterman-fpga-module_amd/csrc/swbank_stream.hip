@@ -409,6 +409,7 @@ sw_status stream_feed(sw_bank* b, const uint8_t* residues, size_t nres,
     std::memset(codes + bytes, 0, 16);  // the last targets' final step reads a few bytes past
     const hipError_t e1 = hipMemcpyAsync(b->sbuf.p + roff[i], codes, bytes + 16,
                                          hipMemcpyHostToDevice, b->copy_stream);
+    __atomic_fetch_add(&b->ctr.h2d_bytes, (uint64_t)(bytes + 16), __ATOMIC_RELAXED);
     const hipError_t e2 = e1 != hipSuccess ? e1 : hipEventRecord(b->h2d_done[s], b->copy_stream);
     const hipError_t e3 = e2 != hipSuccess ? e2 : hipEventRecord(b->sev[i], b->copy_stream);
     if (e3 != hipSuccess) {

@@ -48,7 +48,8 @@ EXPORTS = (
 ABI_VERSION = 6
 COUNTERS = ("stream_calls", "stream_reruns", "stream_declined", "chunked_calls", "device_sorts",
             "gather_timeouts", "mixed_chunks", "mixed_runs", "balanced_calls",
-            "balanced_timeouts", "tail_timeouts", "handoff_reruns", "wave_balanced_timeouts")
+            "balanced_timeouts", "tail_timeouts", "handoff_reruns", "wave_balanced_timeouts",
+            "h2d_bytes")
 MAX_DEVICES = 16
 RECORD_BYTES, RECORD_MAX_BASES = 64, 232
 
