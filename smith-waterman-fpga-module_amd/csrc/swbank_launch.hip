@@ -297,7 +297,8 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   // and the tail of a range are different tiles): checked with the caller's length bounds.
   unsigned rbal_grid = 0;
   if (dsort && !sort_out && !b->no_handoff && !use_wave && !perm && use_f16 && use_pair && !gotoh && nseg == 1 &&
-      wait_prev && packed == SWK_PACK_BYTES && min_len < max_len && max_len < 2048 && !opt16 &&
+      wait_prev && (packed == SWK_PACK_BYTES || packed == SWK_PACK_NIBBLE) && min_len < max_len &&
+      max_len < 2048 && !opt16 &&
       b->R == 32 && b->segs[0].W <= 4 && n <= 0xFFFFFFFFull && env_int("SWBANK_DSORT", 1) != 0 &&
       env_int("SWBANK_BAL", 1) != 0 && env_int("SWBANK_BAL_RAGGED", 1) != 0 &&
       !one_len_bin(min_len, max_len)) {
@@ -395,7 +396,8 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       // through the sort's permutation with the sort's plan.  SWBANK_BAL=0 disables.
       const bool rbal = pass == 0 && rbal_grid && perm && idx == perm && span == n;
       if (rbal || (pass == 0 && !b->no_handoff && f16 && use_pair && !gotoh && nseg == 1 && !idx && wait_prev &&
-                   packed == SWK_PACK_BYTES && min_len == max_len && max_len > 0 && span == n &&
+                   (packed == SWK_PACK_BYTES || packed == SWK_PACK_NIBBLE) && min_len == max_len &&
+                   max_len > 0 && span == n &&
                    ntiles * ((max_len + 7) / 8) < (1ull << 31) && !opt16 && b->R == 32 &&
                    b->segs[0].W <= 4 && env_int("SWBANK_BAL", 1) != 0)) {
         const int Wl = b->segs[0].W;
@@ -425,7 +427,8 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
           // permutation, each score written through it (ScoreArgs.sidx): a tile's targets are
           // then neighbours in memory (the codes' scatter).  =2: the copy in 4-bit
           // codes (SWK_PACK_NIBBLE), for alphabets of <= 16 codes
-          const int gmode = rbal && ragged_trim() ? env_int("SWBANK_RAGGED_GATHER", 0) : 0;
+          const int gmode = rbal && ragged_trim() && packed == SWK_PACK_BYTES
+                                ? env_int("SWBANK_RAGGED_GATHER", 0) : 0;
           const bool gat = gmode != 0;
           const bool gnib = gat && gmode == 2 && b->alpha <= 16;
           SwkDeal dl{};
@@ -454,7 +457,8 @@ sw_status launch(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                                        fw + (b->host_call ? SWK_FAULT_WORDS : 0), poll_limit(1u << 23),
                                        (uint32_t)std::max(0, env_int("SWBANK_STALL", 0)),
                                        rbal && ragged_trim(),
-                                       gnib ? (uint32_t)SWK_PACK_NIBBLE : (uint32_t)SWK_PACK_BYTES,
+                                       gnib ? (uint32_t)SWK_PACK_NIBBLE
+                                            : gat ? (uint32_t)SWK_PACK_BYTES : packed,
                                        gat ? idx : nullptr, st));
           ++b->ctr.balanced_calls;
           const size_t L = strlen(b->last_kernel);

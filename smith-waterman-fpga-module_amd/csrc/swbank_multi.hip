@@ -329,11 +329,18 @@ sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       cnt[d] = n > d ? (n - d + D - 1) / D : 0;
     }
   }
+  // DNA shares cross xGMI as 4-bit codes (SWK_PACK_NIBBLE: half the bytes of the copy that
+  // bounds this path, §7 of DESIGN); query sets and other alphabets as bytes.
+  // SWBANK_DEAL_NIB=0 keeps bytes.
+  const bool nib = !records && !set && b->alpha <= 16 && env_int("SWBANK_DEAL_NIB", 1) != 0;
   // (a 16-byte multiple: the deal gather stores whole 8-code chunks, not bytes)
-  const size_t stride = records ? SWB_RECORD : align16(std::max<uint32_t>(max_len, 1u));
+  const size_t stride = records ? SWB_RECORD
+                        : nib   ? align16(((size_t)std::max<uint32_t>(max_len, 1u) + 7) / 8 * 4)
+                                : align16(std::max<uint32_t>(max_len, 1u));
   SwkDeal dl{};
   dl.D = (unsigned)D;
   dl.stride = (unsigned)stride;
+  dl.nib = nib ? 1u : 0u;
   const uint32_t *perm = nullptr, *ident = nullptr;
   if (!records) {
     // 1. longest first (the sort's scratch zeroes itself; zeroed once here)
@@ -414,8 +421,8 @@ sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       st = set ? launch_set(k, k->res.p, k->offs.p, k->lens.p, c, min_len, max_len, k->scores.p,
                             ks, c)
                : launch(k, k->res.p, k->offs.p, k->lens.p, c, max_len, k->scores.p, ks,
-                        SWK_PACK_BYTES, nullptr, nullptr, true, true, nullptr, nullptr, 0, 0,
-                        min_len);
+                        nib ? SWK_PACK_NIBBLE : SWK_PACK_BYTES, nullptr, nullptr, true, true,
+                        nullptr, nullptr, 0, 0, min_len);
       if (st == SW_OK &&
           hip(hipMemcpyPeerAsync(const_cast<int*>(dl.scores[d]), root->device, k->scores.p,
                                  k->device, c * nq * 4, ks), "scores out"))
@@ -442,8 +449,8 @@ sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   // 4. scores to input order (query-major rows n apart for a set)
   if (!records) HIPOK(b, swk_deal_scatter(perm, ident, n, (unsigned)nq, n, &dl, d_scores, hs));
   HIPOK(b, hipEventRecord(b->ev_used, hs));
-  snprintf(b->last_kernel, sizeof(b->last_kernel), "multi[%zu] device deal%s: %s", D,
-           perm ? " longest-first" : "", root->last_kernel);
+  snprintf(b->last_kernel, sizeof(b->last_kernel), "multi[%zu] device deal%s%s: %s", D,
+           perm ? " longest-first" : "", nib ? " 4-bit" : "", root->last_kernel);
   if (d_ids && !records) {
     if ((st = track_best_device(root, d_scores, d_ids, n, hs)) != SW_OK)
       return fail(b, st, "device %d: %s", root->device, root->err);

@@ -295,8 +295,9 @@ def test_multi_device_bank_equals_single(devices, gather, monkeypatch):
     assert (want == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
 
 
+@pytest.mark.parametrize("nib", ["1", "0"])
 @pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0], [0]])
-def test_multi_device_bank_device_api(devices, poisoned_buffers):
+def test_multi_device_bank_device_api(devices, nib, poisoned_buffers, monkeypatch):
     """ABI 4/5: a multi-device bank takes device buffers (on the root device): the batch is
     sorted longest first on the root and dealt round robin (length-balanced, as the host path),
     each device copies its share into its own HBM, scores it there and copies its scores back,
@@ -305,6 +306,7 @@ def test_multi_device_bank_device_api(devices, poisoned_buffers):
     uniform batch on another stream right after (the staging reuse is ordered), a query set
     (every query broadcast to every device, ScoreBank_v2.v:101-102), and device records."""
     torch = pytest.importorskip("torch")
+    monkeypatch.setenv("SWBANK_DEAL_NIB", nib)  # (round 6: DNA shares cross as 4-bit codes)
     dev = torch.device("cuda", 0)
     q, seqs = _ragged_batch(40 + len(devices), 6000)
     res, offs, lens = O.pack_residues(seqs)
@@ -354,6 +356,7 @@ def test_multi_device_bank_device_api(devices, poisoned_buffers):
         got = run(multi)
         if len(devices) > 1:
             assert got[5].startswith(f"multi[{len(devices)}] device deal longest-first"), got[5]
+            assert (" 4-bit:" in got[5]) == (nib == "1"), got[5]
     assert (got[0] == want[0]).all() and got[1] == want[1]
     assert (got[2] == want[2]).all() and (got[3] == want[3]).all()
     assert (got[4] == want[4]).all()
@@ -629,8 +632,11 @@ def test_multi_device_ragged_gather_knob(monkeypatch):
     res = rng.integers(0, 4, int(lens.sum()) + 16, dtype=np.uint8)
     want = O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)
     d = [torch.from_numpy(x).to(dev) for x in (res, offs.view(np.int64), lens.view(np.int32))]
-    for mode in ("1", "2"):
-        monkeypatch.setenv("SWBANK_RAGGED_GATHER", mode)
+    for mode in ("1", "2", "nib"):
+        # "nib": the default deal (4-bit shares, round 6) -- the children's ragged balanced
+        # ranges read 4-bit codes; the gather knob applies to byte shares only
+        monkeypatch.setenv("SWBANK_DEAL_NIB", "1" if mode == "nib" else "0")
+        monkeypatch.setenv("SWBANK_RAGGED_GATHER", "0" if mode == "nib" else mode)
         with S.ScoreBank(devices=[0, 0]) as bank:
             bank.set_penalties(*REF)
             bank.load_query(q)
@@ -640,5 +646,6 @@ def test_multi_device_ragged_gather_knob(monkeypatch):
             bank.sync()
             kern = bank.last_kernel()
             got = sc.cpu().numpy()
-        assert "gather" in kern and "balanced" in kern, kern
+        assert "balanced" in kern and ("gather" in kern) == (mode != "nib"), kern
+        assert ("4-bit" in kern) == (mode == "nib"), kern
         assert np.array_equal(got, want), (mode, int((got != want).sum()))
