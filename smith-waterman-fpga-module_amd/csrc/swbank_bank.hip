@@ -120,8 +120,18 @@ extern "C" sw_status sw_bank_create(sw_bank** out, const sw_config* cfg_in) {
   if (!b) return SW_ERR_NOMEM;
   b->cfg = cfg;
   b->device = dev;
+  // The bank's four streams are created together, here: HIP maps streams onto its hardware
+  // queues (GPU_MAX_HW_QUEUES, 4 by default) in creation order, so streams the caller creates
+  // between the bank's creation and its first host-buffer call (torch's, in bench.py) used to
+  // push the feeder's second kernel stream onto the bank stream's queue -- the two chunk
+  // streams then serialised: ragged host calls 2.8-3.2 ms instead of 2.2-2.5 (LEDGER §3.2)
   if (hipSetDevice(dev) != hipSuccess ||
-      hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&b->out_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking) != hipSuccess) {
+    for (hipStream_t* x : {&b->stream, &b->copy_stream, &b->out_stream, &b->stream2})
+      if (*x) (void)hipStreamDestroy(*x);
     delete b;
     return SW_ERR_HIP;
   }

@@ -116,10 +116,7 @@ static sw_status feeder_init(sw_bank* b) {
   if (!b->pool) return fail(b, SW_ERR_NOMEM, "host worker pool");
   if (!b->launcher) b->launcher.reset(new (std::nothrow) Launcher(b->device));
   if (!b->launcher) return fail(b, SW_ERR_NOMEM, "feeder launch thread");
-  if (b->copy_stream) return SW_OK;
-  HIPOK(b, hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
-  HIPOK(b, hipStreamCreateWithFlags(&b->out_stream, hipStreamNonBlocking));
-  HIPOK(b, hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking));
+  if (b->ev_s2) return SW_OK;  // (the streams are the bank's, created with it)
   HIPOK(b, hipEventCreateWithFlags(&b->ev_s2, hipEventDisableTiming));
   for (int i = 0; i < sw_bank::NSLOT; ++i)
     HIPOK(b, hipEventCreateWithFlags(&b->h2d_done[i], hipEventDisableTiming));
