@@ -113,10 +113,20 @@ __device__ __forceinline__ void column_merged_f16_mask(const LK& lk, u16x2& diag
 // op_sel FMA per row (gen_f16_rows.py mode F) instead of 2-byte entries interleaved by a v_perm
 #define SWK_HALF_FMA 1
 #endif
+#ifndef SWK_HALF_ABSRING
+// two-pairs wave kernel (FMA profile, words a step ahead): the code ring holds each lane's
+// profile ADDRESS (relative to the ring slot), so with the 32-step ring window unrolled no step
+// computes an LDS address: no profile-address add, no ring-pointer op (wave_two_pairs)
+#define SWK_HALF_ABSRING 1
+#endif
 // the two-pairs kernel's LDS: the profile (letter stride SWK_HALF_LS bytes, 512 rows) and
-// each wave's code ring (profile offsets of both halves' targets, SWK_HALF_RING bytes a wave)
+// each wave's code ring (profile offsets of both halves' targets, SWK_HALF_RING bytes a wave);
+// SWK_HALF_ABSRING: wave 0's ring first, the profile at byte SWK_HALF_ABS_BASE, the other
+// waves' rings after it (the same total)
 #define SWK_HALF_LS (SWK_HALF_FMA ? 2048u : 1024u)
 #define SWK_HALF_RING (SWK_HALF_FMA ? 512u : 1024u)
+#define SWK_HALF_ABS (SWK_HALF_ABSRING && SWK_HALF_FMA && SWK_HALF_AHEAD)
+#define SWK_HALF_ABS_BASE 512u
 #define SWK_W_HT(B)                                                                           \
   [h0] "+v"(Hl[B]), [h1] "+v"(Hl[SWK_CLAMP(B + 1, K)]), [h2] "+v"(Hl[SWK_CLAMP(B + 2, K)]),    \
       [h3] "+v"(Hl[SWK_CLAMP(B + 3, K)]), [h4] "+v"(Hl[SWK_CLAMP(B + 4, K)]),                  \
@@ -849,11 +859,21 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   RingT* ring = reinterpret_cast<RingT*>(cring) + 128 * h;
   const RingT* ring_l = ring + 32 - hl;  // step T + j reads ring_l[j] (A), ring_l[64 + j] (B)
   uint32_t ringprev = pad | pad << 8;
+  // SWK_HALF_ABS: slot j of a half's ring (j in [0, 64): the window before and the current 32
+  // columns) holds the LDS byte address, from the block's LDS base, that lane hl needs at window
+  // step u when it reads slot j = 32 - hl + u, minus 16 u: the lane's rows of the column's letter
+  // sit at profile + letter x LS + 16 hl = (SWK_HALF_ABS_BASE + letter x LS + 16 (32 - j)) + 16 u,
+  // so the step adds 16 u and the profile piece as load offsets (immediates once the window is
+  // unrolled) and no address is computed.  Entries stay in [16, 65535] (24 letters x 2 KB).
+  const auto ring_entry = [&](uint32_t letter, uint32_t j) __attribute__((always_inline)) {
+    return SWK_HALF_ABS ? (RingT)(SWK_HALF_ABS_BASE + letter * LS + 512u - 16u * j)
+                        : (RingT)(letter * LS);
+  };
   const auto ring_write = [&](const uint32_t nc) __attribute__((always_inline)) {
-    ring[hl] = (RingT)((ringprev & 0xFFu) * LS);
-    ring[32 + hl] = (RingT)((nc & 0xFFu) * LS);
-    ring[64 + hl] = (RingT)((ringprev >> 8) * LS);
-    ring[96 + hl] = (RingT)((nc >> 8) * LS);
+    ring[hl] = ring_entry(ringprev & 0xFFu, hl);
+    ring[32 + hl] = ring_entry(nc & 0xFFu, 32 + hl);
+    ring[64 + hl] = ring_entry(ringprev >> 8, hl);
+    ring[96 + hl] = ring_entry(nc >> 8, 32 + hl);
     ringprev = nc;
   };
   // the ring holds the 32-column blocks k - 1 and k while steps 32 k .. 32 k + 31 run (k = t0 /
@@ -867,7 +887,26 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   // covers all 64 banks.  2-byte entries: 2 pieces (rows 0-7, 8-15); FMA words: 4 pieces.
   typedef typename std::conditional<SWK_HALF_FMA != 0, ProfLookupF<K>, ProfLookupK16<K>>::type LK;
   const uint8_t* plds = prof + hl * 16;
-  const auto load_prof = [&](auto& lk, uint32_t oa, uint32_t ob) __attribute__((always_inline)) {
+  // (SWK_HALF_ABS: u = the step's place in the ring window, 16 u a load offset; a ring entry IS
+  // the LDS byte address: score_wave_half declares no static LDS, so its dynamic LDS -- the
+  // profile at SWK_HALF_ABS_BASE -- starts at LDS address 0.  An integer turned into an LDS
+  // pointer, because "dynamic LDS base + entry" keeps an add of the base symbol (0) per load
+  // address that LLVM does not fold.)
+  const auto load_prof = [&](auto& lk, uint32_t oa, uint32_t ob, uint32_t u = 0)
+                             __attribute__((always_inline)) {
+#if SWK_HALF_ABS
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const v4u lds_v4u;
+    (void)plds;
+#pragma unroll
+    for (int q = 0; q < K / 4; ++q) {
+      const v4u x = *reinterpret_cast<lds_v4u*>((uintptr_t)(oa + 16u * u + 512u * q));
+      const v4u y = *reinterpret_cast<lds_v4u*>((uintptr_t)(ob + 16u * u + 512u * q));
+      lk.a[4 * q] = x.x; lk.a[4 * q + 1] = x.y; lk.a[4 * q + 2] = x.z; lk.a[4 * q + 3] = x.w;
+      lk.b[4 * q] = y.x; lk.b[4 * q + 1] = y.y; lk.b[4 * q + 2] = y.z; lk.b[4 * q + 3] = y.w;
+    }
+#else
+    (void)u;
     const uint8_t* la = plds + oa;
     const uint8_t* lb = plds + ob;
     if constexpr (SWK_HALF_FMA) {
@@ -887,6 +926,7 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
         lk.hi[4 * q] = y.x; lk.hi[4 * q + 1] = y.y; lk.hi[4 * q + 2] = y.z; lk.hi[4 * q + 3] = y.w;
       }
     }
+#endif
   };
   // AHEAD: a step's profile words are loaded during the step before (its ring entries two
   // steps before), so no step waits on its own LDS reads: with 3-4 waves per SIMD the other
@@ -906,6 +946,43 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
   // of steps from an even t never wraps, so one address per pair and immediate offsets.
   // SWK_HALF_UNROLL: steps per loop iteration (2 or 4)
   const RingT* rp = ring_l;
+#if SWK_HALF_ABS
+  // one step at window place u (t & 31 == u): the ring refill at u = 30, the words of step t + 1
+  // (place u + 1) and the ring entries of step t + 2 (place u + 2) read with constant offsets
+  // when u is a constant (the unrolled window below), else (the last partial window) computed
+  const auto step_abs = [&](const int t, const int u) __attribute__((always_inline)) {
+    if (u == 30) {
+      ring_write(ncode);
+      uint32_t tt = (uint32_t)t;
+      asm volatile("" : "+s"(tt));
+      ncode = load_codes(tt + 34u + hl);
+    }
+    LK lk = lkn;
+    load_prof(lkn, nra, nrb, (uint32_t)((u + 1) & 31));
+    nra = ring_l[(u + 2) & 31];
+    nrb = ring_l[64 + ((u + 2) & 31)];
+    __builtin_amdgcn_sched_barrier(0);
+    u16x2 upH, upX;
+    uint32_t uh, ux;
+    asm volatile(
+        "s_nop 1\n\t"
+        "s_mov_b64 vcc, %[m]\n\t"
+        "v_cndmask_b32_dpp %[uh], %[bh], %[h0], vcc wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_cndmask_b32_dpp %[ux], %[bx], %[x0], vcc wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : [uh] "=&v"(uh), [ux] "=&v"(ux)
+        : [bh] "v"(botH), [bx] "v"(botX), [h0] "v"(h0v), [x0] "v"(x0v), [m] "s"(topmask)
+        : "vcc");
+    upH = as_u16x2(uh);
+    upX = as_u16x2(ux);
+    u16x2 diag = prevUpH;
+    prevUpH = upH;
+    __builtin_amdgcn_sched_barrier(0);
+    column_f16_lane_asm<K, GOTOH>(lk, diag, upX, Hl, Xl, best, noe, ne, no);
+    asm volatile("" : "+v"(best));
+    botH = as_u32(Hl[K - 1]);
+    botX = as_u32(upX);
+  };
+#endif
   const auto step = [&](const int t, const bool even) __attribute__((always_inline)) {
     // the next 32 columns go in before they are read (AHEAD: two steps before)
     if ((AHEAD ? even : !even) && (t & 31) == (AHEAD ? 30 : 31)) {
@@ -961,6 +1038,17 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
     botX = as_u32(upX);
   };
   const int nsteps = min(Lmax + 31, t1);
+#if SWK_HALF_ABS
+  (void)step;
+  (void)rp;
+  // whole 32-step windows unrolled (t0 is a multiple of 32), then the last partial window
+  int t = t0;
+  for (; t + 32 <= nsteps; t += 32) {
+#pragma unroll
+    for (int u = 0; u < 32; ++u) step_abs(t + u, u);
+  }
+  for (; t < nsteps; ++t) step_abs(t, t & 31);
+#else
   for (int t = t0; t < nsteps; t += SWK_HALF_UNROLL) {
 #pragma unroll
     for (int u = 0; u < SWK_HALF_UNROLL; u += 2) {
@@ -969,6 +1057,7 @@ __device__ __forceinline__ uint2 wave_two_pairs(const ScoreArgs& a, const uint8_
       step(t + u + 1, false);
     }
   }
+#endif
   if (sout) {  // a head visit: the lane state for the successor's tail visit (sc1 stores)
     uint32_t* sp = sout + lane;
 #pragma unroll
@@ -1221,7 +1310,7 @@ __global__ void __launch_bounds__(64 * W, W == 8 ? 4 : 1) score_wave_half(const 
     // l: two 16-byte LDS stores; the loads of a thread's iterations are independent)
     const uint32_t groups = (a.pad + 1) * 64;
     const uint4* src = reinterpret_cast<const uint4*>(a.qtab);
-    uint4* dst = reinterpret_cast<uint4*>(prof);
+    uint4* dst = reinterpret_cast<uint4*>(prof + (SWK_HALF_ABS ? SWK_HALF_ABS_BASE : 0u));
     const auto widen = [](uint32_t x) {  // two entries -> two {s, 1.0} words
       return make_uint2((x & 0xFFFFu) | 0x3C000000u, (x >> 16) | 0x3C000000u);
     };
@@ -1248,7 +1337,11 @@ __global__ void __launch_bounds__(64 * W, W == 8 ? 4 : 1) score_wave_half(const 
     __syncthreads();
   }
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* cring = prof + (a.pad + 1) * SWK_HALF_LS + SWK_HALF_RING * wave;
+  // (SWK_HALF_ABS: wave 0's ring at byte 0, the profile from SWK_HALF_ABS_BASE = one ring on)
+  uint8_t* mprof = prof + (SWK_HALF_ABS ? SWK_HALF_ABS_BASE : 0u);
+  uint8_t* cring = SWK_HALF_ABS && wave == 0
+                       ? prof
+                       : mprof + (a.pad + 1) * SWK_HALF_LS + SWK_HALF_RING * (wave - (SWK_HALF_ABS ? 1 : 0));
   // Balanced ranges (ScoreArgs.wbal_blocks): wave g of the G resident waves scores
   // blocks [A_g, A_g+1) of the unit-major sequence of 32-step blocks, A_g = g U B / G (U units
   // of two pairs, B blocks each), so every wave slot gets the same number of steps whatever
@@ -1299,7 +1392,7 @@ __global__ void __launch_bounds__(64 * W, W == 8 ? 4 : 1) score_wave_half(const 
 #endif
     }
     const uint2 b = wave_two_pairs<GOTOH>(
-        a, prof, cring, lane, 2 * (size_t)unit, tail ? 32 * b0 : 0, head ? 32 * b1 : 0x7FFFFFFF,
+        a, mprof, cring, lane, 2 * (size_t)unit, tail ? 32 * b0 : 0, head ? 32 * b1 : 0x7FFFFFFF,
         tail ? a.bal_state + (size_t)g * sw : nullptr,
         head ? a.bal_state + (size_t)(g + 1) * sw : nullptr);
     if (head) {  // the lane state is out: wave g + 1 may take the unit on
