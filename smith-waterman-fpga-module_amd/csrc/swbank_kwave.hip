@@ -1463,6 +1463,12 @@ static hipError_t launch_wave_half(const ScoreArgs& a, uint32_t prof_bytes, hipS
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
+    // SWK_HALF_ABS: the ring entries are LDS addresses counted from 0, which holds only while
+    // the kernel has no static LDS (its dynamic LDS then starts at 0)
+    hipFuncAttributes fa;
+    e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fn));
+    if (e != hipSuccess) return e;
+    if (SWK_HALF_ABS && fa.sharedSizeBytes != 0) return hipErrorInvalidConfiguration;
     attr_set = true;
   }
   if (lds > 160 * 1024) return hipErrorInvalidConfiguration;
