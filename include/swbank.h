@@ -166,7 +166,9 @@ sw_status sw_score_batch(sw_bank *bank, const uint8_t *residues, size_t residues
  * or from the host.  On a multi-device bank (ABI 5) the buffers and the stream belong to the
  * root device (devices[0]): the batch is ordered longest first on the root (when its lengths
  * differ) and dealt round robin over the devices (length-balanced); each device copies its
- * share into its own HBM (max_len + 12 bytes per target over xGMI), scores it there and copies
+ * share into its own HBM (DNA as 4-bit codes, ceil(max_len / 8) * 4 + 12 bytes per target over
+ * xGMI, a share of more than one round of the kernel's slots in chunks that copy while the
+ * previous chunk is scored; other alphabets max_len + 12 bytes), scores it there and copies
  * its int32 scores back, and the root writes them to d_scores in input order; the devices'
  * work is ordered after the caller's stream and the caller's stream after it (n < 2^32).
  * Device memory is not validated: the caller keeps every target inside d_residues

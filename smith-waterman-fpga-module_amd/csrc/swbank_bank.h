@@ -513,6 +513,8 @@ struct sw_bank {
   uint32_t bal_gen = 0;
   bool peer_ready = false;
   hipEvent_t ev_join = nullptr;
+  // a multi-device child's pipelined deal: chunk p of its share is in its HBM (copy_stream)
+  std::vector<hipEvent_t> deal_ev;
   bool best_root = false;
   // on-device longest-first order of a ragged device batch (sw_score_batch_device):
   // dperm = visiting order + count, dsort = histogram / scan scratch

@@ -191,6 +191,7 @@ extern "C" void sw_bank_destroy(sw_bank* b) {
   if (b->ev_used) (void)hipEventDestroy(b->ev_used);
   if (b->best_ev) (void)hipEventDestroy(b->best_ev);
   if (b->ev_join) (void)hipEventDestroy(b->ev_join);
+  for (hipEvent_t e : b->deal_ev) (void)hipEventDestroy(e);
   b->fb_idx.release();
   b->fb_cnt.release();
   b->best_key.release();

@@ -290,6 +290,26 @@ sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_t* scor
 // reuses the staging buffers only after this call's scatter (ev_done).  A device listed twice,
 // or the root itself, copies within its own memory.  With d_ids the batch best hit is tracked on
 // the root after the scatter (sw_batch_best).
+// Targets per chunk of a pipelined deal (multi_device): a share bigger than one round of the tile
+// kernel's resident workgroup slots (G x 128 targets, G = swk_bal_slots) is copied and scored in
+// chunks of whole rounds, at most SWK_DEAL_PIPE_MAX of them, so chunk p + 1 crosses xGMI while
+// chunk p is scored.  A share within one round is latency-bound at one tile's duration, which a
+// cut cannot shorten, and a device that is the root itself copies within its own HBM:
+// both stay whole.  SWBANK_DEAL_PIPE=0 disables; SWBANK_DEAL_CHUNK=n forces chunks of n targets
+// (tests: it also applies to the root's own share; at most 64 chunks).
+constexpr size_t SWK_DEAL_PIPE_MAX = 8;
+static size_t deal_chunk(sw_bank* k, const sw_bank* root, size_t c) {
+  if (env_int("SWBANK_DEAL_PIPE", 1) == 0) return c;
+  const int forced = env_int("SWBANK_DEAL_CHUNK", 0);
+  if (forced > 0) return std::min(c, std::max((size_t)forced, (c + 63) / 64));  // <= 64 chunks
+  if (k->device == root->device) return c;
+  const unsigned G = swk_bal_slots(k->segs[0].W, k->pair_bytes, 0);  // (on k's device)
+  const size_t round = (size_t)G * SWB_TILE;
+  if (!G || c <= round) return c;
+  const size_t rounds = (c + round - 1) / round;
+  return (rounds + SWK_DEAL_PIPE_MAX - 1) / SWK_DEAL_PIPE_MAX * round;
+}
+
 sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                        const uint32_t* d_lens, const uint64_t* d_ids, size_t n, uint32_t min_len,
                        uint32_t max_len, int32_t* d_scores, hipStream_t hs, bool records) {
@@ -377,6 +397,7 @@ sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   // 3. every device: its share in, scored in its own HBM, scores out
   sw_status st = SW_OK;
   std::vector<bool> launched(D, false);
+  size_t pipe = 1;  // the most chunks a share was cut into
   for (size_t d = 0; d < D && st == SW_OK; ++d) {
     sw_bank* k = b->kids[d];
     const size_t c = cnt[d];
@@ -409,6 +430,45 @@ sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
       if (st == SW_OK &&
           hip(hipMemcpyPeerAsync(d_scores + lo[d], root->device, k->scores.p, k->device, c * 4,
                                  ks), "scores out"))
+        (void)hip(hipEventRecord(k->ev_used, ks), "event");  // the copy-out read k->scores
+    } else if (const size_t chunk = nib ? deal_chunk(k, root, c) : c; chunk < c) {
+      // pipelined: chunk p + 1 crosses xGMI on the copy stream while chunk p is scored on ks.
+      // The share is longest first already (positions d, d + D, ... of the sorted order), so
+      // the chunks launch without a sort of their own.
+      const hipStream_t cs = k->copy_stream;
+      const size_t P = (c + chunk - 1) / chunk;
+      if (!hip(hipStreamWaitEvent(cs, b->ev_join, 0), "stream wait") ||
+          !hip(hipStreamWaitEvent(cs, k->ev_used, 0), "stream wait"))
+        break;
+      while (k->deal_ev.size() < P && st == SW_OK) {
+        hipEvent_t e = nullptr;
+        if (hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event")) k->deal_ev.push_back(e);
+      }
+      size_t copied = 0;  // chunks whose copies are enqueued (and their event recorded)
+      for (; copied < P && st == SW_OK; ++copied) {
+        const size_t c0 = copied * chunk, cc = std::min(chunk, c - c0);
+        if (!hip(hipMemcpyPeerAsync(k->res.p + c0 * stride, k->device, dl.codes[d] + c0 * stride,
+                                    root->device, cc * stride, cs), "codes in") ||
+            !hip(hipMemcpyPeerAsync(k->offs.p + c0, k->device, dl.offs[d] + c0, root->device,
+                                    cc * 8, cs), "offsets in") ||
+            !hip(hipMemcpyPeerAsync(k->lens.p + c0, k->device, dl.lens[d] + c0, root->device,
+                                    cc * 4, cs), "lengths in") ||
+            !hip(hipEventRecord(k->deal_ev[copied], cs), "event"))
+          break;
+      }
+      for (size_t p = 0; p < copied && st == SW_OK; ++p) {
+        const size_t c0 = p * chunk, cc = std::min(chunk, c - c0);
+        if (!hip(hipStreamWaitEvent(ks, k->deal_ev[p], 0), "stream wait")) break;
+        st = launch(k, k->res.p, k->offs.p + c0, k->lens.p + c0, cc, max_len, k->scores.p + c0,
+                    ks, SWK_PACK_NIBBLE, nullptr, nullptr, false, true, nullptr, nullptr, 0, 0,
+                    min_len);
+      }
+      // (after a failure too: nothing on ks may run ahead of copies still reading the staging)
+      if (copied) (void)hipStreamWaitEvent(ks, k->deal_ev[copied - 1], 0);
+      pipe = std::max(pipe, P);
+      if (st == SW_OK &&
+          hip(hipMemcpyPeerAsync(const_cast<int*>(dl.scores[d]), root->device, k->scores.p,
+                                 k->device, c * 4, ks), "scores out"))
         (void)hip(hipEventRecord(k->ev_used, ks), "event");  // the copy-out read k->scores
     } else {
       if (!hip(hipMemcpyPeerAsync(k->res.p, k->device, dl.codes[d], root->device, c * stride, ks),
@@ -449,8 +509,10 @@ sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
   // 4. scores to input order (query-major rows n apart for a set)
   if (!records) HIPOK(b, swk_deal_scatter(perm, ident, n, (unsigned)nq, n, &dl, d_scores, hs));
   HIPOK(b, hipEventRecord(b->ev_used, hs));
-  snprintf(b->last_kernel, sizeof(b->last_kernel), "multi[%zu] device deal%s%s: %s", D,
-           perm ? " longest-first" : "", nib ? " 4-bit" : "", root->last_kernel);
+  char pl[32] = "";
+  if (pipe > 1) snprintf(pl, sizeof(pl), " pipelined x%zu", pipe);
+  snprintf(b->last_kernel, sizeof(b->last_kernel), "multi[%zu] device deal%s%s%s: %s", D,
+           perm ? " longest-first" : "", nib ? " 4-bit" : "", pl, root->last_kernel);
   if (d_ids && !records) {
     if ((st = track_best_device(root, d_scores, d_ids, n, hs)) != SW_OK)
       return fail(b, st, "device %d: %s", root->device, root->err);

@@ -295,7 +295,7 @@ def test_multi_device_bank_equals_single(devices, gather, monkeypatch):
     assert (want == O.score_batch(q, res, offs, lens, O.dna_matrix(), -12, -4)).all()
 
 
-@pytest.mark.parametrize("nib", ["1", "0"])
+@pytest.mark.parametrize("nib", ["1", "0", "pipe"])
 @pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0], [0]])
 def test_multi_device_bank_device_api(devices, nib, poisoned_buffers, monkeypatch):
     """ABI 4/5: a multi-device bank takes device buffers (on the root device): the batch is
@@ -304,9 +304,15 @@ def test_multi_device_bank_device_api(devices, nib, poisoned_buffers, monkeypatc
     asynchronous on the caller's stream (ScoreBank_v2.v:117-137: each module latches its own
     target copy).  Bit-exact against a single bank for a ragged batch with the best hit, a
     uniform batch on another stream right after (the staging reuse is ordered), a query set
-    (every query broadcast to every device, ScoreBank_v2.v:101-102), and device records."""
+    (every query broadcast to every device, ScoreBank_v2.v:101-102), and device records.
+    nib="pipe": 4-bit shares cut into chunks of 700 targets, each scored while the next copies
+    (the pipelined deal; without the knob only a share of more than one round of the tile
+    kernel's slots on another device is cut)."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("SWBANK_DEAL_NIB", nib)  # (round 6: DNA shares cross as 4-bit codes)
+    # (round 6: DNA shares cross as 4-bit codes)
+    monkeypatch.setenv("SWBANK_DEAL_NIB", "0" if nib == "0" else "1")
+    if nib == "pipe":
+        monkeypatch.setenv("SWBANK_DEAL_CHUNK", "700")
     dev = torch.device("cuda", 0)
     q, seqs = _ragged_batch(40 + len(devices), 6000)
     res, offs, lens = O.pack_residues(seqs)
@@ -356,7 +362,8 @@ def test_multi_device_bank_device_api(devices, nib, poisoned_buffers, monkeypatc
         got = run(multi)
         if len(devices) > 1:
             assert got[5].startswith(f"multi[{len(devices)}] device deal longest-first"), got[5]
-            assert (" 4-bit:" in got[5]) == (nib == "1"), got[5]
+            assert (" 4-bit" in got[5]) == (nib != "0"), got[5]
+            assert (" pipelined x" in got[5]) == (nib == "pipe"), got[5]
     assert (got[0] == want[0]).all() and got[1] == want[1]
     assert (got[2] == want[2]).all() and (got[3] == want[3]).all()
     assert (got[4] == want[4]).all()
@@ -489,10 +496,11 @@ _DS_SEEDS = int(os.environ.get("SWBANK_DEAL_SOAK_SEEDS", "3"))
 
 
 @pytest.mark.parametrize("seed", range(_DS_BASE, _DS_BASE + _DS_SEEDS))
-def test_multi_device_deal_soak(seed):
+def test_multi_device_deal_soak(seed, monkeypatch):
     """Seeded device calls on multi-device banks (2-4 devices, every one the box's GPU): random
-    batch sizes, ragged lengths with empties, N codes, scattered offsets; the deal (sort, gather
-    to each device's staging, copies, scatter back) equals a one-device bank on every target."""
+    batch sizes, ragged lengths with empties, N codes, scattered offsets, half of them with the
+    shares cut into random chunks (the pipelined deal); the deal (sort, gather to each device's
+    staging, copies, scatter back) equals a one-device bank on every target."""
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(90_000 + seed)
@@ -514,8 +522,10 @@ def test_multi_device_deal_soak(seed):
     d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
     d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
     L = max(1, int(lens.max()))
+    chunk = int(rng.integers(1, 3000)) if rng.random() < 0.5 else 0
 
     def run(devices):
+        monkeypatch.setenv("SWBANK_DEAL_CHUNK", str(chunk if len(devices) > 1 else 0))
         with S.ScoreBank(devices=devices) as bank:
             bank.set_penalties(*REF)
             bank.load_query(q)
@@ -527,7 +537,7 @@ def test_multi_device_deal_soak(seed):
 
     got = run([0] * D)
     want = run([0])
-    assert np.array_equal(got, want), (D, n, maxl, int((got != want).sum()))
+    assert np.array_equal(got, want), (D, n, maxl, chunk, int((got != want).sum()))
 
 
 @pytest.mark.parametrize("devices,gather", [([0, 0], "copy"), ([0, 0, 0], "copy"),
