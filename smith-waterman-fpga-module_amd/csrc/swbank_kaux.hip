@@ -437,7 +437,10 @@ extern "C" hipError_t swk_launch_i32(int gotoh, const uint8_t* res, const uint64
 // offsets in place + perm_n = n; scatter: per block, LDS bin counts, one global atomic per
 // non-empty bin reserves the block's range, LDS atomics place the elements.
 namespace swk {
-constexpr int SORT_BINS = 2048, SORT_BLOCK = 1024, SORT_ITEMS = 8;
+#ifndef SWK_SORT_ITEMS
+#define SWK_SORT_ITEMS 8  // lengths per thread of the device sort's kernels
+#endif
+constexpr int SORT_BINS = 2048, SORT_BLOCK = 1024, SORT_ITEMS = SWK_SORT_ITEMS;
 
 __device__ __forceinline__ uint32_t sort_bin(uint32_t len, uint32_t max_len, uint32_t shift) {
   return (max_len - min(len, max_len)) >> shift;
