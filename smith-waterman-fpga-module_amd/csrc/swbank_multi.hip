@@ -270,26 +270,6 @@ sw_status multi_records(sw_bank* b, const uint8_t* recs, size_t n, int32_t* scor
   return SW_OK;
 }
 
-// Device buffers on a multi-device bank (the caller's buffers live on the root device,
-// devices[0]; ≙ the ScoreBank's MODULES, each latching its own copy of its target before
-// scoring it, ScoreBank_v2.v:117-137, SM_Feeder3.v:104-182).  Every device scores its share
-// from its OWN HBM: xGMI carries one bulk copy in and the scores out, never the kernel's reads.
-//  1. the visiting order: a ragged batch is sorted longest first on the root (swk_sort_lens),
-//     and position p goes to device p % D -- the length-balanced deal of the host path
-//     (multi_batch); a batch of one length keeps its order;
-//  2. one gather kernel on the root copies each device's targets into its region of a staging
-//     buffer at a fixed stride of max_len bytes rounded up to 16 (offsets rebased, lengths kept);
-//  3. device d copies its region into its own buffers (hipMemcpyPeerAsync on its stream: codes
-//     cnt_d x max_len bytes + 12 bytes per target), scores them there (launch / launch_set) and
-//     copies its nq x cnt_d int32 scores back into the root's receive buffer;
-//  4. one scatter kernel on the root writes them to d_scores in input order.
-// CAPI records (fixed 64 bytes, contiguous ranges) skip 1, 2 and 4: each device copies its
-// range of records and writes its scores straight into the caller's d_scores.
-// Asynchronous: the devices' work waits for the caller's stream (an event after the gather),
-// the caller's stream waits for every device (an event each) before the scatter; the next call
-// reuses the staging buffers only after this call's scatter (ev_done).  A device listed twice,
-// or the root itself, copies within its own memory.  With d_ids the batch best hit is tracked on
-// the root after the scatter (sw_batch_best).
 // Targets per chunk of a pipelined deal (multi_device): a share bigger than one round of the tile
 // kernel's resident workgroup slots (G x 128 targets, G = swk_bal_slots) is copied and scored in
 // chunks of whole rounds, at most SWK_DEAL_PIPE_MAX of them, so chunk p + 1 crosses xGMI while
@@ -310,6 +290,28 @@ static size_t deal_chunk(sw_bank* k, const sw_bank* root, size_t c) {
   return (rounds + SWK_DEAL_PIPE_MAX - 1) / SWK_DEAL_PIPE_MAX * round;
 }
 
+// Device buffers on a multi-device bank (the caller's buffers live on the root device,
+// devices[0]; ≙ the ScoreBank's MODULES, each latching its own copy of its target before
+// scoring it, ScoreBank_v2.v:117-137, SM_Feeder3.v:104-182).  Every device scores its share
+// from its OWN HBM: xGMI carries one bulk copy in and the scores out, never the kernel's reads.
+//  1. the visiting order: a ragged batch is sorted longest first on the root (swk_sort_lens),
+//     and position p goes to device p % D -- the length-balanced deal of the host path
+//     (multi_batch); a batch of one length keeps its order;
+//  2. one gather kernel on the root copies each device's targets into its region of a staging
+//     buffer at a fixed stride of max_len bytes rounded up to 16 (offsets rebased, lengths kept);
+//  3. device d copies its region into its own buffers (hipMemcpyPeerAsync on its stream: codes
+//     cnt_d x stride bytes + 12 bytes per target; a 4-bit share of more than one round in
+//     chunks on its copy stream, each scored as it lands, deal_chunk), scores them there
+//     (launch / launch_set) and copies its nq x cnt_d int32 scores back into the root's
+//     receive buffer;
+//  4. one scatter kernel on the root writes them to d_scores in input order.
+// CAPI records (fixed 64 bytes, contiguous ranges) skip 1, 2 and 4: each device copies its
+// range of records and writes its scores straight into the caller's d_scores.
+// Asynchronous: the devices' work waits for the caller's stream (an event after the gather),
+// the caller's stream waits for every device (an event each) before the scatter; the next call
+// reuses the staging buffers only after this call's scatter (ev_done).  A device listed twice,
+// or the root itself, copies within its own memory.  With d_ids the batch best hit is tracked on
+// the root after the scatter (sw_batch_best).
 sw_status multi_device(sw_bank* b, const uint8_t* d_res, const uint64_t* d_offs,
                        const uint32_t* d_lens, const uint64_t* d_ids, size_t n, uint32_t min_len,
                        uint32_t max_len, int32_t* d_scores, hipStream_t hs, bool records) {
