@@ -855,10 +855,16 @@ __device__ __forceinline__ int tile_nch(const uint8_t* res, const uint32_t* lens
 // wave w reads its row words as 4 blocks of 8 (two ds_read_b128 each), one block ahead of
 // the asm block that consumes them: 6.5 VALU per 2 cells instead of 7.5.
 // Wave-uniform code layout of streamed chunk c, waiting until its copy landed.  Every wait
-// polls the device word; one poll in 16 (staggered by workgroup) also reads the host word over
-// PCIe, and the wave that sees it set copies it to the device word for the others.  Bounded
+// polls the device word; a workgroup's first wave also reads the host word over PCIe (on
+// arrival, then every SWK_STREAM_POLL-th wait) and copies it to the device word.  Bounded
 // (2^20 polls, about a second): a wave that runs out marks the chunk SWK_STREAM_ABORT in the
 // device word and in the host's abort word hflag[nsc + c].
+#ifndef SWK_STREAM_POLL
+#define SWK_STREAM_POLL 64  // streamed batches: waits between one workgroup's host-word reads
+#endif
+#ifndef SWK_STREAM_POLL_ALL
+#define SWK_STREAM_POLL_ALL 0  // 1: every wave reads the host word (round-5 form)
+#endif
 __device__ __forceinline__ uint32_t stream_mode(const uint32_t* hflag, uint32_t* dflag, int c,
                                                 int nsc, int lane) {
   for (int it = 0; it < (1 << 20); ++it) {
@@ -871,7 +877,14 @@ __device__ __forceinline__ uint32_t stream_mode(const uint32_t* hflag, uint32_t*
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       return v;
     }
-    if (((it + (int)blockIdx.x) & 15) == 0) {
+    // The host word is read over PCIe: by each workgroup's first wave only (the others follow
+    // the device word it sets), on arrival and then every SWK_STREAM_POLL-th wait, staggered over
+    // the workgroups.  Every waiting wave reading it every 16th wait (the round-5 form,
+    // SWK_STREAM_POLL_ALL=1 SWK_STREAM_POLL=16: ~600 PCIe reads a microsecond across the chip
+    // while the first chunks cross) made host calls on the headline batch 2.3-2.6 ms instead of
+    // 1.9-2.05 (same box, alternating).
+    if ((SWK_STREAM_POLL_ALL || threadIdx.x < 64) &&
+        (it == 0 || ((it + (int)blockIdx.x) % SWK_STREAM_POLL) == 0)) {
       v = __builtin_amdgcn_readfirstlane(
           __hip_atomic_load(hflag + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
       if (v) {
