@@ -975,10 +975,10 @@ extern "C" sw_status sw_bank_timing(sw_bank* b, uint64_t* launches, double* pack
     if (score_ms) *score_ms = s;
     return SW_OK;
   }
-  for (auto& ev : b->events) {
+  for (auto& ev : b->events) {  // (b == a: the launch had no separate pack interval)
     float t1 = 0, t2 = 0;
     if (st == SW_OK && hipEventSynchronize(ev.c) == hipSuccess &&
-        hipEventElapsedTime(&t1, ev.a, ev.b) == hipSuccess &&
+        (ev.b == ev.a || hipEventElapsedTime(&t1, ev.a, ev.b) == hipSuccess) &&
         hipEventElapsedTime(&t2, ev.b, ev.c) == hipSuccess) {
       p += t1;
       s += t2;
@@ -987,7 +987,7 @@ extern "C" sw_status sw_bank_timing(sw_bank* b, uint64_t* launches, double* pack
       st = fail(b, SW_ERR_HIP, "event timing failed");
     }
     (void)hipEventDestroy(ev.a);
-    (void)hipEventDestroy(ev.b);
+    if (ev.b != ev.a) (void)hipEventDestroy(ev.b);
     (void)hipEventDestroy(ev.c);
   }
   b->events.clear();
