@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
 """In-process A/B of host-buffer API configurations (sw_score_batch: host arrays in, scores
 out, gather + PCIe + kernel inside the clock), interleaved A B A B ... in ONE process so that
-the box state (the "fast" / "slow" host-memory levels DESIGN §8b records) hits every config
+the box state (the "fast" / "slow" host-memory levels LEDGER §2.2 records) hits every config
 alike.  Each config has its own bank, created and called under its environment (knobs read at
 bank creation and knobs read per call both apply).  Reports per config the median, the IQR
 (p25-p75) and the best of all calls, and the device-API rate of the same resident batch.
 
-A knob is worth keeping only when its median moves by more than the IQRs (DESIGN §8b rule).
+A knob is worth keeping only when its median moves by more than the IQRs (LEDGER §1 rule).
 
 usage: python scripts/host_ab.py [--shape ragged|uniform] [--rounds 12] [--calls 4]
                                   [--config NAME:ENV=V,ENV=V ...]

@@ -167,7 +167,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   }
   // (overlapped chunk launches run at full occupancy: with the launch thread and 6 device slots
   // they are paced by the gather and mostly run one at a time, and a half-chip kernel running
-  // alone took ~220 us per 1/8 chunk against ~175 at full occupancy)
+  // alone took ~220 us per 1/8 chunk against ~175 at full occupancy, LEDGER §1)
   Launcher* lz = b->launcher.get();
   if (lz) lz->reset();
   const auto fail_sync = [&](sw_status s) {
@@ -518,7 +518,7 @@ static sw_status batch_feed_once(sw_bank* b, const uint8_t* residues, size_t nre
     if (used) return st;
   } else if (max_len && env_int("SWBANK_STREAM_RAGGED", 0) != 0) {
     // ragged streamed (opt-in): exact, but slower than the chunked feeder on the ragged
-    // bench shape (host-side order per chunk on the gather's critical path)
+    // bench shape (host-side order per chunk on the gather's critical path; LEDGER §3.3)
     bool used = false;
     st = stream_feed(b, residues, nres, offsets, n, max_len, out, used, nullptr, lens);
     if (used) return st;
