@@ -6,7 +6,7 @@ alike.  Each config has its own bank, created and called under its environment (
 bank creation and knobs read per call both apply).  Reports per config the median, the IQR
 (p25-p75) and the best of all calls, and the device-API rate of the same resident batch.
 
-A knob is worth keeping only when its median moves by more than the IQRs (LEDGER §1 rule).
+A knob is worth keeping only when its median moves by more than the IQRs (LEDGER §2.2 rule).
 
 usage: python scripts/host_ab.py [--shape ragged|uniform] [--rounds 12] [--calls 4]
                                   [--config NAME:ENV=V,ENV=V ...]
