@@ -167,7 +167,7 @@ static sw_status feed(sw_bank* b, size_t n, const std::vector<Chunk>& chunks, Ga
   }
   // (overlapped chunk launches run at full occupancy: with the launch thread and 6 device slots
   // they are paced by the gather and mostly run one at a time, and a half-chip kernel running
-  // alone took ~220 us per 1/8 chunk against ~175 at full occupancy, LEDGER §1)
+  // alone took ~220 us per 1/8 chunk against ~175 at full occupancy, measured in round 4)
   Launcher* lz = b->launcher.get();
   if (lz) lz->reset();
   const auto fail_sync = [&](sw_status s) {
